@@ -1,0 +1,49 @@
+# Build of the MI355X reduction engine (libnccl.so, C ABI of include/nccl.h) and of the CPU oracle.
+#   make            -> nccl_amd/lib/libnccl.so  +  oracle/_build/liboracle.so
+#   make lib        -> only the product library
+#   make oracle     -> only the test oracle
+HIPCC    ?= /opt/rocm/bin/hipcc
+CXX      := /opt/rocm/lib/llvm/bin/clang++
+ARCH     ?= gfx950
+BUILD    := build
+LIBDIR   := nccl_amd/lib
+SRCDIR   := nccl_amd/csrc
+
+# -ffp-contract=off: never fuse x*s + acc into one FMA (PreMulSum parity).
+# -fno-gpu-flush-denormals-to-zero: keep fp32 denormals like the reference (no -ftz, common.mk:103).
+COMMON   := -O3 -fPIC -std=c++17 -ffp-contract=off -fvisibility=hidden -Wall -Wno-unused-function \
+            -Wno-unused-variable -Wno-unused-but-set-variable -Iinclude
+HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics
+HOSTSRC  := debug.cc bootstrap.cc transport.cc init.cc group.cc enqueue.cc
+HOSTOBJ  := $(HOSTSRC:%.cc=$(BUILD)/%.o)
+DEVOBJ   := $(BUILD)/kernels.o
+HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
+
+all: lib oracle
+
+lib: $(LIBDIR)/libnccl.so
+
+$(BUILD)/%.o: $(SRCDIR)/%.cc $(HDRS)
+	@mkdir -p $(BUILD)
+	$(CXX) $(COMMON) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c $< -o $@
+
+$(BUILD)/kernels.o: $(SRCDIR)/kernels.hip $(HDRS)
+	@mkdir -p $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIBDIR)/libnccl.so: $(HOSTOBJ) $(DEVOBJ)
+	@mkdir -p $(LIBDIR)
+	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-soname,libnccl.so.2 -Wl,-Bsymbolic \
+	  -o $@ $^ -lpthread
+	ln -sf libnccl.so $(LIBDIR)/libnccl.so.2
+
+oracle: oracle/_build/liboracle.so
+
+oracle/_build/liboracle.so: oracle/nccl_oracle.c
+	@mkdir -p oracle/_build
+	gcc -O2 -fPIC -shared -fopenmp -ffp-contract=off -fno-fast-math -std=c11 -o $@ $< -lm
+
+clean:
+	rm -rf $(BUILD) $(LIBDIR) oracle/_build
+
+.PHONY: all lib oracle clean

@@ -1,0 +1,368 @@
+"""nccl_amd — Python host mirror of the MI355X tensor-bucket reduction engine.
+
+The product is the C-ABI shared library ``nccl_amd/lib/libnccl.so`` (declared in ``include/nccl.h``,
+built from ``nccl_amd/csrc``). This module binds it with ctypes and mirrors the reference's own Python
+interface, nccl4py (``/root/reference/bindings/nccl4py/nccl/core/communicator.py``): ``get_unique_id``,
+``Communicator.init`` / ``Communicator.init_all``, ``allreduce`` / ``reduce_scatter`` / ``allgather`` /
+``reduce``, ``group()`` and ``create_pre_mul_sum``. Buffers are torch tensors on the communicator's
+device (nccl4py takes CuPy/DLPack buffers); streams are HIP streams (torch.cuda streams on ROCm).
+
+There is no fallback: if the HIP library is missing or fails to load, every entry point raises.
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import enum
+import os
+from typing import Optional, Sequence
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libnccl.so")
+
+_lib = None
+
+
+class NcclError(RuntimeError):
+    def __init__(self, code: int, where: str):
+        self.code = code
+        msg = _lib.ncclGetErrorString(code).decode() if _lib is not None else str(code)
+        last = _lib.ncclGetLastError(None).decode() if _lib is not None else ""
+        super().__init__(f"{where} failed: {msg} ({code}){': ' + last if last else ''}")
+
+
+class Result(enum.IntEnum):  # nccl.h.in:44-53
+    Success = 0
+    UnhandledCudaError = 1
+    SystemError = 2
+    InternalError = 3
+    InvalidArgument = 4
+    InvalidUsage = 5
+    RemoteError = 6
+    InProgress = 7
+    Timeout = 8
+
+
+class RedOp(enum.IntEnum):  # nccl.h.in:364-372
+    SUM = 0
+    PROD = 1
+    MAX = 2
+    MIN = 3
+    AVG = 4
+
+
+class DataType(enum.IntEnum):  # nccl.h.in:382-395
+    INT8 = 0
+    UINT8 = 1
+    INT32 = 2
+    UINT32 = 3
+    INT64 = 4
+    UINT64 = 5
+    FLOAT16 = 6
+    FLOAT32 = 7
+    FLOAT64 = 8
+    BFLOAT16 = 9
+    FLOAT8E4M3 = 10
+    FLOAT8E5M2 = 11
+
+
+SUM, PROD, MAX, MIN, AVG = RedOp.SUM, RedOp.PROD, RedOp.MAX, RedOp.MIN, RedOp.AVG
+TYPE_SIZE = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2, 10: 1, 11: 1}
+
+
+class UniqueId(ctypes.Structure):
+    _fields_ = [("internal", ctypes.c_char * 128)]
+
+
+class Config(ctypes.Structure):  # ncclConfig_t, nccl.h.in:84-108
+    _fields_ = [
+        ("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
+        ("blocking", ctypes.c_int), ("cgaClusterSize", ctypes.c_int), ("minCTAs", ctypes.c_int),
+        ("maxCTAs", ctypes.c_int), ("netName", ctypes.c_char_p), ("splitShare", ctypes.c_int),
+        ("trafficClass", ctypes.c_int), ("commName", ctypes.c_char_p), ("collnetEnable", ctypes.c_int),
+        ("CTAPolicy", ctypes.c_int), ("shrinkShare", ctypes.c_int), ("nvlsCTAs", ctypes.c_int),
+        ("nChannelsPerNetPeer", ctypes.c_int), ("nvlinkCentricSched", ctypes.c_int),
+        ("graphUsageMode", ctypes.c_int), ("numRmaCtx", ctypes.c_int), ("maxP2pPeers", ctypes.c_int),
+        ("graphStreamOrdering", ctypes.c_int),
+    ]
+
+    @classmethod
+    def default(cls, **kw) -> "Config":
+        undef = -(2 ** 31)
+        c = cls()
+        c.size = ctypes.sizeof(cls)
+        c.magic = 0xCAFEBEEF
+        c.version = get_version_code_static()
+        for name, ty in cls._fields_[3:]:
+            setattr(c, name, None if ty is ctypes.c_char_p else undef)
+        for k, v in kw.items():
+            setattr(c, k, v.encode() if isinstance(v, str) else v)
+        return c
+
+
+def get_version_code_static() -> int:
+    return 2 * 10000 + 30 * 100 + 7  # NCCL_VERSION(2,30,7)
+
+
+# Every function include/nccl.h declares (the C-ABI surface the tests check for).
+EXPORTED = [
+    "ncclMemAlloc", "ncclMemFree", "ncclGetVersion", "ncclGetUniqueId", "ncclCommInitRankConfig",
+    "ncclCommInitRank", "ncclCommInitAll", "ncclCommFinalize", "ncclCommDestroy", "ncclCommAbort",
+    "ncclGetErrorString", "ncclGetLastError", "ncclCommGetAsyncError", "ncclCommCount", "ncclCommCuDevice",
+    "ncclCommUserRank", "ncclRedOpCreatePreMulSum", "ncclRedOpDestroy", "ncclReduce", "ncclAllReduce",
+    "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
+]
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load libnccl.so (RTLD_LOCAL; the library is linked -Bsymbolic so RCCL, which torch loads, can
+    never interpose on its internal calls)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or os.environ.get("NCCL_AMD_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise RuntimeError(f"nccl_amd: HIP library {p} is missing — build it first (make, or __graft_entry__.build())")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
+    R, P, I, S, U64 = ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64
+    sig = {
+        "ncclGetVersion": (R, [ctypes.POINTER(I)]),
+        "ncclGetUniqueId": (R, [ctypes.POINTER(UniqueId)]),
+        "ncclCommInitRank": (R, [ctypes.POINTER(P), I, UniqueId, I]),
+        "ncclCommInitRankConfig": (R, [ctypes.POINTER(P), I, UniqueId, I, ctypes.POINTER(Config)]),
+        "ncclCommInitAll": (R, [ctypes.POINTER(P), I, ctypes.POINTER(I)]),
+        "ncclCommFinalize": (R, [P]),
+        "ncclCommDestroy": (R, [P]),
+        "ncclCommAbort": (R, [P]),
+        "ncclGetErrorString": (ctypes.c_char_p, [I]),
+        "ncclGetLastError": (ctypes.c_char_p, [P]),
+        "ncclCommGetAsyncError": (R, [P, ctypes.POINTER(I)]),
+        "ncclCommCount": (R, [P, ctypes.POINTER(I)]),
+        "ncclCommCuDevice": (R, [P, ctypes.POINTER(I)]),
+        "ncclCommUserRank": (R, [P, ctypes.POINTER(I)]),
+        "ncclRedOpCreatePreMulSum": (R, [ctypes.POINTER(I), P, I, I, P]),
+        "ncclRedOpDestroy": (R, [I, P]),
+        "ncclAllReduce": (R, [P, P, S, I, I, P, P]),
+        "ncclReduceScatter": (R, [P, P, S, I, I, P, P]),
+        "ncclAllGather": (R, [P, P, S, I, P, P]),
+        "ncclReduce": (R, [P, P, S, I, I, I, P, P]),
+        "ncclGroupStart": (R, []),
+        "ncclGroupEnd": (R, []),
+        "ncclMemAlloc": (R, [ctypes.POINTER(P), S]),
+        "ncclMemFree": (R, [P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(code: int, where: str) -> None:
+    if code != 0:
+        raise NcclError(code, where)
+
+
+def get_version() -> int:
+    v = ctypes.c_int()
+    _check(load().ncclGetVersion(ctypes.byref(v)), "ncclGetVersion")
+    return v.value
+
+
+def get_unique_id() -> bytes:
+    uid = UniqueId()
+    _check(load().ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+    return ctypes.string_at(ctypes.addressof(uid), 128)
+
+
+def _uid(b: bytes) -> UniqueId:
+    u = UniqueId()
+    ctypes.memmove(ctypes.byref(u), b, 128)
+    return u
+
+
+def group_start() -> None:
+    _check(load().ncclGroupStart(), "ncclGroupStart")
+
+
+def group_end() -> None:
+    _check(load().ncclGroupEnd(), "ncclGroupEnd")
+
+
+@contextlib.contextmanager
+def group():
+    group_start()
+    try:
+        yield
+    finally:
+        group_end()
+
+
+def torch_dtype_to_nccl(dtype) -> int:
+    import torch
+    m = {
+        torch.int8: 0, torch.uint8: 1, torch.int32: 2, torch.int64: 4, torch.float16: 6, torch.float32: 7,
+        torch.float64: 8, torch.bfloat16: 9,
+    }
+    for name, code in (("uint32", 3), ("uint64", 5), ("float8_e4m3fn", 10), ("float8_e5m2", 11)):
+        if hasattr(torch, name):
+            m[getattr(torch, name)] = code
+    if dtype not in m:
+        raise TypeError(f"unsupported dtype {dtype}")
+    return m[dtype]
+
+
+def _stream_ptr(stream, device: int) -> int:
+    import torch
+    if stream is None:
+        return torch.cuda.current_stream(device).cuda_stream
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+def _ptr(t) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+class Communicator:
+    """Mirror of nccl4py's Communicator (bindings/nccl4py/nccl/core/communicator.py:223)."""
+
+    def __init__(self, ptr: int):
+        self._comm = ptr
+        self._nranks = None
+        self._rank = None
+        self._device = None
+
+    # ---- construction (nccl4py Communicator.init / init_all) ----
+    @classmethod
+    def init(cls, nranks: int, rank: int, unique_id: bytes, config: Optional[Config] = None) -> "Communicator":
+        lib = load()
+        c = ctypes.c_void_p()
+        if config is None:
+            _check(lib.ncclCommInitRank(ctypes.byref(c), nranks, _uid(unique_id), rank), "ncclCommInitRank")
+        else:
+            _check(lib.ncclCommInitRankConfig(ctypes.byref(c), nranks, _uid(unique_id), rank, ctypes.byref(config)),
+                   "ncclCommInitRankConfig")
+        return cls(c.value)
+
+    @classmethod
+    def init_all(cls, devices: Sequence[int] | int) -> list["Communicator"]:
+        lib = load()
+        devs = list(range(devices)) if isinstance(devices, int) else list(devices)
+        arr = (ctypes.c_void_p * len(devs))()
+        dl = (ctypes.c_int * len(devs))(*devs)
+        _check(lib.ncclCommInitAll(arr, len(devs), dl), "ncclCommInitAll")
+        return [cls(arr[i]) for i in range(len(devs))]
+
+    # ---- properties ----
+    @property
+    def ptr(self) -> int:
+        return self._comm
+
+    @property
+    def nranks(self) -> int:
+        if self._nranks is None:
+            v = ctypes.c_int()
+            _check(load().ncclCommCount(self._comm, ctypes.byref(v)), "ncclCommCount")
+            self._nranks = v.value
+        return self._nranks
+
+    @property
+    def rank(self) -> int:
+        if self._rank is None:
+            v = ctypes.c_int()
+            _check(load().ncclCommUserRank(self._comm, ctypes.byref(v)), "ncclCommUserRank")
+            self._rank = v.value
+        return self._rank
+
+    @property
+    def device(self) -> int:
+        if self._device is None:
+            v = ctypes.c_int()
+            _check(load().ncclCommCuDevice(self._comm, ctypes.byref(v)), "ncclCommCuDevice")
+            self._device = v.value
+        return self._device
+
+    def async_error(self) -> int:
+        v = ctypes.c_int()
+        _check(load().ncclCommGetAsyncError(self._comm, ctypes.byref(v)), "ncclCommGetAsyncError")
+        return v.value
+
+    # ---- collectives on torch tensors ----
+    def allreduce(self, sendbuf, recvbuf, op=RedOp.SUM, *, stream=None) -> None:
+        if sendbuf.numel() != recvbuf.numel() or sendbuf.dtype != recvbuf.dtype:
+            raise ValueError("allreduce: sendbuf/recvbuf must match in dtype and count")
+        self.all_reduce_raw(sendbuf.data_ptr(), recvbuf.data_ptr(), sendbuf.numel(),
+                            torch_dtype_to_nccl(sendbuf.dtype), int(op), _stream_ptr(stream, self.device))
+
+    def reduce_scatter(self, sendbuf, recvbuf, op=RedOp.SUM, *, stream=None) -> None:
+        if sendbuf.numel() != recvbuf.numel() * self.nranks or sendbuf.dtype != recvbuf.dtype:
+            raise ValueError("reduce_scatter: sendbuf must hold nranks * recvbuf.numel() elements of the same dtype")
+        self.reduce_scatter_raw(sendbuf.data_ptr(), recvbuf.data_ptr(), recvbuf.numel(),
+                                torch_dtype_to_nccl(sendbuf.dtype), int(op), _stream_ptr(stream, self.device))
+
+    def allgather(self, sendbuf, recvbuf, *, stream=None) -> None:
+        if recvbuf.numel() != sendbuf.numel() * self.nranks or sendbuf.dtype != recvbuf.dtype:
+            raise ValueError("allgather: recvbuf must hold nranks * sendbuf.numel() elements of the same dtype")
+        self.all_gather_raw(sendbuf.data_ptr(), recvbuf.data_ptr(), sendbuf.numel(),
+                            torch_dtype_to_nccl(sendbuf.dtype), _stream_ptr(stream, self.device))
+
+    def reduce(self, sendbuf, recvbuf, op=RedOp.SUM, root: int = 0, *, stream=None) -> None:
+        self.reduce_raw(sendbuf.data_ptr(), _ptr(recvbuf), sendbuf.numel(), torch_dtype_to_nccl(sendbuf.dtype),
+                        int(op), root, _stream_ptr(stream, self.device))
+
+    # ---- collectives on raw device pointers (the C ABI one-to-one) ----
+    def all_reduce_raw(self, send: int, recv: int, count: int, dtype: int, op: int, stream: int) -> None:
+        _check(load().ncclAllReduce(send, recv, count, dtype, op, self._comm, stream), "ncclAllReduce")
+
+    def reduce_scatter_raw(self, send: int, recv: int, recvcount: int, dtype: int, op: int, stream: int) -> None:
+        _check(load().ncclReduceScatter(send, recv, recvcount, dtype, op, self._comm, stream), "ncclReduceScatter")
+
+    def all_gather_raw(self, send: int, recv: int, sendcount: int, dtype: int, stream: int) -> None:
+        _check(load().ncclAllGather(send, recv, sendcount, dtype, self._comm, stream), "ncclAllGather")
+
+    def reduce_raw(self, send: int, recv: Optional[int], count: int, dtype: int, op: int, root: int,
+                   stream: int) -> None:
+        _check(load().ncclReduce(send, recv, count, dtype, op, root, self._comm, stream), "ncclReduce")
+
+    # ---- custom operators ----
+    def create_pre_mul_sum(self, scalar, dtype: int, device_scalar_ptr: Optional[int] = None) -> int:
+        """ncclRedOpCreatePreMulSum; `scalar` is a host value (ncclScalarHostImmediate) unless
+        `device_scalar_ptr` is given (ncclScalarDevice)."""
+        import numpy as np
+        op = ctypes.c_int()
+        if device_scalar_ptr is not None:
+            _check(load().ncclRedOpCreatePreMulSum(ctypes.byref(op), device_scalar_ptr, dtype, 0, self._comm),
+                   "ncclRedOpCreatePreMulSum")
+        else:
+            npdt = {0: np.int8, 1: np.uint8, 2: np.int32, 3: np.uint32, 4: np.int64, 5: np.uint64, 6: np.float16,
+                    7: np.float32, 8: np.float64}.get(dtype)
+            if npdt is not None:
+                buf = np.array([scalar], dtype=npdt).tobytes()
+            else:  # bf16 / fp8: caller passes the raw bit pattern as an int
+                buf = int(scalar).to_bytes(TYPE_SIZE[dtype], "little")
+            cbuf = ctypes.create_string_buffer(buf, 8)
+            _check(load().ncclRedOpCreatePreMulSum(ctypes.byref(op), cbuf, dtype, 1, self._comm),
+                   "ncclRedOpCreatePreMulSum")
+        return op.value
+
+    def destroy_op(self, op: int) -> None:
+        _check(load().ncclRedOpDestroy(op, self._comm), "ncclRedOpDestroy")
+
+    # ---- teardown ----
+    def finalize(self) -> None:
+        _check(load().ncclCommFinalize(self._comm), "ncclCommFinalize")
+
+    def destroy(self) -> None:
+        if self._comm:
+            _check(load().ncclCommDestroy(self._comm), "ncclCommDestroy")
+            self._comm = 0
+
+    def abort(self) -> None:
+        if self._comm:
+            _check(load().ncclCommAbort(self._comm), "ncclCommAbort")
+            self._comm = 0

@@ -1,0 +1,196 @@
+// core.h — internal definitions of the MI355X reduction engine (host side).
+//
+// Layer map (reference SURVEY.md §1): L7 public API (api.cc) → L5 enqueue/group (enqueue.cc, group.cc)
+// → L6 device kernels (kernels.hip) over L3 peer-mapped staging (transport.cc) set up by
+// L4 init (init.cc) using the L1 TCP bootstrap (bootstrap.cc). L0 = debug.cc / param.cc.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <functional>
+#include <cstdint>
+#include <cstdio>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/nccl.h"
+#include "device_abi.h"
+
+#define NCCL_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace ncclamd {
+
+// ---------------------------------------------------------------- logging (reference src/debug.cc)
+enum LogLevel { LOG_NONE = 0, LOG_VERSION = 1, LOG_WARN = 2, LOG_INFO = 3, LOG_ABORT = 4, LOG_TRACE = 5 };
+void logInit();
+extern int gLogLevel;
+void logMessage(int level, const char* file, int line, const char* fmt, ...) __attribute__((format(printf, 4, 5)));
+void setLastError(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+const char* lastError();
+
+#define WARN(...) ::ncclamd::logMessage(::ncclamd::LOG_WARN, __FILE__, __LINE__, __VA_ARGS__)
+#define INFO(...)                                                                         \
+  do {                                                                                    \
+    if (::ncclamd::gLogLevel >= ::ncclamd::LOG_INFO)                                      \
+      ::ncclamd::logMessage(::ncclamd::LOG_INFO, __FILE__, __LINE__, __VA_ARGS__);        \
+  } while (0)
+#define TRACE(...)                                                                        \
+  do {                                                                                    \
+    if (::ncclamd::gLogLevel >= ::ncclamd::LOG_TRACE)                                     \
+      ::ncclamd::logMessage(::ncclamd::LOG_TRACE, __FILE__, __LINE__, __VA_ARGS__);       \
+  } while (0)
+
+#define NCCLCHECK(call)                                   \
+  do {                                                    \
+    ncclResult_t _r = (call);                             \
+    if (_r != ncclSuccess && _r != ncclInProgress) {      \
+      INFO("%s:%d -> %d", __FILE__, __LINE__, (int)_r);   \
+      return _r;                                          \
+    }                                                     \
+  } while (0)
+
+#define HIPCHECK(call)                                                           \
+  do {                                                                           \
+    hipError_t _e = (call);                                                      \
+    if (_e != hipSuccess) {                                                      \
+      WARN("HIP failure '%s' at %s", hipGetErrorString(_e), #call);              \
+      return ncclUnhandledCudaError;                                             \
+    }                                                                            \
+  } while (0)
+
+#define SYSCHECK(cond, what)                                                     \
+  do {                                                                           \
+    if (!(cond)) {                                                               \
+      WARN("system error in %s: %s", what, strerror(errno));                     \
+      return ncclSystemError;                                                    \
+    }                                                                            \
+  } while (0)
+
+// ---------------------------------------------------------------- params (reference src/misc/param.cc)
+int64_t paramInt(const char* name, int64_t deflt);
+const char* paramStr(const char* name);  // nullptr when unset
+
+// ---------------------------------------------------------------- bootstrap (reference src/bootstrap.cc)
+struct Bootstrap;
+ncclResult_t bootstrapGetUniqueId(ncclUniqueId* id);
+ncclResult_t bootstrapInit(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out);
+ncclResult_t bootstrapAllGather(Bootstrap* b, void* data, size_t bytesPerRank);
+ncclResult_t bootstrapBarrier(Bootstrap* b);
+void bootstrapClose(Bootstrap* b);
+
+// ---------------------------------------------------------------- communicator (reference src/include/comm.h)
+constexpr uint64_t kCommMagic = 0x4d493335584e4343ull;  // "MI35XNCC"
+
+struct PeerInfo {  // exchanged once at init (reference: struct ncclPeerInfo, src/init.cc:1035-1037)
+  int rank;
+  int device;
+  int pid;
+  uint64_t hostHash;
+  char busId[32];
+  hipIpcMemHandle_t stagingHandle;
+  hipIpcMemHandle_t flagsHandle;
+  uint64_t stagingPtr;  // raw pointers, valid only inside the same process
+  uint64_t flagsPtr;
+};
+
+struct UserRedOp {  // ncclRedOpCreatePreMulSum state (reference src/enqueue.cc:2560-2576)
+  bool used;
+  ncclDataType_t datatype;
+  int devOp;
+  uint64_t scalarArg;      // immediate scalar bits
+  const void* scalarPtr;   // device scalar (ncclScalarDevice), read by the kernel
+};
+
+struct ncclCommImpl;
+}  // namespace ncclamd
+
+// The opaque handle type of the public header.
+struct ncclComm {
+  uint64_t startMagic;
+  int rank, nRanks, device;
+  bool blocking;
+  int minCTAs, maxCTAs;
+  std::string commName;
+
+  ncclamd::Bootstrap* bootstrap = nullptr;
+  std::vector<ncclamd::PeerInfo> peers;
+
+  // Device resources (transport.cc)
+  void* staging = nullptr;          // local uncached staging area [ch][kind][slot][from][slotBytes]
+  uint64_t* flags = nullptr;        // local uncached flag words [ch][flagKind][from]
+  uint64_t* counters = nullptr;     // local connection step counters [ch][ctrKind][peer]
+  void* peerStaging[NCCL_AMD_MAX_RANKS] = {};
+  uint64_t* peerFlags[NCCL_AMD_MAX_RANKS] = {};
+  bool peerIsIpc[NCCL_AMD_MAX_RANKS] = {};
+  ncclamd::DevComm* devComm = nullptr;  // device copy of the DevComm struct
+  ncclamd::DevComm hostDevComm;          // host mirror
+  uint32_t* hostAbort = nullptr;         // pinned, mapped: host→device abort flag
+  uint32_t* hostError = nullptr;         // pinned, mapped: device→host error word
+  size_t slotBytes = 0;
+  int nSlots = 0;
+  int maxChannels = 0;
+  hipStream_t internalStream = nullptr;
+
+  std::vector<ncclamd::UserRedOp> userOps;
+  std::atomic<int> asyncResult{ncclSuccess};
+  bool finalized = false;
+  bool destroyed = false;
+  uint64_t opCount = 0;
+  uint64_t endMagic;
+};
+
+namespace ncclamd {
+
+ncclResult_t commCheck(const ncclComm* comm, const char* opname, const char* what);
+ncclResult_t transportSetup(ncclComm* comm);     // allocate staging/flags + IPC export
+ncclResult_t transportConnect(ncclComm* comm);   // map peers after the PeerInfo exchange
+ncclResult_t transportFree(ncclComm* comm);
+ncclResult_t commAllocDevState(ncclComm* comm);  // counters, DevComm upload, abort/error words
+
+// ---------------------------------------------------------------- enqueue (reference src/enqueue.cc)
+enum CollFunc { FUNC_ALLREDUCE = 0, FUNC_REDUCESCATTER = 1, FUNC_ALLGATHER = 2, FUNC_REDUCE = 3 };
+
+struct CollInfo {  // reference: struct ncclInfo, src/include/info.h:17-41
+  CollFunc func;
+  const char* opName;
+  const void* sendbuff;
+  void* recvbuff;
+  size_t count;
+  ncclDataType_t datatype;
+  ncclRedOp_t op;
+  int root;
+  ncclComm* comm;
+  hipStream_t stream;
+};
+
+enum Algo { ALGO_COPY = 0, ALGO_ONERANK = 1, ALGO_DIRECT = 2 };
+
+struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src/include/comm.h)
+  CollFunc func;
+  int algo;
+  ncclDataType_t datatype;
+  int eltSize;
+  int devOp;
+  int nChannels;
+  size_t bytes;
+  hipStream_t stream;
+  CollArgs args;
+};
+
+ncclResult_t enqueueCheck(CollInfo* info);
+ncclResult_t launchColl(const CollInfo& info);  // plan + launch (enqueue.cc)
+ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
+ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream);
+int typeSize(ncclDataType_t t);
+
+// ---------------------------------------------------------------- groups (reference src/group.cc)
+ncclResult_t groupStartInternal();
+ncclResult_t groupEndInternal();
+bool groupActive();
+void groupRecordError(ncclResult_t r);
+ncclResult_t groupDeferColl(const CollInfo& info);
+ncclResult_t groupDeferInit(std::function<ncclResult_t()> job);
+
+}  // namespace ncclamd

@@ -1,0 +1,156 @@
+// debug.cc — NCCL_DEBUG / NCCL_DEBUG_FILE logging, last-error buffer and NCCL_* parameter lookup.
+//
+// Reference behaviour: src/debug.cc:45-132 (levels VERSION/WARN/INFO/ABORT/TRACE, NCCL_DEBUG_FILE with
+// %h/%p substitution), src/init.cc:3415-3443 (ncclGetLastError returns the last WARN text),
+// src/misc/param.cc:54-111 (env first, then NCCL_CONF_FILE, ~/.nccl.conf, /etc/nccl.conf).
+#include <errno.h>
+#include <stdarg.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "core.h"
+
+namespace ncclamd {
+
+int gLogLevel = -1;
+static FILE* gLogFile = stderr;
+static std::mutex gLogMutex;
+static char gLastError[1024] = "";
+static std::once_flag gLogOnce;
+
+static void logInitOnce() {
+  const char* lvl = getenv("NCCL_DEBUG");
+  int level = LOG_NONE;
+  if (lvl) {
+    if (!strcasecmp(lvl, "VERSION")) level = LOG_VERSION;
+    else if (!strcasecmp(lvl, "WARN")) level = LOG_WARN;
+    else if (!strcasecmp(lvl, "INFO")) level = LOG_INFO;
+    else if (!strcasecmp(lvl, "ABORT")) level = LOG_ABORT;
+    else if (!strcasecmp(lvl, "TRACE")) level = LOG_TRACE;
+  }
+  const char* file = getenv("NCCL_DEBUG_FILE");
+  if (file && level > LOG_NONE) {
+    char path[4096];
+    int o = 0;
+    char host[256] = "";
+    gethostname(host, sizeof(host) - 1);
+    for (const char* p = file; *p && o < (int)sizeof(path) - 64; p++) {
+      if (p[0] == '%' && p[1] == 'h') { o += snprintf(path + o, sizeof(path) - o, "%s", host); p++; }
+      else if (p[0] == '%' && p[1] == 'p') { o += snprintf(path + o, sizeof(path) - o, "%d", getpid()); p++; }
+      else path[o++] = *p;
+    }
+    path[o] = 0;
+    FILE* f = fopen(path, "w");
+    if (f) { setvbuf(f, nullptr, _IOLBF, 0); gLogFile = f; }
+  }
+  gLogLevel = level;
+}
+
+void logInit() { std::call_once(gLogOnce, logInitOnce); }
+
+static const char* levelName(int l) {
+  switch (l) {
+    case LOG_WARN: return "WARN";
+    case LOG_INFO: return "INFO";
+    case LOG_TRACE: return "TRACE";
+    default: return "";
+  }
+}
+
+void logMessage(int level, const char* file, int line, const char* fmt, ...) {
+  logInit();
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  if (level == LOG_WARN) {
+    std::lock_guard<std::mutex> g(gLogMutex);
+    snprintf(gLastError, sizeof(gLastError), "%s", buf);
+  }
+  if (gLogLevel < level) return;
+  char host[64] = "";
+  gethostname(host, sizeof(host) - 1);
+  std::lock_guard<std::mutex> g(gLogMutex);
+  if (level == LOG_WARN)
+    fprintf(gLogFile, "%s:%d:%ld [%s] %s:%d NCCL %s %s\n", host, getpid(), (long)syscall(SYS_gettid),
+            "mi355x", file, line, levelName(level), buf);
+  else
+    fprintf(gLogFile, "%s:%d:%ld NCCL %s %s\n", host, getpid(), (long)syscall(SYS_gettid), levelName(level), buf);
+}
+
+void setLastError(const char* fmt, ...) {
+  std::lock_guard<std::mutex> g(gLogMutex);
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(gLastError, sizeof(gLastError), fmt, ap);
+  va_end(ap);
+}
+
+const char* lastError() { return gLastError; }
+
+// ---------------------------------------------------------------- parameters
+static std::map<std::string, std::string>* gConf = nullptr;
+static std::once_flag gConfOnce;
+
+static void loadConfFile(const char* path) {
+  FILE* f = fopen(path, "r");
+  if (!f) return;
+  char line[1024];
+  while (fgets(line, sizeof(line), f)) {
+    char* s = line;
+    while (*s == ' ' || *s == '\t') s++;
+    if (*s == '#' || *s == '\n' || !*s) continue;
+    char* eq = strchr(s, '=');
+    if (!eq) continue;
+    *eq = 0;
+    char* v = eq + 1;
+    char* end = v + strlen(v);
+    while (end > v && (end[-1] == '\n' || end[-1] == ' ' || end[-1] == '\r')) *--end = 0;
+    char* kend = eq;
+    while (kend > s && (kend[-1] == ' ' || kend[-1] == '\t')) *--kend = 0;
+    if (!gConf->count(s)) (*gConf)[s] = v;  // first file wins, env overrides all
+  }
+  fclose(f);
+}
+
+static void confInit() {
+  gConf = new std::map<std::string, std::string>();
+  const char* userFile = getenv("NCCL_CONF_FILE");
+  if (userFile) loadConfFile(userFile);
+  const char* home = getenv("HOME");
+  if (home) {
+    std::string p = std::string(home) + "/.nccl.conf";
+    loadConfFile(p.c_str());
+  }
+  loadConfFile("/etc/nccl.conf");
+}
+
+const char* paramStr(const char* name) {
+  const char* v = getenv(name);
+  if (v) return v;
+  std::call_once(gConfOnce, confInit);
+  auto it = gConf->find(name);
+  return it == gConf->end() ? nullptr : it->second.c_str();
+}
+
+int64_t paramInt(const char* name, int64_t deflt) {
+  const char* v = paramStr(name);
+  if (!v || !*v) return deflt;
+  errno = 0;
+  char* end = nullptr;
+  long long x = strtoll(v, &end, 0);
+  if (errno || end == v) {
+    WARN("Invalid value %s for %s, using default %lld", v, name, (long long)deflt);
+    return deflt;
+  }
+  return x;
+}
+
+}  // namespace ncclamd

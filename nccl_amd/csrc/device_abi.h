@@ -1,0 +1,79 @@
+// device_abi.h — data layout shared by the host runtime and the gfx950 kernels.
+//
+// HBM layout per rank (all offsets in bytes, every region 16-byte aligned):
+//
+//   staging  (hipExtMallocWithFlags(..., hipDeviceMallocUncached), exported by HIP IPC)
+//     [channel c < maxChannels][kind k < 2 (RS, AG)][slot s < nSlots][from < nRanks][slotBytes]
+//     Written ONLY by peer `from` over xGMI (remote write-through stores); read ONLY by the owner.
+//
+//   flags    (uncached, exported by HIP IPC)
+//     uint64 [channel][flag kind < 4][from < NCCL_AMD_MAX_RANKS]
+//       RS_READY[c][from]  = number of RS slices `from` has written into my staging (monotonic)
+//       RS_ACK[c][from]    = number of my RS slices `from` has consumed from ITS staging
+//       AG_READY / AG_ACK  = the same for the all-gather direction
+//     A word is written by exactly one remote rank and polled only by its owner.
+//
+//   counters (plain device memory, local)
+//     uint64 [channel][ctr kind < 4 (sendRS, recvRS, sendAG, recvAG)][peer < NCCL_AMD_MAX_RANKS]
+//     Per-connection step counters (reference: conn->step, src/device/prims_simple.h:100-173),
+//     kept in device memory so a captured hipGraph replays correctly.
+#pragma once
+#include <stdint.h>
+
+#define NCCL_AMD_MAX_RANKS 16
+#define NCCL_AMD_MAX_CHANNELS 128
+
+namespace ncclamd {
+
+enum StagingKind { STG_RS = 0, STG_AG = 1, STG_KINDS = 2 };
+enum FlagKind { FLG_RS_READY = 0, FLG_RS_ACK = 1, FLG_AG_READY = 2, FLG_AG_ACK = 3, FLG_KINDS = 4 };
+enum CtrKind { CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_KINDS = 4 };
+
+// Device reduction kinds (reference ncclDevRedOp_t subset, src/include/device.h)
+enum DevRedOp { DEV_SUM = 0, DEV_PROD = 1, DEV_MINMAX = 2, DEV_PREMULSUM = 3, DEV_SUMPOSTDIV = 4, DEV_NUMOPS = 5 };
+
+// Error codes written by a kernel into the host-visible error word.
+enum DevError { DERR_NONE = 0, DERR_TIMEOUT = 1, DERR_ABORT = 2 };
+
+struct DevComm {
+  int rank;
+  int nRanks;
+  int nSlots;
+  int maxChannels;
+  uint64_t slotBytes;
+  uint64_t timeoutTicks;  // s_memrealtime ticks (100 MHz) before a spin gives up
+  char* staging[NCCL_AMD_MAX_RANKS];     // every rank's staging base as mapped here
+  uint64_t* flags[NCCL_AMD_MAX_RANKS];   // every rank's flag block as mapped here
+  uint64_t* counters;                    // local step counters
+  uint32_t* abortFlag;                   // host-pinned; nonzero = abort
+  uint32_t* errorWord;                   // host-pinned; first DevError recorded
+};
+
+// Kernel argument block (passed by value, < 4 KiB like the reference's ncclDevKernelArgs4K,
+// src/device/common.h:435-449).
+struct CollArgs {
+  const void* sendbuff;
+  void* recvbuff;
+  const DevComm* comm;
+  uint64_t count;      // AR/Reduce: elements; RS: recvcount; AG: sendcount (bytes for AG)
+  uint64_t chunk;      // elements per rank block (AR: alignUp(divUp(count,n),EPP); RS/AG: count)
+  uint64_t part;       // elements per channel within a rank block
+  uint64_t slice;      // elements per pipeline step (per peer)
+  uint64_t redArg;     // scalar / xormask / divisor bits
+  const void* redArgPtr;  // device scalar (PreMulSum with ncclScalarDevice), else nullptr
+  int nSteps;
+  int root;
+  int aligned;         // send/recv base pointers are 16-byte aligned
+};
+
+__host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int kind, int slot, int from) {
+  return ((((uint64_t)c * STG_KINDS + kind) * dc.nSlots + slot) * dc.nRanks + from) * dc.slotBytes;
+}
+__host__ __device__ inline uint64_t flagIndex(int c, int kind, int from) {
+  return ((uint64_t)c * FLG_KINDS + kind) * NCCL_AMD_MAX_RANKS + from;
+}
+__host__ __device__ inline uint64_t ctrIndex(int c, int kind, int peer) {
+  return ((uint64_t)c * CTR_KINDS + kind) * NCCL_AMD_MAX_RANKS + peer;
+}
+
+}  // namespace ncclamd

@@ -1,0 +1,299 @@
+// enqueue.cc — collective entry points, argument checks, op mapping, algorithm/channel choice, launch.
+//
+// Reference: src/collectives.cc:129-256 (entry points build ncclInfo), src/enqueue.cc:3124-3172
+// (ncclEnqueueCheck: CommCheck → implicit group → ArgsCheck → taskAppend), :3014-3122 (taskAppend:
+// count==0 no-op, nRanks==1 → ncclLaunchOneRank), :2479-2583 (hostToDevRedOp), src/misc/argcheck.cc:
+// 12-45, 201-254 (pointer / comm / argument checks), src/graph/tuning.cc (algorithm cost model —
+// replaced by the small MI355X table in choosePlan()).
+#include <string.h>
+
+#include "core.h"
+
+namespace ncclamd {
+
+int typeSize(ncclDataType_t t) {
+  switch (t) {
+    case ncclInt8: case ncclUint8: case ncclFloat8e4m3: case ncclFloat8e5m2: return 1;
+    case ncclFloat16: case ncclBfloat16: return 2;
+    case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+    case ncclInt64: case ncclUint64: case ncclFloat64: return 8;
+    default: return -1;
+  }
+}
+
+static uint16_t hostF32ToHalf(float f);
+static uint16_t hostF32ToBf16(float f);
+static uint8_t hostF32ToFp8(float f, bool e5m2);
+
+// hostToDevRedOp (reference src/enqueue.cc:2479-2583).
+static ncclResult_t hostToDevRedOp(ncclComm* comm, ncclRedOp_t op, ncclDataType_t dt, int* devOp,
+                                   uint64_t* arg, const void** argPtr) {
+  int nbits = 8 * typeSize(dt);
+  if (nbits <= 0) return ncclInvalidArgument;
+  uint64_t allBits = nbits == 64 ? ~0ull : ((1ull << nbits) - 1);
+  uint64_t signBit = allBits ^ (allBits >> 1);
+  *arg = 0;
+  *argPtr = nullptr;
+  switch ((int)op) {
+    case ncclSum: *devOp = DEV_SUM; return ncclSuccess;
+    case ncclProd: *devOp = DEV_PROD; return ncclSuccess;
+    case ncclMin:
+    case ncclMax:
+      *devOp = DEV_MINMAX;
+      if (dt == ncclInt8 || dt == ncclInt32 || dt == ncclInt64) *arg ^= signBit;
+      if (op == ncclMax) *arg ^= allBits;
+      return ncclSuccess;
+    case ncclAvg: {
+      int n = comm->nRanks;
+      switch (dt) {
+        case ncclInt8: case ncclInt32: case ncclInt64:
+          *devOp = DEV_SUMPOSTDIV; *arg = ((uint64_t)n << 1) | 1; return ncclSuccess;
+        case ncclUint8: case ncclUint32: case ncclUint64:
+          *devOp = DEV_SUMPOSTDIV; *arg = (uint64_t)n << 1; return ncclSuccess;
+        case ncclFloat16: *devOp = DEV_PREMULSUM; *arg = hostF32ToHalf((float)(1.0 / n)); return ncclSuccess;
+        case ncclBfloat16: *devOp = DEV_PREMULSUM; *arg = hostF32ToBf16((float)(1.0 / n)); return ncclSuccess;
+        case ncclFloat8e4m3: *devOp = DEV_PREMULSUM; *arg = hostF32ToFp8((float)(1.0 / n), false); return ncclSuccess;
+        case ncclFloat8e5m2: *devOp = DEV_PREMULSUM; *arg = hostF32ToFp8((float)(1.0 / n), true); return ncclSuccess;
+        case ncclFloat32: { float s = (float)(1.0 / n); *devOp = DEV_PREMULSUM; memcpy(arg, &s, 4); return ncclSuccess; }
+        case ncclFloat64: { double s = 1.0 / n; *devOp = DEV_PREMULSUM; memcpy(arg, &s, 8); return ncclSuccess; }
+        default: return ncclInvalidArgument;
+      }
+    }
+    default: {
+      int ix = (int)op - (int)ncclNumOps;
+      const UserRedOp& u = comm->userOps[ix];
+      if (dt != u.datatype) {
+        WARN("Data type supplied to user-created ncclRedOp_t does not match type given to reduction operation");
+        return ncclInvalidArgument;
+      }
+      *devOp = u.devOp;
+      *arg = u.scalarArg;
+      *argPtr = u.scalarPtr;
+      return ncclSuccess;
+    }
+  }
+}
+
+// Pointer check (reference argcheck.cc:12-28), active with NCCL_CHECK_POINTERS=1.
+static ncclResult_t ptrCheck(const void* p, ncclComm* comm, const char* name, const char* opname) {
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess || attr.devicePointer == nullptr) {
+    (void)hipGetLastError();
+    WARN("%s : %s %p is not a valid pointer", opname, name, p);
+    return ncclInvalidArgument;
+  }
+  if (attr.type == hipMemoryTypeDevice && attr.device != comm->device) {
+    WARN("%s : %s allocated on device %d mismatchs with NCCL device %d", opname, name, attr.device, comm->device);
+    return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
+// ArgsCheck (reference argcheck.cc:201-254).
+static ncclResult_t argsCheck(CollInfo* info) {
+  ncclComm* comm = info->comm;
+  if (info->root < 0 || info->root >= comm->nRanks) {
+    WARN("%s : invalid root %d (root should be in the 0..%d range)", info->opName, info->root, comm->nRanks);
+    return ncclInvalidArgument;
+  }
+  if (info->datatype < 0 || info->datatype >= ncclNumTypes) {
+    WARN("%s : invalid type %d", info->opName, info->datatype);
+    return ncclInvalidArgument;
+  }
+  if (info->op < 0 || ncclMaxRedOp < info->op) {
+    WARN("%s : invalid reduction operation %d", info->opName, info->op);
+    return ncclInvalidArgument;
+  }
+  int opIx = (int)info->op - (int)ncclNumOps;
+  if (ncclNumOps <= info->op && (opIx >= (int)comm->userOps.size() || !comm->userOps[opIx].used)) {
+    WARN("%s : reduction operation %d unknown to this communicator", info->opName, info->op);
+    return ncclInvalidArgument;
+  }
+  if (paramInt("NCCL_CHECK_POINTERS", 0) && info->count > 0) {
+    NCCLCHECK(ptrCheck(info->sendbuff, comm, "sendbuff", info->opName));
+    if (info->func != FUNC_REDUCE || comm->rank == info->root)
+      NCCLCHECK(ptrCheck(info->recvbuff, comm, "recvbuff", info->opName));
+  }
+  return ncclSuccess;
+}
+
+// ---- algorithm / channel choice (reference tuning.cc:243-400, enqueue.cc:2028-2180, 576-857) ----
+// One node, full xGMI mesh: the only algorithm is the direct scatter-reduce-gather; what is tuned is
+// the channel (workgroup) count and the pipeline slice. Every rank computes the same plan from the
+// same (count, type, nRanks, params), which the protocol requires.
+static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchPlan& p) {
+  const size_t minPart = (size_t)paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
+  int nch = (int)((blockBytes + minPart - 1) / minPart);
+  if (nch < comm->minCTAs) nch = comm->minCTAs;
+  if (nch > comm->maxChannels) nch = comm->maxChannels;
+  if (nch < 1) nch = 1;
+  const uint64_t epp = 16 / eltSize;
+  uint64_t blockElems = blockBytes / eltSize;
+  uint64_t part = (blockElems + nch - 1) / nch;
+  part = (part + epp - 1) / epp * epp;
+  if (part == 0) part = epp;
+  uint64_t slice = comm->slotBytes / eltSize;
+  slice = slice / epp * epp;
+  if (slice > part) slice = part;
+  p.nChannels = nch;
+  p.args.part = part;
+  p.args.slice = slice;
+  p.args.nSteps = (int)((part + slice - 1) / slice);
+}
+
+ncclResult_t launchColl(const CollInfo& info) {
+  ncclComm* comm = info.comm;
+  HIPCHECK(hipSetDevice(comm->device));
+  const int ts = typeSize(info.datatype);
+  LaunchPlan p;
+  memset(&p, 0, sizeof(p));
+  p.func = info.func;
+  p.datatype = info.datatype;
+  p.eltSize = ts;
+  p.stream = info.stream;
+  p.args.sendbuff = info.sendbuff;
+  p.args.recvbuff = info.recvbuff;
+  p.args.comm = comm->devComm;
+  p.args.root = info.root;
+  const void* argPtr = nullptr;
+  if (info.func != FUNC_ALLGATHER) {
+    NCCLCHECK(hostToDevRedOp(comm, info.op, info.datatype, &p.devOp, &p.args.redArg, &argPtr));
+    p.args.redArgPtr = argPtr;
+  }
+  const int n = comm->nRanks;
+  comm->opCount++;
+
+  if (n == 1) {
+    // reference taskAppend → ncclLaunchOneRank (enqueue.cc:3039-3041, onerank.cu:49-110)
+    size_t bytes = info.count * (size_t)ts;
+    if (info.func == FUNC_REDUCE && info.recvbuff == nullptr) return ncclSuccess;
+    if (p.devOp == DEV_PREMULSUM) {
+      p.algo = ALGO_ONERANK;
+      p.args.count = info.count;
+      return launchPlan(p);
+    }
+    p.algo = ALGO_COPY;
+    p.bytes = bytes;
+    return launchPlan(p);
+  }
+
+  p.algo = ALGO_DIRECT;
+  const uint64_t epp = 16 / ts;
+  size_t count = info.count;
+  uint64_t blockElems;
+  switch (info.func) {
+    case FUNC_ALLREDUCE:
+    case FUNC_REDUCE:
+      // rank block = alignUp(divUp(count, n), 16/sizeof(T)) (reference all_reduce.h:38)
+      blockElems = (count + n - 1) / n;
+      blockElems = (blockElems + epp - 1) / epp * epp;
+      break;
+    default:  // RS: recvcount, AG: sendcount
+      blockElems = count;
+      break;
+  }
+  p.args.count = count;
+  p.args.chunk = blockElems;
+  uintptr_t bases = (uintptr_t)info.sendbuff | (uintptr_t)info.recvbuff;
+  bool aligned = (bases & 15) == 0;
+  if (info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER) aligned = aligned && ((count * ts) & 15) == 0;
+  p.args.aligned = aligned ? 1 : 0;
+  planChannels(comm, blockElems * ts, ts, p);
+  TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
+        (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,
+        p.args.nSteps, p.args.aligned);
+  return launchPlan(p);
+}
+
+ncclResult_t enqueueCheck(CollInfo* info) {
+  logInit();
+  ncclResult_t ret = commCheck(info->comm, info->opName, "comm");
+  if (ret != ncclSuccess) {
+    groupRecordError(ret);
+    return ret;
+  }
+  ret = argsCheck(info);
+  if (ret == ncclSuccess && info->comm->asyncResult.load() != ncclSuccess) {
+    WARN("%s: communicator is in error state %d", info->opName, info->comm->asyncResult.load());
+    ret = ncclInvalidUsage;
+  }
+  if (ret != ncclSuccess) {
+    groupRecordError(ret);
+    return ret;
+  }
+  INFO("%s: opCount %lx sendbuff %p recvbuff %p count %zu datatype %d op %d root %d comm %p [nranks=%d] stream %p",
+       info->opName, (unsigned long)info->comm->opCount, info->sendbuff, info->recvbuff, info->count,
+       (int)info->datatype, (int)info->op, info->root, (void*)info->comm, info->comm->nRanks, (void*)info->stream);
+  if (info->count == 0) return ncclSuccess;  // reference enqueue.cc:3024
+  if (groupActive()) return groupDeferColl(*info);
+  return launchColl(*info);
+}
+
+// ---- small host conversions for the avg scalar ----
+static uint16_t hostF32ToHalf(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+static uint16_t hostF32ToBf16(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1);
+  return (uint16_t)(u >> 16);
+}
+static uint8_t hostF32ToFp8(float f, bool e5m2) {
+  // 1/n for n in 1..16 is well inside both fp8 ranges: round via half, then RNE to 3/2 mantissa bits
+  float h = (float)(_Float16)f;
+  uint32_t u;
+  memcpy(&u, &h, 4);
+  int mbits = e5m2 ? 2 : 3, bias = e5m2 ? 15 : 7;
+  int e = (int)((u >> 23) & 0xff) - 127;
+  uint32_t man = u & 0x7fffff;
+  if (e < 1 - bias) {  // subnormal fp8
+    float q = h * (e5m2 ? 65536.0f : 512.0f);
+    uint32_t qi = (uint32_t)q;
+    float fr = q - (float)qi;
+    if (fr > 0.5f || (fr == 0.5f && (qi & 1))) qi++;
+    return (uint8_t)qi;
+  }
+  uint32_t code = ((uint32_t)(e + bias) << mbits) | (man >> (23 - mbits));
+  uint32_t rem = man & ((1u << (23 - mbits)) - 1), halfway = 1u << (22 - mbits);
+  if (rem > halfway || (rem == halfway && (code & 1))) code++;
+  return (uint8_t)code;
+}
+
+}  // namespace ncclamd
+
+using namespace ncclamd;
+
+#define NCCL_ALIAS(ret, name, ...) extern "C" __attribute__((visibility("default"), alias(#name))) ret p##name(__VA_ARGS__);
+
+NCCL_EXPORT ncclResult_t ncclAllReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                       ncclRedOp_t op, ncclComm_t comm, hipStream_t stream) {
+  CollInfo info = {FUNC_ALLREDUCE, "AllReduce", sendbuff, recvbuff, count, datatype, op, 0, comm, stream};
+  return enqueueCheck(&info);
+}
+NCCL_ALIAS(ncclResult_t, ncclAllReduce, const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+           hipStream_t)
+
+NCCL_EXPORT ncclResult_t ncclReduceScatter(const void* sendbuff, void* recvbuff, size_t recvcount,
+                                           ncclDataType_t datatype, ncclRedOp_t op, ncclComm_t comm,
+                                           hipStream_t stream) {
+  CollInfo info = {FUNC_REDUCESCATTER, "ReduceScatter", sendbuff, recvbuff, recvcount, datatype, op, 0, comm, stream};
+  return enqueueCheck(&info);
+}
+NCCL_ALIAS(ncclResult_t, ncclReduceScatter, const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+           hipStream_t)
+
+NCCL_EXPORT ncclResult_t ncclAllGather(const void* sendbuff, void* recvbuff, size_t sendcount,
+                                       ncclDataType_t datatype, ncclComm_t comm, hipStream_t stream) {
+  CollInfo info = {FUNC_ALLGATHER, "AllGather", sendbuff, recvbuff, sendcount, datatype, ncclSum, 0, comm, stream};
+  return enqueueCheck(&info);
+}
+NCCL_ALIAS(ncclResult_t, ncclAllGather, const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t)
+
+NCCL_EXPORT ncclResult_t ncclReduce(const void* sendbuff, void* recvbuff, size_t count, ncclDataType_t datatype,
+                                    ncclRedOp_t op, int root, ncclComm_t comm, hipStream_t stream) {
+  CollInfo info = {FUNC_REDUCE, "Reduce", sendbuff, recvbuff, count, datatype, op, root, comm, stream};
+  return enqueueCheck(&info);
+}
+NCCL_ALIAS(ncclResult_t, ncclReduce, const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t,
+           hipStream_t)

@@ -1,0 +1,454 @@
+// init.cc — communicator lifecycle: unique id, InitRank(Config), InitAll, Finalize/Destroy/Abort,
+// error strings, async error, queries, custom PreMulSum operators, ncclMemAlloc/Free.
+//
+// Reference: src/init.cc (ncclGetUniqueId :183, ncclCommInitRankFunc :1831-1968,
+// initTransportsRank :965-1720, ncclCommInitRank :2562, ncclCommInitAll :2581-2643,
+// ncclCommDestroy :2879, ncclCommAbort :3025, ncclGetErrorString :3415, ncclCommGetAsyncError :3449),
+// src/enqueue.cc:2479-2583 (user PreMulSum ops), src/allocator.cc (ncclMemAlloc).
+// What is NOT rebuilt (out of scope): topology/graph search (single-node full mesh is
+// fixed), proxy thread, net/SHM/NVLS transports, split/shrink/grow, windows, suspend/resume.
+#include <string.h>
+#include <unistd.h>
+
+#include <fstream>
+#include <functional>
+#include <thread>
+
+#include "core.h"
+
+namespace ncclamd {
+ncclResult_t exportHandles(ncclComm* comm, PeerInfo* info);
+
+ncclResult_t commCheck(const ncclComm* comm, const char* opname, const char* what) {
+  if (comm == nullptr) {
+    WARN("%s : %s argument is NULL", opname, what);
+    return ncclInvalidArgument;
+  }
+  if (comm->startMagic != kCommMagic || comm->endMagic != kCommMagic) {
+    WARN("Error: corrupted comm object detected");
+    return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
+static uint64_t hostHash() {
+  char host[256] = "";
+  gethostname(host, sizeof(host) - 1);
+  std::string s(host);
+  std::ifstream f("/proc/sys/kernel/random/boot_id");
+  std::string boot;
+  if (f) std::getline(f, boot);
+  s += boot;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a
+  for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+  return h;
+}
+
+static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclConfig_t* cfg) {
+  c->startMagic = c->endMagic = kCommMagic;
+  c->rank = rank;
+  c->nRanks = nranks;
+  c->device = dev;
+  c->blocking = true;
+  c->minCTAs = 1;
+  c->maxCTAs = (int)paramInt("NCCL_MAX_CTAS", paramInt("NCCL_MAX_NCHANNELS", 64));
+  if (cfg) {
+    if (cfg->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = cfg->blocking != 0;
+    if (cfg->minCTAs != NCCL_CONFIG_UNDEF_INT) c->minCTAs = cfg->minCTAs;
+    if (cfg->maxCTAs != NCCL_CONFIG_UNDEF_INT) c->maxCTAs = cfg->maxCTAs;
+    if (cfg->commName) c->commName = cfg->commName;
+  }
+  if (c->maxCTAs < 1) c->maxCTAs = 1;
+  if (c->maxCTAs > NCCL_AMD_MAX_CHANNELS) c->maxCTAs = NCCL_AMD_MAX_CHANNELS;
+  if (c->minCTAs < 1) c->minCTAs = 1;
+  if (c->minCTAs > c->maxCTAs) c->minCTAs = c->maxCTAs;
+  c->maxChannels = c->maxCTAs;
+  c->nSlots = (int)paramInt("NCCL_AMD_NSLOTS", 2);
+  if (c->nSlots < 1) c->nSlots = 1;
+  int64_t sb = paramInt("NCCL_AMD_SLOT_BYTES", 128 << 10);
+  sb = (sb + 4095) / 4096 * 4096;
+  if (sb < 4096) sb = 4096;
+  c->slotBytes = (size_t)sb;
+}
+
+static ncclResult_t checkConfig(const ncclConfig_t* cfg) {
+  if (!cfg) return ncclSuccess;
+  if (cfg->magic != NCCL_API_MAGIC || cfg->size < offsetof(ncclConfig_t, cgaClusterSize)) {
+    WARN("ncclConfig_t was not initialized with NCCL_CONFIG_INITIALIZER");
+    return ncclInvalidArgument;
+  }
+  if (cfg->blocking != NCCL_CONFIG_UNDEF_INT && cfg->blocking != 0 && cfg->blocking != 1) {
+    WARN("Invalid config blocking attribute value %d", cfg->blocking);
+    return ncclInvalidArgument;
+  }
+  if (cfg->minCTAs != NCCL_CONFIG_UNDEF_INT && cfg->minCTAs <= 0) {
+    WARN("Invalid config minCTAs %d", cfg->minCTAs);
+    return ncclInvalidArgument;
+  }
+  if (cfg->maxCTAs != NCCL_CONFIG_UNDEF_INT && cfg->maxCTAs <= 0) {
+    WARN("Invalid config maxCTAs %d", cfg->maxCTAs);
+    return ncclInvalidArgument;
+  }
+  return ncclSuccess;
+}
+
+static ncclResult_t fillPeerInfo(ncclComm* comm, PeerInfo* p) {
+  memset(p, 0, sizeof(*p));
+  p->rank = comm->rank;
+  p->device = comm->device;
+  p->pid = getpid();
+  p->hostHash = hostHash();
+  HIPCHECK(hipDeviceGetPCIBusId(p->busId, sizeof(p->busId), comm->device));
+  NCCLCHECK(exportHandles(comm, p));
+  return ncclSuccess;
+}
+
+// Shape parameters every rank must agree on (exchanged with the PeerInfo block).
+struct ShapeInfo {
+  int maxChannels, nSlots;
+  uint64_t slotBytes;
+};
+
+static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id, int rank, int dev,
+                                    const ncclConfig_t* cfg) {
+  ncclComm* comm = new ncclComm();
+  commDefaults(comm, rank, nranks, dev, cfg);
+  ncclResult_t res = ncclSuccess;
+  struct Blob {
+    PeerInfo info;
+    ShapeInfo shape;
+  };
+  std::vector<Blob> blobs(nranks);
+  if ((res = bootstrapInit(&id, rank, nranks, &comm->bootstrap)) != ncclSuccess) goto fail;
+  // Agree on the channel/slot shape: rank 0's parameters win (env may differ per process).
+  {
+    std::vector<ShapeInfo> shapes(nranks);
+    shapes[rank] = {comm->maxChannels, comm->nSlots, comm->slotBytes};
+    if ((res = bootstrapAllGather(comm->bootstrap, shapes.data(), sizeof(ShapeInfo))) != ncclSuccess) goto fail;
+    comm->maxChannels = comm->maxCTAs = shapes[0].maxChannels;
+    comm->nSlots = shapes[0].nSlots;
+    comm->slotBytes = shapes[0].slotBytes;
+    if (comm->minCTAs > comm->maxCTAs) comm->minCTAs = comm->maxCTAs;
+  }
+  if ((res = transportSetup(comm)) != ncclSuccess) goto fail;
+  if ((res = fillPeerInfo(comm, &blobs[rank].info)) != ncclSuccess) goto fail;
+  if ((res = bootstrapAllGather(comm->bootstrap, blobs.data(), sizeof(Blob))) != ncclSuccess) goto fail;
+  comm->peers.resize(nranks);
+  for (int r = 0; r < nranks; r++) comm->peers[r] = blobs[r].info;
+  if ((res = transportConnect(comm)) != ncclSuccess) goto fail;
+  if ((res = commAllocDevState(comm)) != ncclSuccess) goto fail;
+  if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
+  INFO("comm %p rank %d nRanks %d dev %d busId %s - Init COMPLETE", (void*)comm, rank, nranks, dev,
+       comm->peers[rank].busId);
+  *out = comm;
+  return ncclSuccess;
+fail:
+  transportFree(comm);
+  bootstrapClose(comm->bootstrap);
+  comm->startMagic = comm->endMagic = 0;
+  delete comm;
+  *out = nullptr;
+  return res;
+}
+
+}  // namespace ncclamd
+
+using namespace ncclamd;
+
+#define NCCL_ALIAS(ret, name, ...) extern "C" __attribute__((visibility("default"), alias(#name))) ret p##name(__VA_ARGS__);
+
+NCCL_EXPORT ncclResult_t ncclGetVersion(int* version) {
+  if (version == nullptr) return ncclInvalidArgument;
+  *version = NCCL_VERSION_CODE;
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclGetVersion, int*)
+
+NCCL_EXPORT ncclResult_t ncclGetUniqueId(ncclUniqueId* out) {
+  logInit();
+  if (out == nullptr) {
+    WARN("ncclGetUniqueId : out argument is NULL");
+    return ncclInvalidArgument;
+  }
+  return bootstrapGetUniqueId(out);
+}
+NCCL_ALIAS(ncclResult_t, ncclGetUniqueId, ncclUniqueId*)
+
+static ncclResult_t initRankCommon(ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank,
+                                   ncclConfig_t* config) {
+  logInit();
+  if (newcomm == nullptr) {
+    WARN("CommInitRank : comm argument is NULL");
+    return ncclInvalidArgument;
+  }
+  *newcomm = nullptr;
+  if (nranks < 1 || nranks > NCCL_AMD_MAX_RANKS) {
+    WARN("Invalid number of ranks %d (this engine supports 1..%d intra-node ranks)", nranks, NCCL_AMD_MAX_RANKS);
+    return ncclInvalidArgument;
+  }
+  if (myrank < 0 || myrank >= nranks) {
+    WARN("Invalid rank requested : %d/%d", myrank, nranks);
+    return ncclInvalidArgument;
+  }
+  NCCLCHECK(checkConfig(config));
+  int dev = 0;
+  HIPCHECK(hipGetDevice(&dev));
+  ncclConfig_t cfgCopy;
+  bool hasCfg = config != nullptr;
+  if (hasCfg) cfgCopy = *config;
+  if (groupActive()) {
+    // Deferred to ncclGroupEnd, where all pending inits run concurrently (reference group.cc:35).
+    return groupDeferInit([=]() -> ncclResult_t {
+      HIPCHECK(hipSetDevice(dev));
+      return commInitRankDev(newcomm, nranks, commId, myrank, dev, hasCfg ? &cfgCopy : nullptr);
+    });
+  }
+  return commInitRankDev(newcomm, nranks, commId, myrank, dev, hasCfg ? &cfgCopy : nullptr);
+}
+
+NCCL_EXPORT ncclResult_t ncclCommInitRankConfig(ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank,
+                                                ncclConfig_t* config) {
+  return initRankCommon(newcomm, nranks, commId, myrank, config);
+}
+NCCL_ALIAS(ncclResult_t, ncclCommInitRankConfig, ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*)
+
+NCCL_EXPORT ncclResult_t ncclCommInitRank(ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank) {
+  return initRankCommon(newcomm, nranks, commId, myrank, nullptr);
+}
+NCCL_ALIAS(ncclResult_t, ncclCommInitRank, ncclComm_t*, int, ncclUniqueId, int)
+
+// Single-process clique: every comm lives in this process, so peers are connected by raw pointers and
+// no socket rendezvous is needed (reference init.cc:2581-2643 runs the generic path in threads).
+NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
+  logInit();
+  if (comms == nullptr) {
+    WARN("CommInitAll : comms argument is NULL");
+    return ncclInvalidArgument;
+  }
+  if (ndev < 0 || ndev > NCCL_AMD_MAX_RANKS) {
+    WARN("Invalid device count requested : %d", ndev);
+    return ncclInvalidArgument;
+  }
+  int total = 0;
+  HIPCHECK(hipGetDeviceCount(&total));
+  bool multiRank = paramInt("NCCL_MULTI_RANK_GPU_ENABLE", 0) != 0;  // reference init.cc:68
+  std::vector<int> seen(total > 0 ? total : 1, 0);
+  for (int i = 0; i < ndev; i++) {
+    int d = devlist ? devlist[i] : i;
+    if (d < 0 || d >= total) {
+      WARN("Invalid device %d (totalnDev=%d)", d, total);
+      return ncclInvalidArgument;
+    }
+    if (seen[d] && !multiRank) {
+      WARN("Duplicate device %d in devlist (set NCCL_MULTI_RANK_GPU_ENABLE=1 to allow)", d);
+      return ncclInvalidUsage;
+    }
+    seen[d] = 1;
+  }
+  if (ndev == 0) return ncclSuccess;
+  int oldDev = 0;
+  HIPCHECK(hipGetDevice(&oldDev));
+  std::vector<ncclComm*> cs(ndev, nullptr);
+  ncclResult_t res = ncclSuccess;
+  std::vector<PeerInfo> infos(ndev);
+  for (int i = 0; i < ndev && res == ncclSuccess; i++) {
+    int d = devlist ? devlist[i] : i;
+    cs[i] = new ncclComm();
+    commDefaults(cs[i], i, ndev, d, nullptr);
+    res = transportSetup(cs[i]);
+    if (res == ncclSuccess) res = fillPeerInfo(cs[i], &infos[i]);
+  }
+  for (int i = 0; i < ndev && res == ncclSuccess; i++) {
+    cs[i]->peers = infos;
+    res = transportConnect(cs[i]);
+    if (res == ncclSuccess) res = commAllocDevState(cs[i]);
+  }
+  (void)hipSetDevice(oldDev);
+  if (res != ncclSuccess) {
+    for (auto* c : cs)
+      if (c) {
+        transportFree(c);
+        delete c;
+      }
+    return res;
+  }
+  for (int i = 0; i < ndev; i++) comms[i] = cs[i];
+  INFO("ncclCommInitAll COMPLETE: %d ranks", ndev);
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommInitAll, ncclComm_t*, int, const int*)
+
+static void pollAsync(ncclComm* comm) {
+  if (comm->hostError && __atomic_load_n(comm->hostError, __ATOMIC_ACQUIRE) != DERR_NONE) {
+    uint32_t e = __atomic_load_n(comm->hostError, __ATOMIC_ACQUIRE);
+    int cur = ncclSuccess;
+    ncclResult_t r = e == DERR_ABORT ? ncclRemoteError : ncclSystemError;
+    if (comm->asyncResult.compare_exchange_strong(cur, r))
+      WARN("rank %d: device-side %s in a collective kernel", comm->rank,
+           e == DERR_TIMEOUT ? "spin timeout (peer never arrived)" : "abort");
+  }
+}
+
+NCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
+  NCCLCHECK(commCheck(comm, "ncclCommFinalize", "comm"));
+  if (comm->finalized) return ncclInvalidUsage;
+  HIPCHECK(hipSetDevice(comm->device));
+  HIPCHECK(hipDeviceSynchronize());
+  if (comm->bootstrap) NCCLCHECK(bootstrapBarrier(comm->bootstrap));
+  comm->finalized = true;
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommFinalize, ncclComm_t)
+
+static ncclResult_t commFree(ncclComm* comm) {
+  if (comm->internalStream) (void)hipStreamDestroy(comm->internalStream);
+  transportFree(comm);
+  bootstrapClose(comm->bootstrap);
+  comm->bootstrap = nullptr;
+  comm->startMagic = comm->endMagic = 0;
+  delete comm;
+  return ncclSuccess;
+}
+
+NCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;  // reference: destroying NULL is a no-op
+  NCCLCHECK(commCheck(comm, "ncclCommDestroy", "comm"));
+  int old = 0;
+  (void)hipGetDevice(&old);
+  (void)hipSetDevice(comm->device);
+  if (!comm->finalized) {
+    // Wait for this rank's kernels, then for every peer (no peer may still write into our slab).
+    (void)hipDeviceSynchronize();
+    if (comm->bootstrap) (void)bootstrapBarrier(comm->bootstrap);
+  }
+  commFree(comm);
+  (void)hipSetDevice(old);
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommDestroy, ncclComm_t)
+
+NCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
+  if (comm == nullptr) return ncclSuccess;
+  NCCLCHECK(commCheck(comm, "ncclCommAbort", "comm"));
+  // Kernels poll the abort word inside every bounded spin (reference primitives.h:154-164).
+  if (comm->hostAbort) __atomic_store_n(comm->hostAbort, 1u, __ATOMIC_RELEASE);
+  (void)hipSetDevice(comm->device);
+  (void)hipDeviceSynchronize();
+  commFree(comm);
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommAbort, ncclComm_t)
+
+NCCL_EXPORT const char* ncclGetErrorString(ncclResult_t code) {
+  switch (code) {
+    case ncclSuccess: return "no error";
+    case ncclUnhandledCudaError: return "unhandled hip error (run with NCCL_DEBUG=INFO for details)";
+    case ncclSystemError: return "unhandled system error (run with NCCL_DEBUG=INFO for details)";
+    case ncclInternalError: return "internal error - please report this issue to the NCCL developers";
+    case ncclInvalidArgument: return "invalid argument (run with NCCL_DEBUG=WARN for details)";
+    case ncclInvalidUsage: return "invalid usage (run with NCCL_DEBUG=WARN for details)";
+    case ncclRemoteError: return "remote process exited or there was a network error";
+    case ncclInProgress: return "NCCL operation in progress";
+    case ncclTimeout: return "timeout";
+    default: return "unknown result code";
+  }
+}
+NCCL_ALIAS(const char*, ncclGetErrorString, ncclResult_t)
+
+NCCL_EXPORT const char* ncclGetLastError(ncclComm_t comm) {
+  (void)comm;
+  return lastError();
+}
+NCCL_ALIAS(const char*, ncclGetLastError, ncclComm_t)
+
+NCCL_EXPORT ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* asyncError) {
+  NCCLCHECK(commCheck(comm, "ncclGetAsyncError", "comm"));
+  if (asyncError == nullptr) {
+    WARN("ncclGetAsyncError : asyncError argument is NULL");
+    return ncclInvalidArgument;
+  }
+  pollAsync(comm);
+  *asyncError = (ncclResult_t)comm->asyncResult.load();
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommGetAsyncError, ncclComm_t, ncclResult_t*)
+
+NCCL_EXPORT ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+  NCCLCHECK(commCheck(comm, "CommCount", "comm"));
+  if (!count) return ncclInvalidArgument;
+  *count = comm->nRanks;
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommCount, const ncclComm_t, int*)
+
+NCCL_EXPORT ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* devid) {
+  NCCLCHECK(commCheck(comm, "CommCuDevice", "comm"));
+  if (!devid) return ncclInvalidArgument;
+  *devid = comm->device;
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommCuDevice, const ncclComm_t, int*)
+
+NCCL_EXPORT ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+  NCCLCHECK(commCheck(comm, "CommUserRank", "comm"));
+  if (!rank) return ncclInvalidArgument;
+  *rank = comm->rank;
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclCommUserRank, const ncclComm_t, int*)
+
+// ---- custom operators (reference enqueue.cc:2560-2576 user ops, ncclRedOpCreatePreMulSum) ----
+NCCL_EXPORT ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,
+                                                  ncclScalarResidence_t residence, ncclComm_t comm) {
+  NCCLCHECK(commCheck(comm, "ncclRedOpCreatePreMulSum", "comm"));
+  if (op == nullptr || scalar == nullptr || datatype < 0 || datatype >= ncclNumTypes) return ncclInvalidArgument;
+  UserRedOp u = {};
+  u.used = true;
+  u.datatype = datatype;
+  u.devOp = DEV_PREMULSUM;
+  if (residence == ncclScalarHostImmediate) {
+    memcpy(&u.scalarArg, scalar, typeSize(datatype));
+    u.scalarPtr = nullptr;
+  } else if (residence == ncclScalarDevice) {
+    u.scalarPtr = scalar;
+  } else {
+    return ncclInvalidArgument;
+  }
+  size_t ix = 0;
+  while (ix < comm->userOps.size() && comm->userOps[ix].used) ix++;
+  if (ix == comm->userOps.size()) comm->userOps.push_back(u);
+  else comm->userOps[ix] = u;
+  *op = (ncclRedOp_t)(ncclNumOps + ix);
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclRedOpCreatePreMulSum, ncclRedOp_t*, void*, ncclDataType_t, ncclScalarResidence_t,
+           ncclComm_t)
+
+NCCL_EXPORT ncclResult_t ncclRedOpDestroy(ncclRedOp_t op, ncclComm_t comm) {
+  NCCLCHECK(commCheck(comm, "ncclRedOpDestroy", "comm"));
+  int ix = (int)op - (int)ncclNumOps;
+  if (ix < 0 || ix >= (int)comm->userOps.size() || !comm->userOps[ix].used) {
+    WARN("ncclRedOpDestroy : operator %d unknown to this communicator", (int)op);
+    return ncclInvalidArgument;
+  }
+  comm->userOps[ix].used = false;
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclRedOpDestroy, ncclRedOp_t, ncclComm_t)
+
+NCCL_EXPORT ncclResult_t ncclMemAlloc(void** ptr, size_t size) {
+  if (ptr == nullptr) return ncclInvalidArgument;
+  if (size == 0) {
+    *ptr = nullptr;
+    return ncclSuccess;
+  }
+  HIPCHECK(hipMalloc(ptr, size));
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclMemAlloc, void**, size_t)
+
+NCCL_EXPORT ncclResult_t ncclMemFree(void* ptr) {
+  if (ptr) HIPCHECK(hipFree(ptr));
+  return ncclSuccess;
+}
+NCCL_ALIAS(ncclResult_t, ncclMemFree, void*)

@@ -1,0 +1,208 @@
+// numerics.h — element types and reduction functors of the MI355X kernels.
+//
+// Semantics follow the reference functors (src/device/reduce_kernel.h):
+//   Sum/Prod on integers wrap mod 2^k; signed integers use the unsigned kernels (generate.py:138-146).
+//   MinMax on integers: (a^m) < (b^m) ? a : b with the xormask m from hostToDevRedOp
+//     (enqueue.cc:2517-2526; reduce_kernel.h:349-356).
+//   MinMax on floats: fminf/fmaxf, NaN-ignoring (reduce_kernel.h:409-410, __hmin/__hmax :428-459).
+//   fp16/bf16 Sum/Prod: one IEEE operation rounded RNE to the storage type after every hop
+//     (== __hadd/__hmul: an fp32 add/mul of two 11- or 8-bit-significand values rounded once to T is
+//     the correctly rounded result).
+//   fp8 (OCP e4m3fn / e5m2): computed in half, then converted back with saturation to the largest
+//     finite value (reduce_kernel.h:461-487; __NV_SATFINITE).
+//   PreMulSum: preOp x*s rounded to T, then Sum (reduce_kernel.h:586-712). SumPostDiv (integer avg):
+//     Sum, then divide the wrapped sum by n, sign-magnitude (reduce_kernel.h:936-966).
+// The kernels are built with -ffp-contract=off so x*s + acc is never fused into one FMA.
+//
+// All helpers are __host__ __device__ so tests/ can check them exhaustively on the host against the
+// independent C oracle (oracle/nccl_oracle.c).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ncclamd {
+
+struct half_t { uint16_t x; };
+struct bf16_t { uint16_t x; };
+struct e4m3_t { uint8_t x; };
+struct e5m2_t { uint8_t x; };
+
+__host__ __device__ inline float u32AsF32(uint32_t u) { return __builtin_bit_cast(float, u); }
+__host__ __device__ inline uint32_t f32AsU32(float f) { return __builtin_bit_cast(uint32_t, f); }
+
+// ---- fp16 ----
+__host__ __device__ inline float halfToF32(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+__host__ __device__ inline uint16_t f32ToHalf(float f) { return __builtin_bit_cast(uint16_t, (_Float16)f); }
+
+// ---- bf16: RNE with NaN kept NaN (v_cvt_pk_bf16_f32 on gfx950) ----
+__host__ __device__ inline float bf16ToF32(uint16_t b) { return u32AsF32((uint32_t)b << 16); }
+__host__ __device__ inline uint16_t f32ToBf16(float f) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+#else
+  uint32_t u = f32AsU32(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1);
+  return (uint16_t)(u >> 16);
+#endif
+}
+
+// ---- fp8 (OCP). Decode is exact; encode rounds RNE and saturates to max finite. ----
+template <bool E5M2>
+__host__ __device__ inline float fp8ToF32(uint8_t v) {
+  uint32_t sign = (uint32_t)(v & 0x80) << 24;
+  if (E5M2) {
+    uint32_t e = (v >> 2) & 0x1f, m = v & 3;
+    if (e == 31) return u32AsF32(sign | 0x7f800000u | (m ? 0x400000u : 0u));
+    if (e == 0) return u32AsF32(sign | f32AsU32((float)m * (1.0f / 65536.0f)));
+    return u32AsF32(sign | ((e + 112) << 23) | (m << 21));
+  } else {
+    uint32_t e = (v >> 3) & 0xf, m = v & 7;
+    if (e == 15 && m == 7) return u32AsF32(sign | 0x7fc00000u);
+    if (e == 0) return u32AsF32(sign | f32AsU32((float)m * (1.0f / 512.0f)));
+    return u32AsF32(sign | ((e + 120) << 23) | (m << 20));
+  }
+}
+
+template <bool E5M2>
+__host__ __device__ inline uint8_t f32ToFp8Sat(float f) {
+  uint32_t u = f32AsU32(f);
+  uint8_t sign = (uint8_t)((u >> 24) & 0x80);
+  uint32_t a = u & 0x7fffffffu;
+  if (a > 0x7f800000u) return sign | 0x7f;  // NaN
+  constexpr uint32_t kMax = E5M2 ? 0x47600000u : 0x43e00000u;     // 57344 / 448
+  constexpr uint32_t kMinNorm = E5M2 ? 0x38800000u : 0x3c800000u; // 2^-14 / 2^-6
+  constexpr uint8_t kMaxCode = E5M2 ? 0x7b : 0x7e;
+  constexpr int kMan = E5M2 ? 2 : 3;
+  constexpr int kBiasAdj = E5M2 ? 112 : 120;  // 127 - bias
+  if (a >= kMax) return sign | kMaxCode;
+  if (a < kMinNorm) {
+    // subnormal quantum 2^-16 / 2^-9: scale exactly, round to nearest even integer
+    float q = u32AsF32(a) * (E5M2 ? 65536.0f : 512.0f);
+    uint32_t qi = (uint32_t)q;
+    float frac = q - (float)qi;
+    if (frac > 0.5f || (frac == 0.5f && (qi & 1))) qi++;
+    return sign | (uint8_t)qi;  // qi == 2^kMan becomes the smallest normal code
+  }
+  uint32_t e = (a >> 23) - kBiasAdj;
+  uint32_t man = a & 0x7fffffu;
+  uint32_t code = (e << kMan) | (man >> (23 - kMan));
+  uint32_t rem = man & ((1u << (23 - kMan)) - 1);
+  uint32_t halfway = 1u << (22 - kMan);
+  if (rem > halfway || (rem == halfway && (code & 1))) code++;
+  if (code > kMaxCode) code = kMaxCode;
+  return sign | (uint8_t)code;
+}
+
+// ---- per-type traits: load as f32 ("compute" value) and store back with the type's rounding ----
+template <typename T> struct Traits;
+template <> struct Traits<uint8_t>  { static constexpr bool isFloat = false; };
+template <> struct Traits<uint16_t> { static constexpr bool isFloat = false; };
+template <> struct Traits<uint32_t> { static constexpr bool isFloat = false; };
+template <> struct Traits<uint64_t> { static constexpr bool isFloat = false; };
+template <> struct Traits<float>    { static constexpr bool isFloat = true; };
+template <> struct Traits<double>   { static constexpr bool isFloat = true; };
+template <> struct Traits<half_t> {
+  static constexpr bool isFloat = true;
+  __host__ __device__ static float toF(half_t v) { return halfToF32(v.x); }
+  __host__ __device__ static half_t fromF(float f) { return half_t{f32ToHalf(f)}; }
+};
+template <> struct Traits<bf16_t> {
+  static constexpr bool isFloat = true;
+  __host__ __device__ static float toF(bf16_t v) { return bf16ToF32(v.x); }
+  __host__ __device__ static bf16_t fromF(float f) { return bf16_t{f32ToBf16(f)}; }
+};
+template <> struct Traits<e4m3_t> {
+  static constexpr bool isFloat = true;
+  __host__ __device__ static float toF(e4m3_t v) { return fp8ToF32<false>(v.x); }
+  // the reference's fp8 ops run on __half and convert back with saturation: round to half first
+  __host__ __device__ static e4m3_t fromF(float f) { return e4m3_t{f32ToFp8Sat<false>(halfToF32(f32ToHalf(f)))}; }
+};
+template <> struct Traits<e5m2_t> {
+  static constexpr bool isFloat = true;
+  __host__ __device__ static float toF(e5m2_t v) { return fp8ToF32<true>(v.x); }
+  __host__ __device__ static e5m2_t fromF(float f) { return e5m2_t{f32ToFp8Sat<true>(halfToF32(f32ToHalf(f)))}; }
+};
+
+// ---- functors: pre(x), red(preLocal, acc), post(acc) ----
+template <typename T, int OP> struct Red;
+
+// integers (unsigned storage)
+template <typename T, int OP>
+struct RedInt {
+  T arg;  // xormask (MinMax) / scalar (PreMulSum)
+  uint32_t divisor;
+  bool isSigned;
+  __host__ __device__ explicit RedInt(uint64_t a) : arg((T)a), divisor((uint32_t)(a >> 1)), isSigned(a & 1) {}
+  __host__ __device__ T pre(T x) const { return OP == 3 ? (T)(x * arg) : x; }
+  __host__ __device__ T red(T a, T b) const {
+    if (OP == 1) return (T)(a * b);
+    if (OP == 2) return (T)(a ^ arg) < (T)(b ^ arg) ? a : b;
+    return (T)(a + b);
+  }
+  __host__ __device__ T post(T x) const {
+    if (OP != 4) return x;
+    const T signBit = (T)((T)1 << (sizeof(T) * 8 - 1));
+    bool neg = isSigned && (x & signBit);
+    T xabs = neg ? (T)(0 - x) : x;
+    T q = (T)(xabs / (T)divisor);
+    return neg ? (T)(0 - q) : q;
+  }
+};
+template <int OP> struct Red<uint8_t, OP> : RedInt<uint8_t, OP> { using RedInt<uint8_t, OP>::RedInt; };
+template <int OP> struct Red<uint16_t, OP> : RedInt<uint16_t, OP> { using RedInt<uint16_t, OP>::RedInt; };
+template <int OP> struct Red<uint32_t, OP> : RedInt<uint32_t, OP> { using RedInt<uint32_t, OP>::RedInt; };
+template <int OP> struct Red<uint64_t, OP> : RedInt<uint64_t, OP> { using RedInt<uint64_t, OP>::RedInt; };
+
+template <int OP> struct Red<float, OP> {
+  float s;
+  bool isMin;
+  __host__ __device__ explicit Red(uint64_t a) : s(u32AsF32((uint32_t)a)), isMin((a & 1) == 0) {}
+  __host__ __device__ float pre(float x) const { return OP == 3 ? x * s : x; }
+  __host__ __device__ float red(float a, float b) const {
+    if (OP == 1) return a * b;
+    if (OP == 2) return isMin ? fminf(a, b) : fmaxf(a, b);
+    return a + b;
+  }
+  __host__ __device__ float post(float x) const { return x; }
+};
+template <int OP> struct Red<double, OP> {
+  double s;
+  bool isMin;
+  __host__ __device__ explicit Red(uint64_t a) : s(__builtin_bit_cast(double, a)), isMin((a & 1) == 0) {}
+  __host__ __device__ double pre(double x) const { return OP == 3 ? x * s : x; }
+  __host__ __device__ double red(double a, double b) const {
+    if (OP == 1) return a * b;
+    if (OP == 2) return isMin ? fmin(a, b) : fmax(a, b);
+    return a + b;
+  }
+  __host__ __device__ double post(double x) const { return x; }
+};
+
+// small floats: compute in f32, round to T after every operation
+template <typename T, int OP>
+struct RedSmall {
+  float s;
+  bool isMin;
+  __host__ __device__ explicit RedSmall(uint64_t a) {
+    T sv;
+    __builtin_memcpy(&sv, &a, sizeof(T));
+    s = Traits<T>::toF(sv);
+    isMin = (a & 1) == 0;
+  }
+  __host__ __device__ T pre(T x) const { return OP == 3 ? Traits<T>::fromF(Traits<T>::toF(x) * s) : x; }
+  __host__ __device__ T red(T a, T b) const {
+    float x = Traits<T>::toF(a), y = Traits<T>::toF(b), r;
+    if (OP == 1) r = x * y;
+    else if (OP == 2) r = isMin ? fminf(x, y) : fmaxf(x, y);
+    else r = x + y;
+    return Traits<T>::fromF(r);
+  }
+  __host__ __device__ T post(T x) const { return x; }
+};
+template <int OP> struct Red<half_t, OP> : RedSmall<half_t, OP> { using RedSmall<half_t, OP>::RedSmall; };
+template <int OP> struct Red<bf16_t, OP> : RedSmall<bf16_t, OP> { using RedSmall<bf16_t, OP>::RedSmall; };
+template <int OP> struct Red<e4m3_t, OP> : RedSmall<e4m3_t, OP> { using RedSmall<e4m3_t, OP>::RedSmall; };
+template <int OP> struct Red<e5m2_t, OP> : RedSmall<e5m2_t, OP> { using RedSmall<e5m2_t, OP>::RedSmall; };
+
+}  // namespace ncclamd

@@ -1,0 +1,159 @@
+// transport.cc — the xGMI peer-memory transport: staging + flag allocation, HIP IPC export/import.
+//
+// Reference: src/transport/p2p.cc:130-618 allocates, per ring edge and channel, a receiver-side FIFO
+// (ncclRecvMem + buffers) and sender-side head word, shares them through CUDA IPC / cuMem handles
+// (p2p.cc:220-325) or a direct pointer inside one process (p2p.cc:345-386), and connects only the
+// ring neighbours. On MI355X every GPU of the node has a direct xGMI link to every other GPU, so here
+// each rank allocates ONE staging slab and ONE flag block that ALL peers write into (full mesh), and
+// maps every peer's slab once at init:
+//   - same process (ncclCommInitAll / threads): raw pointer + hipDeviceEnablePeerAccess;
+//   - other process: hipIpcGetMemHandle / hipIpcOpenMemHandle (dmabuf IPC on this platform).
+// Staging and flags are allocated UNCACHED (hipDeviceMallocUncached): they are written by remote
+// GPUs over xGMI and read locally, so no L2 anywhere may hold a stale copy.
+#include <string.h>
+#include <unistd.h>
+
+#include "core.h"
+
+namespace ncclamd {
+
+static size_t stagingBytes(const ncclComm* c) {
+  return (size_t)c->maxChannels * STG_KINDS * c->nSlots * c->nRanks * c->slotBytes;
+}
+static size_t flagsBytes(const ncclComm* c) {
+  return (size_t)c->maxChannels * FLG_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
+}
+
+ncclResult_t transportSetup(ncclComm* comm) {
+  HIPCHECK(hipSetDevice(comm->device));
+  if (comm->nRanks == 1) return ncclSuccess;  // nranks==1 never touches peers (onerank.cu:49-110)
+  size_t sb = stagingBytes(comm), fb = flagsBytes(comm);
+  HIPCHECK(hipExtMallocWithFlags(&comm->staging, sb, hipDeviceMallocUncached));
+  HIPCHECK(hipExtMallocWithFlags((void**)&comm->flags, fb, hipDeviceMallocUncached));
+  HIPCHECK(hipMemset(comm->flags, 0, fb));
+  HIPCHECK(hipDeviceSynchronize());
+  INFO("rank %d dev %d: staging %zu MiB (%d ch x %d slots x %zu KiB), flags %zu KiB", comm->rank, comm->device,
+       sb >> 20, comm->maxChannels, comm->nSlots, comm->slotBytes >> 10, fb >> 10);
+  return ncclSuccess;
+}
+
+ncclResult_t transportConnect(ncclComm* comm) {
+  if (comm->nRanks == 1) return ncclSuccess;
+  HIPCHECK(hipSetDevice(comm->device));
+  const PeerInfo& me = comm->peers[comm->rank];
+  for (int r = 0; r < comm->nRanks; r++) {
+    const PeerInfo& p = comm->peers[r];
+    if (r == comm->rank) {
+      comm->peerStaging[r] = comm->staging;
+      comm->peerFlags[r] = comm->flags;
+      continue;
+    }
+    if (p.hostHash != me.hostHash) {
+      WARN("rank %d is on another host: this engine is intra-node only", r);
+      return ncclInvalidUsage;
+    }
+    if (p.pid == me.pid) {
+      // Same process: direct pointers (reference p2p.cc:345-386 "P2P/direct pointer").
+      if (p.device != comm->device) {
+        int can = 0;
+        HIPCHECK(hipDeviceCanAccessPeer(&can, comm->device, p.device));
+        if (!can) {
+          WARN("device %d cannot access peer device %d", comm->device, p.device);
+          return ncclSystemError;
+        }
+        hipError_t e = hipDeviceEnablePeerAccess(p.device, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+          WARN("hipDeviceEnablePeerAccess(%d->%d): %s", comm->device, p.device, hipGetErrorString(e));
+          return ncclUnhandledCudaError;
+        }
+        (void)hipGetLastError();
+      }
+      comm->peerStaging[r] = (void*)p.stagingPtr;
+      comm->peerFlags[r] = (uint64_t*)p.flagsPtr;
+      comm->peerIsIpc[r] = false;
+    } else {
+      void* s = nullptr;
+      void* f = nullptr;
+      HIPCHECK(hipIpcOpenMemHandle(&s, p.stagingHandle, hipIpcMemLazyEnablePeerAccess));
+      HIPCHECK(hipIpcOpenMemHandle(&f, p.flagsHandle, hipIpcMemLazyEnablePeerAccess));
+      comm->peerStaging[r] = s;
+      comm->peerFlags[r] = (uint64_t*)f;
+      comm->peerIsIpc[r] = true;
+    }
+  }
+  return ncclSuccess;
+}
+
+ncclResult_t transportFree(ncclComm* comm) {
+  (void)hipSetDevice(comm->device);
+  for (int r = 0; r < comm->nRanks && r < NCCL_AMD_MAX_RANKS; r++) {
+    if (comm->peerIsIpc[r]) {
+      if (comm->peerStaging[r]) (void)hipIpcCloseMemHandle(comm->peerStaging[r]);
+      if (comm->peerFlags[r]) (void)hipIpcCloseMemHandle(comm->peerFlags[r]);
+    }
+    comm->peerStaging[r] = nullptr;
+    comm->peerFlags[r] = nullptr;
+    comm->peerIsIpc[r] = false;
+  }
+  if (comm->staging) (void)hipFree(comm->staging);
+  if (comm->flags) (void)hipFree(comm->flags);
+  if (comm->counters) (void)hipFree(comm->counters);
+  if (comm->devComm) (void)hipFree(comm->devComm);
+  if (comm->hostAbort) (void)hipHostFree(comm->hostAbort);
+  if (comm->hostError) (void)hipHostFree(comm->hostError);
+  comm->staging = nullptr;
+  comm->flags = nullptr;
+  comm->counters = nullptr;
+  comm->devComm = nullptr;
+  comm->hostAbort = nullptr;
+  comm->hostError = nullptr;
+  return ncclSuccess;
+}
+
+ncclResult_t commAllocDevState(ncclComm* comm) {
+  HIPCHECK(hipSetDevice(comm->device));
+  size_t cb = (size_t)comm->maxChannels * CTR_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
+  HIPCHECK(hipMalloc((void**)&comm->counters, cb));
+  HIPCHECK(hipMemset(comm->counters, 0, cb));
+  HIPCHECK(hipHostMalloc((void**)&comm->hostAbort, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  HIPCHECK(hipHostMalloc((void**)&comm->hostError, 64, hipHostMallocMapped | hipHostMallocCoherent));
+  memset(comm->hostAbort, 0, 64);
+  memset(comm->hostError, 0, 64);
+  DevComm& d = comm->hostDevComm;
+  memset(&d, 0, sizeof(d));
+  d.rank = comm->rank;
+  d.nRanks = comm->nRanks;
+  d.nSlots = comm->nSlots;
+  d.maxChannels = comm->maxChannels;
+  d.slotBytes = comm->slotBytes;
+  // s_memrealtime runs at 100 MHz on gfx9 parts.
+  d.timeoutTicks = (uint64_t)paramInt("NCCL_AMD_SPIN_TIMEOUT_MS", 120000) * 100000ull;
+  for (int r = 0; r < comm->nRanks; r++) {
+    d.staging[r] = (char*)comm->peerStaging[r];
+    d.flags[r] = comm->peerFlags[r];
+  }
+  d.counters = comm->counters;
+  void* dAbort = nullptr;
+  void* dErr = nullptr;
+  HIPCHECK(hipHostGetDevicePointer(&dAbort, comm->hostAbort, 0));
+  HIPCHECK(hipHostGetDevicePointer(&dErr, comm->hostError, 0));
+  d.abortFlag = (uint32_t*)dAbort;
+  d.errorWord = (uint32_t*)dErr;
+  HIPCHECK(hipMalloc((void**)&comm->devComm, sizeof(DevComm)));
+  HIPCHECK(hipMemcpy(comm->devComm, &d, sizeof(DevComm), hipMemcpyHostToDevice));
+  HIPCHECK(hipStreamCreateWithFlags(&comm->internalStream, hipStreamNonBlocking));
+  return ncclSuccess;
+}
+
+ncclResult_t exportHandles(ncclComm* comm, PeerInfo* info) {
+  memset(&info->stagingHandle, 0, sizeof(info->stagingHandle));
+  memset(&info->flagsHandle, 0, sizeof(info->flagsHandle));
+  info->stagingPtr = (uint64_t)comm->staging;
+  info->flagsPtr = (uint64_t)comm->flags;
+  if (comm->nRanks == 1) return ncclSuccess;
+  HIPCHECK(hipIpcGetMemHandle(&info->stagingHandle, comm->staging));
+  HIPCHECK(hipIpcGetMemHandle(&info->flagsHandle, comm->flags));
+  return ncclSuccess;
+}
+
+}  // namespace ncclamd

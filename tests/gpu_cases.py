@@ -1,0 +1,157 @@
+"""Shared helpers for the GPU parity tests: run a collective through the C ABI (nccl_amd) on torch
+device buffers and compare with the CPU oracle. Imported by tests only."""
+from __future__ import annotations
+
+import numpy as np
+
+import oracle
+
+# dtype code -> torch dtype name used to allocate raw storage of the same width
+TORCH_STORAGE = {0: "int8", 1: "uint8", 2: "int32", 3: "int32", 4: "int64", 5: "int64", 6: "int16", 7: "float32",
+                 8: "float64", 9: "int16", 10: "uint8", 11: "uint8"}
+FLOAT_TYPES = {6, 7, 8, 9, 10, 11}
+
+
+def to_device(arr: np.ndarray, device, offset_elems: int = 0):
+    """Copy a numpy storage array to a fresh device buffer; `offset_elems` > 0 returns a view that is
+    deliberately NOT 16-byte aligned (exercises the reference's unaligned fallback)."""
+    import torch
+    raw = np.ascontiguousarray(arr).view(np.uint8)
+    es = arr.dtype.itemsize
+    buf = torch.empty(raw.size + offset_elems * es + 64, dtype=torch.uint8, device=device)
+    view = buf[offset_elems * es: offset_elems * es + raw.size]
+    view.copy_(torch.from_numpy(raw.copy()))
+    return buf, view
+
+
+def from_device(view, dtype_np) -> np.ndarray:
+    return view.cpu().numpy().view(dtype_np).copy()
+
+
+def same_bits(a: np.ndarray, b: np.ndarray, dtype: int) -> bool:
+    """Bitwise equality, with every NaN equal to every NaN for float types."""
+    if a.shape != b.shape:
+        return False
+    if dtype not in FLOAT_TYPES:
+        return np.array_equal(a, b)
+    fa, fb = oracle.to_f32(dtype, a), oracle.to_f32(dtype, b)
+    nan = np.isnan(fa) & np.isnan(fb)
+    return bool(np.all((a == b) | nan))
+
+
+def make_inputs(n: int, dtype: int, count: int, seed: int, kind: int = 0):
+    return [oracle.fill(dtype, seed * 131 + r, count, kind) for r in range(n)]
+
+
+def expected(coll: str, inputs, dtype: int, op: int, root: int = 0):
+    if coll == "allreduce":
+        out = oracle.all_reduce(inputs, dtype, op)
+        return [out] * len(inputs)
+    if coll == "reducescatter":
+        return oracle.reduce_scatter(inputs, dtype, op)
+    if coll == "allgather":
+        out = oracle.all_gather(inputs)
+        return [out] * len(inputs)
+    if coll == "reduce":
+        return [oracle.reduce(inputs, dtype, op, root)]
+    raise ValueError(coll)
+
+
+def out_count(coll: str, n: int, count: int) -> int:
+    return {"allreduce": count, "reducescatter": count // n, "allgather": count * n, "reduce": count}[coll]
+
+
+def launch(comm, coll: str, send_view, recv_view, count: int, dtype: int, op: int, root: int, stream_ptr: int):
+    n = comm.nranks
+    if coll == "allreduce":
+        comm.all_reduce_raw(send_view.data_ptr(), recv_view.data_ptr(), count, dtype, op, stream_ptr)
+    elif coll == "reducescatter":
+        comm.reduce_scatter_raw(send_view.data_ptr(), recv_view.data_ptr(), count // n, dtype, op, stream_ptr)
+    elif coll == "allgather":
+        comm.all_gather_raw(send_view.data_ptr(), recv_view.data_ptr(), count, dtype, stream_ptr)
+    elif coll == "reduce":
+        rp = recv_view.data_ptr() if recv_view is not None else None
+        comm.reduce_raw(send_view.data_ptr(), rp, count, dtype, op, root, stream_ptr)
+
+
+# A compact but broad case list: (collective, dtype, op, count, misalign)
+def case_list(n: int, quick: bool = False):
+    cases = []
+    counts = [1, 5, 4096 + 3, 300_001] if not quick else [5, 70_001]
+    for coll in ("allreduce", "reducescatter", "allgather", "reduce"):
+        for dtype in (7, 9, 6, 2, 3, 4, 0, 1, 5, 8, 10, 11):
+            ops = [0] if coll == "allgather" else [0, 1, 2, 3, 4]
+            for op in ops:
+                if quick and dtype not in (7, 9, 2) and op != 0:
+                    continue
+                for count in counts:
+                    if coll == "reducescatter":
+                        count = max(1, count // n) * n
+                    cases.append((coll, dtype, op, count, 0))
+        cases.append((coll, 7, 0, 100_003 * n, 1))   # misaligned base pointers
+        cases.append((coll, 9, 0, 10_001 * n, 3))
+    return cases
+
+
+def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=False, root=0, sync=True):
+    """Run one collective on every (comm, stream) of this process; returns list of error strings.
+    `comms_and_streams` holds the ranks owned by this process: [(comm, torch stream), ...]; the
+    inputs of ALL ranks are regenerated deterministically so each process can check its own ranks."""
+    import torch
+    n = comms_and_streams[0][0].nranks
+    inputs = make_inputs(n, dtype, count, seed)
+    exp = expected(coll, inputs, dtype, op, root)
+    npdt = oracle.NP_STORAGE[dtype]
+    es = np.dtype(npdt).itemsize
+    ocount = out_count(coll, n, count)
+    keep, views = [], []
+    for comm, stream in comms_and_streams:
+        r = comm.rank
+        dev = torch.device("cuda", comm.device)
+        with torch.cuda.device(dev):
+            if inplace:
+                # one buffer: AR send==recv; RS recv = send + r*recvcount; AG send = recv + r*sendcount
+                if coll in ("allreduce", "reduce"):
+                    buf, sv = to_device(inputs[r], dev, misalign)
+                    rv = sv
+                elif coll == "reducescatter":
+                    buf, sv = to_device(inputs[r], dev, misalign)
+                    rc = count // n
+                    rv = sv[r * rc * es:(r + 1) * rc * es]
+                else:  # allgather
+                    full = np.zeros(count * n, dtype=npdt)
+                    full[r * count:(r + 1) * count] = inputs[r]
+                    buf, rv = to_device(full, dev, misalign)
+                    sv = rv[r * count * es:(r + 1) * count * es]
+                keep.append(buf)
+            else:
+                b1, sv = to_device(inputs[r], dev, misalign)
+                rv = None
+                if coll != "reduce" or r == root:
+                    b2, rv = to_device(np.zeros(ocount, dtype=npdt), dev, misalign)
+                    keep.append(b2)
+                keep.append(b1)
+            views.append((comm, stream, sv, rv))
+    import nccl_amd
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for comm, stream, sv, rv in views:
+            launch(comm, coll, sv, rv, count, dtype, op, root, stream.cuda_stream)
+    errs = []
+    for comm, stream, sv, rv in views:
+        stream.synchronize()
+        ae = comm.async_error()
+        if ae != 0:
+            errs.append(f"rank {comm.rank}: async error {ae}")
+            continue
+        r = comm.rank
+        if coll == "reduce" and r != root:
+            continue
+        got = from_device(rv, npdt)
+        want = exp[0] if coll == "reduce" else exp[r]
+        if not same_bits(got, want, dtype):
+            bad = np.nonzero(got != want)[0]
+            errs.append(f"rank {r} {coll} dt={dtype} op={op} count={count} mis={misalign} inplace={inplace}: "
+                        f"{bad.size} mismatches, first at {bad[:5].tolist()} got {got[bad[:3]].tolist()} "
+                        f"want {want[bad[:3]].tolist()}")
+    return errs

@@ -1,0 +1,99 @@
+"""GPU parity tests: the HIP kernels behind the C ABI vs the CPU oracle (bit-exact for every type,
+including floats, because the kernels fold in the oracle's order with the same per-hop rounding).
+
+Multi-rank cases run several ranks on the ONE GPU of the test box: single-process (ncclCommInitAll
+with a repeated device, NCCL_MULTI_RANK_GPU_ENABLE=1, reference init.cc:68) and multi-process
+(ncclCommInitRank over the TCP bootstrap + HIP IPC). The 8-GPU xGMI path runs the same kernels."""
+import multiprocessing as mp
+import os
+
+import pytest
+
+os.environ.setdefault("NCCL_AMD_SPIN_TIMEOUT_MS", "30000")
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "GPU test on a box without a GPU"
+    return torch
+
+
+def test_one_rank_all_cases(built):
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    torch.cuda.set_device(0)
+    comm = nccl_amd.Communicator.init_all([0])[0]
+    s = torch.cuda.Stream()
+    errs = []
+    for i, (coll, dt, op, count, mis) in enumerate(G.case_list(1)):
+        errs += G.run_case([(comm, s)], coll, dt, op, count, mis, seed=i)
+        errs += G.run_case([(comm, s)], coll, dt, op, count, mis, seed=i, inplace=True) if mis == 0 and i % 3 == 0 else []
+    comm.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_single_process_multirank(built, nranks):
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0] * nranks)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    cs = list(zip(comms, streams))
+    errs = []
+    for i, (coll, dt, op, count, mis) in enumerate(G.case_list(nranks, quick=(nranks > 2))):
+        for root in ([0] if coll != "reduce" else [0, nranks - 1]):
+            errs += G.run_case(cs, coll, dt, op, count, mis, seed=i, root=root)
+        if i % 4 == 0 and mis == 0:
+            errs += G.run_case(cs, coll, dt, op, count, mis, seed=i, inplace=True)
+        if errs:
+            break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
+def _mp_worker(rank, nranks, uid, quick, q):
+    try:
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "30000"
+        import torch
+        import nccl_amd
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.Stream()
+        errs = []
+        for i, (coll, dt, op, count, mis) in enumerate(G.case_list(nranks, quick=quick)):
+            root = i % nranks
+            errs += G.run_case([(comm, s)], coll, dt, op, count, mis, seed=i, root=root)
+            if errs:
+                break
+        comm.destroy()
+        q.put((rank, errs))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, [f"rank {rank} exception: {e!r}"]))
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_multi_process(built, nranks):
+    _torch()
+    import nccl_amd
+    uid = nccl_amd.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_mp_worker, args=(r, nranks, uid, nranks > 2, q)) for r in range(nranks)]
+    for p in ps:
+        p.start()
+    results = {}
+    for _ in range(nranks):
+        r, errs = q.get(timeout=900)
+        results[r] = errs
+    for p in ps:
+        p.join(timeout=60)
+    bad = [e for r in sorted(results) for e in results[r]]
+    assert not bad, "\n".join(bad[:20])
