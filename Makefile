@@ -19,7 +19,7 @@ HOSTOBJ  := $(HOSTSRC:%.cc=$(BUILD)/%.o)
 DEVOBJ   := $(BUILD)/kernels.o
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle
+all: lib oracle numerics-host bootstrap-test
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -47,3 +47,22 @@ clean:
 	rm -rf $(BUILD) $(LIBDIR) oracle/_build
 
 .PHONY: all lib oracle clean
+
+# test-only host build of the kernels' numerics, checked exhaustively against the oracle
+numerics-host: build/libnumerics_host.so
+
+build/libnumerics_host.so: tests/native/numerics_host.cc $(SRCDIR)/numerics.h
+	@mkdir -p build
+	$(CXX) -O2 -std=c++17 -fPIC -shared -ffp-contract=off -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ $<
+
+.PHONY: numerics-host
+
+# test-only host program exercising the TCP bootstrap across forked processes
+bootstrap-test: build/bootstrap_test
+
+build/bootstrap_test: tests/native/bootstrap_test.cc $(SRCDIR)/bootstrap.cc $(SRCDIR)/debug.cc $(HDRS)
+	@mkdir -p build
+	$(CXX) -O2 -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ tests/native/bootstrap_test.cc \
+	  $(SRCDIR)/bootstrap.cc $(SRCDIR)/debug.cc -lpthread
+
+.PHONY: bootstrap-test

@@ -81,7 +81,7 @@ static void rootThread(int listenFd, uint64_t commId) {
   std::vector<int> fds;
   int nranks = -1;
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(bootstrapTimeoutMs());
-  while (nranks < 0 || (int)fds.size() < nranks) {
+  while (true) {  // until every rank has said hello
     struct pollfd pfd = {listenFd, POLLIN, 0};
     int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
     if (left <= 0) { WARN("bootstrap root: timed out waiting for ranks"); goto done; }

@@ -4,7 +4,8 @@
 //   Sum/Prod on integers wrap mod 2^k; signed integers use the unsigned kernels (generate.py:138-146).
 //   MinMax on integers: (a^m) < (b^m) ? a : b with the xormask m from hostToDevRedOp
 //     (enqueue.cc:2517-2526; reduce_kernel.h:349-356).
-//   MinMax on floats: fminf/fmaxf, NaN-ignoring (reduce_kernel.h:409-410, __hmin/__hmax :428-459).
+//   MinMax on floats: fminf/fmaxf, NaN-ignoring (reduce_kernel.h:409-410, __hmin/__hmax :428-459),
+//     with -0 ordered below +0 (see minOrdered).
 //   fp16/bf16 Sum/Prod: one IEEE operation rounded RNE to the storage type after every hop
 //     (== __hadd/__hmul: an fp32 add/mul of two 11- or 8-bit-significand values rounded once to T is
 //     the correctly rounded result).
@@ -94,6 +95,28 @@ __host__ __device__ inline uint8_t f32ToFp8Sat(float f) {
   return sign | (uint8_t)code;
 }
 
+// ---- min/max with a defined signed-zero order ----
+// The reference uses fminf/fmaxf (reduce_kernel.h:409-410) and __hmin/__hmax: NaN-ignoring, but the
+// result for (+0, -0) is implementation-defined in C. Here -0 orders below +0 (IEEE 754-2019
+// minimumNumber/maximumNumber), identically on host and device, so results never depend on the
+// instruction the compiler picks.
+template <typename F>
+__host__ __device__ inline F minOrdered(F a, F b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  if (a < b) return a;
+  if (b < a) return b;
+  return __builtin_signbit(a) ? a : b;
+}
+template <typename F>
+__host__ __device__ inline F maxOrdered(F a, F b) {
+  if (a != a) return b;
+  if (b != b) return a;
+  if (a > b) return a;
+  if (b > a) return b;
+  return __builtin_signbit(a) ? b : a;
+}
+
 // ---- per-type traits: load as f32 ("compute" value) and store back with the type's rounding ----
 template <typename T> struct Traits;
 template <> struct Traits<uint8_t>  { static constexpr bool isFloat = false; };
@@ -161,7 +184,7 @@ template <int OP> struct Red<float, OP> {
   __host__ __device__ float pre(float x) const { return OP == 3 ? x * s : x; }
   __host__ __device__ float red(float a, float b) const {
     if (OP == 1) return a * b;
-    if (OP == 2) return isMin ? fminf(a, b) : fmaxf(a, b);
+    if (OP == 2) return isMin ? minOrdered(a, b) : maxOrdered(a, b);
     return a + b;
   }
   __host__ __device__ float post(float x) const { return x; }
@@ -173,11 +196,21 @@ template <int OP> struct Red<double, OP> {
   __host__ __device__ double pre(double x) const { return OP == 3 ? x * s : x; }
   __host__ __device__ double red(double a, double b) const {
     if (OP == 1) return a * b;
-    if (OP == 2) return isMin ? fmin(a, b) : fmax(a, b);
+    if (OP == 2) return isMin ? minOrdered(a, b) : maxOrdered(a, b);
     return a + b;
   }
   __host__ __device__ double post(double x) const { return x; }
 };
+
+// Keep an f32 result opaque to the optimiser before it is rounded to a narrower type: at -O3 the
+// backend folds fptrunc(fmul(x, y)) into v_fma_mixlo_f16(x, y, +0.0), which turns (-0)*y into +0
+// (found by the fp8 avg parity test). The empty asm forces a plain v_mul_f32 + v_cvt.
+__host__ __device__ inline float opaqueF(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(x));
+#endif
+  return x;
+}
 
 // small floats: compute in f32, round to T after every operation
 template <typename T, int OP>
@@ -190,11 +223,11 @@ struct RedSmall {
     s = Traits<T>::toF(sv);
     isMin = (a & 1) == 0;
   }
-  __host__ __device__ T pre(T x) const { return OP == 3 ? Traits<T>::fromF(Traits<T>::toF(x) * s) : x; }
+  __host__ __device__ T pre(T x) const { return OP == 3 ? Traits<T>::fromF(opaqueF(Traits<T>::toF(x) * s)) : x; }
   __host__ __device__ T red(T a, T b) const {
     float x = Traits<T>::toF(a), y = Traits<T>::toF(b), r;
-    if (OP == 1) r = x * y;
-    else if (OP == 2) r = isMin ? fminf(x, y) : fmaxf(x, y);
+    if (OP == 1) r = opaqueF(x * y);
+    else if (OP == 2) r = isMin ? minOrdered(x, y) : maxOrdered(x, y);
     else r = x + y;
     return Traits<T>::fromF(r);
   }

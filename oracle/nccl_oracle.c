@@ -231,6 +231,21 @@ int oracle_host_to_dev_op(int op, int dt, int nranks, int* devop, uint64_t* arg)
 
 /* ---------------- functors ---------------- */
 
+/* fminf/fmaxf semantics (NaN-ignoring, reduce_kernel.h:409-410) with the signed-zero tie made
+ * explicit: -0 is the smaller of (-0, +0). C leaves fmin(+0,-0) implementation-defined. */
+static double omin(double x, double y) {
+  if (isnan(x)) return y;
+  if (isnan(y)) return x;
+  if (x == y) return signbit(x) ? x : y;
+  return x < y ? x : y;
+}
+static double omax(double x, double y) {
+  if (isnan(x)) return y;
+  if (isnan(y)) return x;
+  if (x == y) return signbit(x) ? y : x;
+  return x > y ? x : y;
+}
+
 static inline uint64_t pre_op(int dt, int devop, uint64_t arg, uint64_t x) {
   if (devop != DEV_PREMULSUM) return x;
   if (is_int(dt)) return (x * arg) & mask_of(dt);
@@ -256,7 +271,7 @@ static inline uint64_t reduce2(int dt, int devop, uint64_t arg, uint64_t a, uint
     switch (kind) {
       case DEV_SUM: r = x + y; break;
       case DEV_PROD: r = x * y; break;
-      default: r = isMin ? fminf(x, y) : fmaxf(x, y); break;
+      default: r = (float)(isMin ? omin(x, y) : omax(x, y)); break;
     }
     return f2u(r);
   }
@@ -265,7 +280,7 @@ static inline uint64_t reduce2(int dt, int devop, uint64_t arg, uint64_t a, uint
     switch (kind) {
       case DEV_SUM: r = x + y; break;
       case DEV_PROD: r = x * y; break;
-      default: r = isMin ? fmin(x, y) : fmax(x, y); break;
+      default: r = isMin ? omin(x, y) : omax(x, y); break;
     }
     uint64_t u; memcpy(&u, &r, 8); return u;
   }
@@ -273,7 +288,7 @@ static inline uint64_t reduce2(int dt, int devop, uint64_t arg, uint64_t a, uint
   switch (kind) {
     case DEV_SUM: r = x + y; break;
     case DEV_PROD: r = x * y; break;
-    default: r = isMin ? fminf(x, y) : fmaxf(x, y); break;
+    default: r = (float)(isMin ? omin(x, y) : omax(x, y)); break;
   }
   return f_to_sf(dt, r);
 }

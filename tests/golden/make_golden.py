@@ -1,0 +1,173 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/*.npz — golden vectors from an INDEPENDENT numpy restatement of the
+reference's reduction semantics (not the C oracle, which these fixtures pin).
+
+Reference rules restated (NVIDIA/nccl 2.30.7):
+  - ring fold order: AllReduce block c (c = i // chunk, chunk = alignUp(divUp(count,n), 16/sizeof(T)),
+    src/device/all_reduce.h:38-66) folds ranks c+1, c+2, ..., c; ReduceScatter block d folds d+1..d
+    (reduce_scatter.h:34-55); Reduce folds root+1..root (reduce.h:34-52).
+  - every hop rounds to T (the FIFO holds T); acc_new = f(pre(x_local), acc) (common_kernel.h:83-121)
+  - Min/Max/Sum/Prod semantics of reduce_kernel.h; avg = PreMulSum(1/n) on floats, SumPostDiv on ints.
+The reference itself cannot be built or imported here (CUDA-only), so these are
+restatement vectors; the reference's own known-answer tests are checked in tests/test_oracle.py.
+
+Run: python tests/golden/make_golden.py   (rewrites the .npz files next to this script)
+"""
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def bf16_round(f32: np.ndarray) -> np.ndarray:
+    u = f32.astype(np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    nan = np.isnan(f32)
+    r[nan] = ((u[nan] >> 16) | 0x40).astype(np.uint16)
+    return r
+
+
+def bf16_to_f32(b: np.ndarray) -> np.ndarray:
+    return (b.astype(np.uint32) << 16).view(np.float32)
+
+
+def reduce_pair(kind, dtype, a, b):
+    """f(a, b) with a = pre'd local input, b = accumulator; arrays in storage representation."""
+    if dtype == "bf16":
+        x, y = bf16_to_f32(a), bf16_to_f32(b)
+        r = {"sum": x + y, "prod": x * y, "min": np.fmin(x, y), "max": np.fmax(x, y)}[kind]
+        return bf16_round(r.astype(np.float32))
+    if dtype == "f16":
+        x, y = a.view(np.float16).astype(np.float32), b.view(np.float16).astype(np.float32)
+        r = {"sum": x + y, "prod": x * y, "min": np.fmin(x, y), "max": np.fmax(x, y)}[kind]
+        return r.astype(np.float16).view(np.uint16)
+    if kind == "sum":
+        return a + b
+    if kind == "prod":
+        return a * b
+    if kind == "min":
+        return np.fmin(a, b) if a.dtype.kind == "f" else np.minimum(a, b)
+    return np.fmax(a, b) if a.dtype.kind == "f" else np.maximum(a, b)
+
+
+def pre(kind, dtype, x, n):
+    if kind != "avg" or dtype in ("i32", "u8", "i8", "u32", "i64"):
+        return x
+    if dtype == "f32":
+        return (x * np.float32(1.0 / n)).astype(np.float32)
+    if dtype == "bf16":
+        s = bf16_to_f32(bf16_round(np.array([1.0 / n], dtype=np.float32)))[0]
+        return bf16_round(bf16_to_f32(x) * s)
+    raise ValueError(dtype)
+
+
+def post(kind, dtype, x, n):
+    if kind != "avg" or dtype in ("f32", "bf16", "f16"):
+        return x
+    # exact big-integer arithmetic: |x| // n with the sign restored (truncation toward zero)
+    q = [(-(-int(v) // n) if int(v) < 0 else int(v) // n) for v in x.tolist()]
+    bits = 8 * x.dtype.itemsize
+    return np.array([v % (1 << bits) for v in q], dtype=np.uint64).astype(x.dtype.newbyteorder("=")) \
+        if x.dtype.kind == "u" else np.array([((v + (1 << (bits - 1))) % (1 << bits)) - (1 << (bits - 1))
+                                               for v in q], dtype=x.dtype)
+
+
+def fold(kind, dtype, ins, idx, first, n):
+    base = "sum" if kind == "avg" else kind
+    acc = pre(kind, dtype, ins[first][idx], n)
+    for k in range(1, n):
+        r = (first + k) % n
+        acc = reduce_pair(base, dtype, pre(kind, dtype, ins[r][idx], n), acc)
+    return post(kind, dtype, acc, n)
+
+
+NCCL_DT = {"i8": 0, "u8": 1, "i32": 2, "u32": 3, "i64": 4, "f16": 6, "f32": 7, "bf16": 9}
+NCCL_OP = {"sum": 0, "prod": 1, "max": 2, "min": 3, "avg": 4}
+ESIZE = {"i8": 1, "u8": 1, "i32": 4, "u32": 4, "i64": 8, "f16": 2, "f32": 4, "bf16": 2}
+
+
+def gen_inputs(rng, dtype, n, count):
+    if dtype == "f32":
+        return [rng.uniform(-1, 1, count).astype(np.float32) for _ in range(n)]
+    if dtype == "bf16":
+        return [bf16_round(rng.uniform(-1, 1, count).astype(np.float32)) for _ in range(n)]
+    if dtype == "f16":
+        return [rng.uniform(-1, 1, count).astype(np.float16).view(np.uint16) for _ in range(n)]
+    info = {"i8": np.int8, "u8": np.uint8, "i32": np.int32, "u32": np.uint32, "i64": np.int64}[dtype]
+    ii = np.iinfo(info)
+    out = []
+    for _ in range(n):
+        x = rng.integers(ii.min, ii.max, count, dtype=info, endpoint=True)
+        x[1::97] = ii.min
+        x[2::97] = ii.max
+        out.append(x)
+    return out
+
+
+def allreduce(kind, dtype, ins):
+    n, count = len(ins), ins[0].size
+    epp = 16 // ESIZE[dtype]
+    chunk = -(-count // n)
+    chunk = -(-chunk // epp) * epp
+    out = np.empty_like(ins[0])
+    for c in range(n):
+        lo, hi = c * chunk, min(count, (c + 1) * chunk)
+        if lo >= hi:
+            continue
+        out[lo:hi] = fold(kind, dtype, ins, slice(lo, hi), (c + 1) % n, n)
+    return out
+
+
+def reducescatter(kind, dtype, ins):
+    n = len(ins)
+    rc = ins[0].size // n
+    return [fold(kind, dtype, ins, slice(d * rc, (d + 1) * rc), (d + 1) % n, n) for d in range(n)]
+
+
+def reduce_root(kind, dtype, ins, root):
+    n = len(ins)
+    return fold(kind, dtype, ins, slice(0, ins[0].size), (root + 1) % n, n)
+
+
+CASES = [
+    ("allreduce", "sum", "f32", 2, 4099), ("allreduce", "sum", "f32", 3, 4099), ("allreduce", "sum", "f32", 8, 1037),
+    ("allreduce", "prod", "f32", 3, 999), ("allreduce", "max", "f32", 4, 999), ("allreduce", "min", "f32", 4, 999),
+    ("allreduce", "avg", "f32", 4, 2000), ("allreduce", "sum", "bf16", 4, 3001), ("allreduce", "avg", "bf16", 3, 3001),
+    ("allreduce", "sum", "f16", 3, 2049), ("allreduce", "max", "bf16", 8, 1000),
+    ("allreduce", "sum", "i32", 5, 2000), ("allreduce", "min", "i32", 5, 2000), ("allreduce", "max", "i32", 5, 2000),
+    ("allreduce", "avg", "i32", 5, 2000), ("allreduce", "sum", "u8", 3, 777), ("allreduce", "avg", "u8", 3, 777),
+    ("allreduce", "min", "i8", 4, 777), ("allreduce", "prod", "i64", 2, 500), ("allreduce", "avg", "i64", 3, 500),
+    ("reducescatter", "sum", "f32", 4, 4 * 1001), ("reducescatter", "sum", "bf16", 8, 8 * 301),
+    ("reducescatter", "max", "u32", 2, 2 * 1000),
+    ("reduce", "min", "i32", 8, 3000), ("reduce", "max", "i32", 8, 3000), ("reduce", "sum", "f32", 4, 3000),
+]
+
+
+def main():
+    rng = np.random.default_rng(20261015)
+    for f in os.listdir(HERE):
+        if f.endswith(".npz"):
+            os.remove(os.path.join(HERE, f))
+    for i, (coll, kind, dtype, n, count) in enumerate(CASES):
+        ins = gen_inputs(rng, dtype, n, count)
+        d = {"coll": coll, "dtype": NCCL_DT[dtype], "op": NCCL_OP[kind], "n": n}
+        for r, x in enumerate(ins):
+            d[f"in{r}"] = x
+        name = f"{i:02d}_{coll}_{kind}_{dtype}_n{n}"
+        if coll == "allreduce":
+            d["out"] = allreduce(kind, dtype, ins)
+        elif coll == "reducescatter":
+            for r, o in enumerate(reducescatter(kind, dtype, ins)):
+                d[f"out{r}"] = o
+        else:
+            root = 0 if kind == "min" else n // 2
+            d["root"] = root
+            d["out"] = reduce_root(kind, dtype, ins, root)
+            name += f"_root{root}"
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+    print(f"wrote {len(CASES)} fixtures to {HERE}")
+
+
+if __name__ == "__main__":
+    main()

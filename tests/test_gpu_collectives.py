@@ -89,10 +89,24 @@ def test_multi_process(built, nranks):
     ps = [ctx.Process(target=_mp_worker, args=(r, nranks, uid, nranks > 2, q)) for r in range(nranks)]
     for p in ps:
         p.start()
+    import queue
+    import time
     results = {}
-    for _ in range(nranks):
-        r, errs = q.get(timeout=900)
-        results[r] = errs
+    t0 = time.time()
+    while len(results) < nranks and time.time() - t0 < 900:
+        try:
+            r, errs = q.get(timeout=30)
+            results[r] = errs
+        except queue.Empty:
+            alive = sum(p.is_alive() for p in ps)
+            print(f"[multi_process n={nranks}] waiting: {len(results)} done, {alive} alive, {time.time() - t0:.0f}s",
+                  flush=True)
+            if alive == 0:
+                break
+    for p in ps:
+        if p.is_alive() and len(results) < nranks:
+            p.kill()
+    assert len(results) == nranks, f"only {len(results)} of {nranks} ranks reported"
     for p in ps:
         p.join(timeout=60)
     bad = [e for r in sorted(results) for e in results[r]]

@@ -1,0 +1,90 @@
+"""CPU tests of the product library's host side: the C ABI loads and exports every symbol that
+include/nccl.h declares, version / error strings / argument checks behave like the reference, and
+the TCP bootstrap works across processes. No compute call is made (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import nccl_amd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "nccl.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:ncclResult_t|const char\*)\s+(p?nccl\w+)\s*\(", src, re.M)))
+
+
+def test_exports_every_declared_symbol(built):
+    lib = nccl_amd.load()
+    names = _declared_functions()
+    assert len(names) >= 48
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the python mirror binds exactly the non-profiling set
+    assert sorted(nccl_amd.EXPORTED) == sorted(n for n in names if not n.startswith("p"))
+
+
+def test_exports_are_nccl_only(built):
+    out = subprocess.check_output(["nm", "-D", "--defined-only", nccl_amd.LIB_PATH], text=True)
+    syms = [l.split()[-1] for l in out.splitlines() if " T " in l]
+    assert syms and all(s.startswith("nccl") or s.startswith("pnccl") for s in syms), syms
+
+
+def test_version_and_error_strings(built):
+    assert nccl_amd.get_version() == 23007  # NCCL_VERSION(2,30,7), nccl.h.in:26
+    lib = nccl_amd.load()
+    assert lib.ncclGetErrorString(0) == b"no error"
+    assert lib.ncclGetErrorString(4).startswith(b"invalid argument")
+    assert lib.ncclGetErrorString(5).startswith(b"invalid usage")
+    assert lib.ncclGetErrorString(7) == b"NCCL operation in progress"
+    assert lib.ncclGetErrorString(99) == b"unknown result code"
+
+
+def test_unique_id_is_128_bytes_and_distinct(built):
+    a, b = nccl_amd.get_unique_id(), nccl_amd.get_unique_id()
+    assert len(a) == 128 and len(b) == 128 and a != b
+
+
+def test_argument_checks_without_gpu(built):
+    lib = nccl_amd.load()
+    P = ctypes.c_void_p
+    # invalid comm (NULL) -> ncclInvalidArgument (argcheck.cc:30-45)
+    assert lib.ncclAllReduce(None, None, 10, 7, 0, None, None) == 4
+    assert lib.ncclReduce(None, None, 10, 7, 0, 0, None, None) == 4
+    # bad rank count / rank (init.cc: ncclCommInitRankDev checks) before any device call
+    c = P()
+    uid = nccl_amd._uid(nccl_amd.get_unique_id())
+    assert lib.ncclCommInitRank(ctypes.byref(c), 0, uid, 0) == 4
+    assert lib.ncclCommInitRank(ctypes.byref(c), 2, uid, 2) == 4
+    assert lib.ncclCommInitRank(ctypes.byref(c), 2, uid, -1) == 4
+    # bad config magic
+    cfg = nccl_amd.Config.default()
+    cfg.magic = 0
+    assert lib.ncclCommInitRankConfig(ctypes.byref(c), 2, uid, 0, ctypes.byref(cfg)) == 4
+    # unmatched group end -> ncclInvalidUsage
+    assert lib.ncclGroupEnd() == 5
+    assert lib.ncclGroupStart() == 0 and lib.ncclGroupEnd() == 0
+    # an invalid call inside a group poisons the group (reference group.cc error propagation)
+    assert lib.ncclGroupStart() == 0
+    assert lib.ncclAllReduce(None, None, 10, 7, 0, None, None) == 4
+    assert lib.ncclGroupEnd() == 4
+    v = ctypes.c_int()
+    assert lib.ncclCommCount(None, ctypes.byref(v)) == 4
+    assert lib.ncclGetVersion(None) == 4
+    # destroying / aborting NULL is a no-op
+    assert lib.ncclCommDestroy(None) == 0 and lib.ncclCommAbort(None) == 0
+    assert b"NULL" in lib.ncclGetLastError(None) or lib.ncclGetLastError(None) != b""
+
+
+@pytest.mark.parametrize("n", [2, 5, 8])
+def test_bootstrap_across_processes(built, n):
+    exe = os.path.join(ROOT, "build", "bootstrap_test")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "bootstrap-test"], cwd=ROOT)
+    env = dict(os.environ, NCCL_AMD_BOOTSTRAP_TIMEOUT_MS="20000")
+    r = subprocess.run([exe, str(n), "4"], env=env, capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
