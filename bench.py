@@ -52,6 +52,32 @@ def hbm_bytes_per_rank(coll: str, n: int, S: int) -> int:
     raise ValueError(coll)
 
 
+def exchange_unique_id(dist, rank: int) -> bytes:
+    """Rank 0 creates the ncclUniqueId (starts the bootstrap root), every rank receives it (gloo)."""
+    import nccl_amd
+    obj = [nccl_amd.get_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def max_over_ranks(dist, values):
+    """Element-wise MAX over ranks (the contract's max-over-ranks timing)."""
+    import torch
+    if dist is None:
+        return [float(v) for v in values]
+    t = torch.tensor(values, dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def rates(n: int, S: int, ms_per_step: float):
+    """(value, algBW, busBW) in GB/s for one AllReduce of S bytes per rank taking ms_per_step."""
+    algbw = S / (ms_per_step * 1e-3) / 1e9
+    busbw = algbw * bus_factor("allreduce", n)
+    value = 2 * S / (ms_per_step * 1e-3) / 1e9 if n == 1 else n * busbw
+    return value, algbw, busbw
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -100,7 +126,8 @@ def load_pmc(workload_key: str):
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
-            return json.load(f).get(workload_key)
+            ent = json.load(f).get(workload_key)
+            return None if ent is None else ent.get("bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -121,9 +148,7 @@ def main(argv=None):
     if n > 1:
         import torch.distributed as dist
         dist.init_process_group("gloo")
-        obj = [nccl_amd.get_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm = nccl_amd.Communicator.init(n, rank, obj[0])
+        comm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
     else:
         comm = nccl_amd.Communicator.init_all([dev])[0]
 
@@ -159,10 +184,7 @@ def main(argv=None):
     t1 = time.perf_counter()
     wall = t1 - t0
     gpu_ms = e0.elapsed_time(e1) / args.steps
-    if dist is not None:
-        t = torch.tensor([wall, gpu_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall, gpu_ms = float(t[0]), float(t[1])
+    wall, gpu_ms = max_over_ranks(dist, [wall, gpu_ms])
     err = comm.async_error()
 
     # size-independent correctness property at full size: dyadic inputs => exact sums
@@ -180,18 +202,15 @@ def main(argv=None):
         ok = int(t[0]) == 0
 
     ms_per_step = wall / args.steps * 1e3
-    algbw = S / (ms_per_step * 1e-3) / 1e9
-    busbw = algbw * bus_factor("allreduce", n)
-    if n == 1:
-        value = 2 * S / (ms_per_step * 1e-3) / 1e9
-    else:
-        value = n * busbw
+    value, algbw, busbw = rates(n, S, ms_per_step)
     hbm_bytes = hbm_bytes_per_rank("allreduce", n, S)
     achieved = hbm_bytes / (gpu_ms * 1e-3) / 1e9
     wkey = f"allreduce_f32_{size_mib}MiB_n{n}"
     traffic = load_pmc(wkey)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+            "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)"
+            if traffic else None,
             "kernel": "copyKernel<4>" if n == 1 else "collKernel<float,SUM,AR>",
             "algorithmic_bytes_per_launch": hbm_bytes, "kernel_avg_ms": round(gpu_ms, 5)}
     if n > 1:

@@ -1,0 +1,61 @@
+"""world_size-2 gloo tests (CPU) of the N>1 harness path of bench.py: the ncclUniqueId created by rank 0
+(which starts this library's bootstrap root) reaches every rank intact, the max-over-ranks timing, and
+the bus-bandwidth arithmetic (reference inspector.cc:1450-1492)."""
+import multiprocessing as mp
+import os
+import socket
+
+import pytest
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        import torch.distributed as dist
+        import bench
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        uid = bench.exchange_unique_id(dist, rank)
+        ids = [None] * world
+        dist.all_gather_object(ids, uid)
+        same = all(x == ids[0] for x in ids) and len(uid) == 128
+        mx = bench.max_over_ranks(dist, [1.0 + rank, 10.0 - rank])
+        dist.destroy_process_group()
+        q.put((rank, same, mx))
+    except Exception as e:
+        q.put((rank, False, repr(e)))
+
+
+@pytest.mark.parametrize("world", [2])
+def test_gloo_harness(built, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in ps:
+        p.join(timeout=30)
+    for rank, same, mx in res:
+        assert same, (rank, mx)
+        assert mx == [float(world), 10.0], mx
+
+
+def test_rates():
+    import bench
+    S = 256 << 20
+    v, alg, bus = bench.rates(8, S, 1.0)
+    assert abs(alg - S / 1e-3 / 1e9) < 1e-6
+    assert abs(bus - alg * 2 * 7 / 8) < 1e-6 and abs(v - 8 * bus) < 1e-6
+    v1, _, bus1 = bench.rates(1, 64 << 20, 1.0)
+    assert bus1 == 0 and abs(v1 - 2 * (64 << 20) / 1e-3 / 1e9) < 1e-6
+    assert bench.hbm_bytes_per_rank("allreduce", 8, S) == int(2 * S + 4 * 7 * S / 8)
+    assert bench.bus_factor("reducescatter", 4) == 0.75 and bench.bus_factor("reduce", 4) == 1.0
