@@ -16,7 +16,8 @@ COMMON   := -O3 -fPIC -std=c++17 -ffp-contract=off -fvisibility=hidden -Wall -Wn
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics
 HOSTSRC  := debug.cc bootstrap.cc transport.cc init.cc group.cc enqueue.cc
 HOSTOBJ  := $(HOSTSRC:%.cc=$(BUILD)/%.o)
-DEVOBJ   := $(BUILD)/kernels.o
+DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
+DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
 all: lib oracle numerics-host bootstrap-test
@@ -27,7 +28,7 @@ $(BUILD)/%.o: $(SRCDIR)/%.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	$(CXX) $(COMMON) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c $< -o $@
 
-$(BUILD)/kernels.o: $(SRCDIR)/kernels.hip $(HDRS)
+$(BUILD)/%.o: $(SRCDIR)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -1,0 +1,492 @@
+// kernels.h — gfx950 device code of the reduction engine (templates; instantiated per element type in
+// kern_<type>.hip so the kernels build in parallel) + the typed launch templates.
+//
+// Replaces the reference's device tree src/device/ (runRing in all_reduce.h / reduce_scatter.h /
+// all_gather.h / reduce.h, Primitives<ProtoSimple> in prims_simple.h, reduceCopy in
+// common_kernel.h, oneRankReduce in onerank.cu). It is NOT a ring: every MI355X of the node has a
+// direct xGMI link to every other one, so the buffer is cut into nRanks blocks (block q owned by
+// rank q) and each rank
+//   A  scatters block q of its input to owner q's staging (n-1 remote write streams, one per link),
+//   B  folds the n contributions of its own block in the reference's ring order (owner+1, ...,
+//      owner; per-hop rounding to T) and pushes the result to every peer's all-gather staging,
+//   C  copies the n-1 gathered blocks from its own staging into the output.
+// Each workgroup is an independent "channel" (reference: one CTA per channel) that pipelines its
+// part of every block in slices through nSlots staging slots per peer, with per-connection credit
+// counters exactly like the reference's head/tail protocol (prims_simple.h:100-173), but
+// bidirectional over all 7 links at once instead of one ring neighbour.
+//
+// Memory model: remote payload = `global_store_dwordx4 ... sc0 sc1` (system-scope
+// write-through) into the peer's UNCACHED staging; every storing wave drains (s_waitcnt vmcnt(0)),
+// the workgroup barriers, one lane issues a system release fence and then a system-scope flag
+// store. The consumer polls its local flag with system-scope loads (one wave, s_sleep between polls,
+// bounded by NCCL_AMD_SPIN_TIMEOUT_MS and the host abort word), then one system acquire
+// (buffer_inv sc0 sc1), vmcnt(0), barrier, plain loads.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "core.h"
+#include "numerics.h"
+
+namespace ncclamd {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kThreads = 512;  // 8 waves of 64 per channel workgroup
+
+// ------------------------------------------------------------------------------------ primitives
+
+__device__ __forceinline__ uint64_t clockTicks() { return __builtin_amdgcn_s_memrealtime(); }
+
+__device__ __forceinline__ void storeRemote(void* p, u32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void drainStores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ uint64_t loadFlag(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void storeFlag(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ void reportError(const DevComm& dc, uint32_t code) {
+  uint32_t expected = 0;
+  __hip_atomic_compare_exchange_strong(dc.errorWord, &expected, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Block-wide state kept in LDS.
+struct ChanState {
+  uint64_t ctr[CTR_KINDS][NCCL_AMD_MAX_RANKS];
+  int abort;
+};
+
+
+// Wave 0 waits until every selected flag word reaches its target (target[r] == 0: no wait on r).
+// ACQ: follow with a system-scope acquire (needed before reading data the flags publish; not for
+// credit/ack words, which guard no data). All threads must call it (it ends in a barrier).
+template <bool ACQ>
+__device__ bool waitAll(const DevComm& dc, ChanState& st, const uint64_t* flagBase, const uint64_t* target) {
+  if (threadIdx.x < 64) {
+    int lane = threadIdx.x;
+    bool need = lane < dc.nRanks && target[lane] != 0;
+    uint64_t t0 = 0;
+    uint32_t iter = 0;
+    while (true) {
+      bool ok = !need || loadFlag(flagBase + lane) >= target[lane];
+      if (__all(ok)) break;
+      if (iter == 0) t0 = clockTicks();
+      __builtin_amdgcn_s_sleep(1);
+      if ((++iter & 255) == 0) {
+        bool bad = false;
+        if (__hip_atomic_load(dc.abortFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          if (lane == 0) reportError(dc, DERR_ABORT);
+          bad = true;
+        } else if (__hip_atomic_load(dc.errorWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          bad = true;  // another workgroup already failed: stop waiting
+        } else if (clockTicks() - t0 > dc.timeoutTicks) {
+          if (lane == 0) reportError(dc, DERR_TIMEOUT);
+          bad = true;
+        }
+        if (bad) {
+          if (lane == 0) st.abort = 1;
+          break;
+        }
+      }
+    }
+    if (ACQ && lane == 0) __atomic_thread_fence(__ATOMIC_ACQUIRE);  // buffer_inv sc0 sc1 (system acquire)
+    drainStores();
+  }
+  __syncthreads();
+  return st.abort == 0;
+}
+
+// Every wave drains its memory operations, then wave-0 lane i stores val[i] into ptr[i] (val 0 = skip)
+// with a system-scope store. REL: precede with a system release fence (publishing data); without it
+// the stores are credits/acks: our loads of the consumed slot have completed (vmcnt(0)) and nothing
+// we wrote needs to be visible.
+template <bool REL>
+__device__ void signalAll(uint64_t* const* ptr, const uint64_t* val, int nsig) {
+  drainStores();
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    int lane = threadIdx.x;
+    if (REL) {
+      __atomic_thread_fence(__ATOMIC_RELEASE);  // buffer_wbl2 sc0 sc1 + vmcnt(0)
+      drainStores();                            // kept explicit: see MI355X_MICROARCH "Compiler hazard"
+    }
+    if (lane < nsig && val[lane] != 0) storeFlag(ptr[lane], val[lane]);
+  }
+}
+
+// ------------------------------------------------------------------------------------ data movement
+
+// Copy [0,nbytes) from src to dst. Both 16-byte aligned when `aligned`; nbytes multiple of sizeof(T).
+template <typename T, bool REMOTE>
+__device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t nbytes, bool aligned) {
+  if (aligned) {
+    uint64_t npk = nbytes >> 4;
+    const u32x4* s = (const u32x4*)src;
+    u32x4* d = (u32x4*)dst;
+    constexpr int U = 4;
+    uint64_t i = threadIdx.x;
+    for (; i + (U - 1) * kThreads < npk; i += U * kThreads) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s + i + u * kThreads);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        if (REMOTE) storeRemote(d + i + u * kThreads, v[u]);
+        else d[i + u * kThreads] = v[u];
+      }
+    }
+    for (; i < npk; i += kThreads) {
+      u32x4 v = __builtin_nontemporal_load(s + i);
+      if (REMOTE) storeRemote(d + i, v);
+      else d[i] = v;
+    }
+    uint64_t done = npk << 4;
+    uint64_t tail = (nbytes - done) / sizeof(T);
+    if (threadIdx.x < tail) {
+      const T* st = (const T*)((const char*)src + done);
+      T* dt = (T*)((char*)dst + done);
+      dt[threadIdx.x] = st[threadIdx.x];
+    }
+  } else {
+    uint64_t n = nbytes / sizeof(T);
+    const T* s = (const T*)src;
+    T* d = (T*)dst;
+    for (uint64_t i = threadIdx.x; i < n; i += kThreads) d[i] = s[i];
+  }
+}
+
+template <typename T>
+union PackU {
+  u32x4 v;
+  T e[16 / sizeof(T)];
+};
+
+// Fold n sources into dst (and optionally into nPush remote copies). src[k] is the k-th source in
+// fold order: acc = pre(src[0]); acc = red(pre(src[k]), acc) ...; out = post(acc).
+template <typename T, int OP>
+__device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const void* const* src, uint64_t nelem,
+                                          void* dstLocal, void* const* dstPush, int nPush, bool aligned) {
+  constexpr int EPP = 16 / sizeof(T);
+  if (aligned) {
+    uint64_t npk = nelem / EPP;
+    for (uint64_t i = threadIdx.x; i < npk; i += kThreads) {
+      PackU<T> v[NCCL_AMD_MAX_RANKS];
+#pragma unroll
+      for (int k = 0; k < NCCL_AMD_MAX_RANKS; k++)
+        if (k < n) v[k].v = __builtin_nontemporal_load((const u32x4*)src[k] + i);
+      PackU<T> acc;
+#pragma unroll
+      for (int e = 0; e < EPP; e++) acc.e[e] = fn.pre(v[0].e[e]);
+#pragma unroll
+      for (int k = 1; k < NCCL_AMD_MAX_RANKS; k++)
+        if (k < n) {
+#pragma unroll
+          for (int e = 0; e < EPP; e++) acc.e[e] = fn.red(fn.pre(v[k].e[e]), acc.e[e]);
+        }
+#pragma unroll
+      for (int e = 0; e < EPP; e++) acc.e[e] = fn.post(acc.e[e]);
+      if (dstLocal) ((u32x4*)dstLocal)[i] = acc.v;
+#pragma unroll
+      for (int p = 0; p < NCCL_AMD_MAX_RANKS - 1; p++)
+        if (p < nPush) storeRemote((u32x4*)dstPush[p] + i, acc.v);
+    }
+    uint64_t done = npk * EPP;
+    uint64_t t = done + threadIdx.x;
+    if (t < nelem) {
+      T acc = fn.pre(((const T*)src[0])[t]);
+      for (int k = 1; k < n; k++) acc = fn.red(fn.pre(((const T*)src[k])[t]), acc);
+      acc = fn.post(acc);
+      if (dstLocal) ((T*)dstLocal)[t] = acc;
+      for (int p = 0; p < nPush; p++) ((T*)dstPush[p])[t] = acc;  // < 16 B: plain store, fenced below
+    }
+  } else {
+    for (uint64_t t = threadIdx.x; t < nelem; t += kThreads) {
+      T acc = fn.pre(((const T*)src[0])[t]);
+      for (int k = 1; k < n; k++) acc = fn.red(fn.pre(((const T*)src[k])[t]), acc);
+      acc = fn.post(acc);
+      if (dstLocal) ((T*)dstLocal)[t] = acc;
+      for (int p = 0; p < nPush; p++) ((T*)dstPush[p])[t] = acc;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------ collective kernel
+
+enum Coll { COLL_AR = 0, COLL_RS = 1, COLL_AG = 2, COLL_REDUCE = 3 };
+
+// Element range [lo,hi) of a block handled by channel c at pipeline step s (offsets inside the block).
+__device__ __forceinline__ void sliceRange(const CollArgs& a, int c, int s, uint64_t blockLen, uint64_t& lo,
+                                           uint64_t& hi) {
+  uint64_t pEnd = min((uint64_t)(c + 1) * a.part, blockLen);
+  lo = min((uint64_t)c * a.part + (uint64_t)s * a.slice, pEnd);
+  hi = min(lo + a.slice, pEnd);
+}
+
+// Per-workgroup (channel) LDS scratch for the handshake arrays.
+struct Shared {
+  ChanState st;
+  uint64_t want[NCCL_AMD_MAX_RANKS];
+  uint64_t* sigPtr[2 * NCCL_AMD_MAX_RANKS];
+  uint64_t sigVal[2 * NCCL_AMD_MAX_RANKS];
+};
+
+template <typename T, int OP, int COLL>
+struct Channel {
+  const CollArgs& a;
+  const DevComm& dc;
+  Shared& sh;
+  const Red<T, OP>& fn;
+  int c, me, n, nSlots;
+  bool aligned, isRoot;
+  static constexpr uint64_t ts = sizeof(T);
+
+  __device__ uint64_t blockLen(int q) const {
+    if (COLL == COLL_AR || COLL == COLL_REDUCE) {
+      uint64_t b = (uint64_t)q * a.chunk;
+      return b >= a.count ? 0 : min(a.chunk, a.count - b);
+    }
+    return a.chunk;
+  }
+  __device__ uint64_t& ctr(int k, int r) const { return sh.st.ctr[k][r]; }
+  __device__ const uint64_t* myFlags(int kind) const { return dc.flags[me] + flagIndex(c, kind, 0); }
+  __device__ bool pushesTo(int p) const {
+    if (COLL == COLL_AR || COLL == COLL_AG) return true;
+    return COLL == COLL_REDUCE && !isRoot && p == a.root;
+  }
+
+  // A: scatter input block p to owner p's RS staging (AR, RS, REDUCE)
+  __device__ bool phaseA(int step) {
+    int tid = threadIdx.x;
+    if (tid < NCCL_AMD_MAX_RANKS) {
+      uint64_t s = ctr(CTR_SEND_RS, tid);
+      sh.want[tid] = (tid < n && tid != me && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
+    }
+    __syncthreads();
+    if (!waitAll<false>(dc, sh.st, myFlags(FLG_RS_ACK), sh.want)) return false;
+    for (int k = 1; k < n; k++) {
+      int p = (me + k) % n;
+      uint64_t lo, hi;
+      sliceRange(a, c, step, blockLen(p), lo, hi);
+      int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
+      char* dst = dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me);
+      const char* src = (const char*)a.sendbuff + ((uint64_t)p * a.chunk + lo) * ts;
+      copyRange<T, true>(dst, src, (hi - lo) * ts, aligned);
+    }
+    if (tid < NCCL_AMD_MAX_RANKS) {
+      bool act = tid < n && tid != me;
+      sh.sigVal[tid] = act ? ctr(CTR_SEND_RS, tid) + 1 : 0;
+      sh.sigPtr[tid] = act ? dc.flags[tid] + flagIndex(c, FLG_RS_READY, me) : nullptr;
+    }
+    __syncthreads();
+    signalAll<true>(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS);
+    if (tid < n && tid != me) ctr(CTR_SEND_RS, tid)++;
+    __syncthreads();
+    return true;
+  }
+
+  // B: fold my block (AR, RS, REDUCE) or publish my input block (AG); push to AG staging
+  __device__ bool phaseB(int step) {
+    int tid = threadIdx.x;
+    const bool push = (COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && !isRoot));
+    if (COLL != COLL_AG) {
+      if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
+      __syncthreads();
+      if (!waitAll<true>(dc, sh.st, myFlags(FLG_RS_READY), sh.want)) return false;
+    }
+    if (push) {
+      if (tid < NCCL_AMD_MAX_RANKS) {
+        uint64_t s = ctr(CTR_SEND_AG, tid);
+        bool dstPeer = tid < n && tid != me && pushesTo(tid);
+        sh.want[tid] = (dstPeer && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
+      }
+      __syncthreads();
+      if (!waitAll<false>(dc, sh.st, myFlags(FLG_AG_ACK), sh.want)) return false;
+    }
+    uint64_t lo, hi;
+    sliceRange(a, c, step, blockLen(me), lo, hi);
+    const uint64_t nelem = hi - lo;
+    void* dstPush[NCCL_AMD_MAX_RANKS];
+    int nPush = 0;
+    for (int k = 1; k < n; k++) {
+      int p = (me + k) % n;
+      if (pushesTo(p)) {
+        int slot = (int)(ctr(CTR_SEND_AG, p) % nSlots);
+        dstPush[nPush++] = dc.staging[p] + stagingOffset(dc, c, STG_AG, slot, me);
+      }
+    }
+    if (COLL == COLL_AG) {
+      const char* src = (const char*)a.sendbuff + lo * ts;
+      for (int i = 0; i < nPush; i++) copyRange<T, true>(dstPush[i], src, nelem * ts, aligned);
+      char* dst = (char*)a.recvbuff + ((uint64_t)me * a.chunk + lo) * ts;
+      if (dst != src) copyRange<T, false>(dst, src, nelem * ts, aligned);
+    } else {
+      // fold order: owner+1, ..., owner (AR/RS, all_reduce.h:43-66) or root+1, ..., root (reduce.h:34-52)
+      int first = (COLL == COLL_REDUCE ? a.root + 1 : me + 1) % n;
+      const void* src[NCCL_AMD_MAX_RANKS];
+      for (int k = 0; k < n; k++) {
+        int q = (first + k) % n;
+        if (q == me) src[k] = (const char*)a.sendbuff + ((uint64_t)me * a.chunk + lo) * ts;
+        else src[k] = dc.staging[me] + stagingOffset(dc, c, STG_RS, (int)(ctr(CTR_RECV_RS, q) % nSlots), q);
+      }
+      void* dstLocal = nullptr;
+      if (COLL == COLL_RS) dstLocal = (char*)a.recvbuff + lo * ts;
+      else if (COLL == COLL_AR || isRoot) dstLocal = (char*)a.recvbuff + ((uint64_t)me * a.chunk + lo) * ts;
+      foldRange<T, OP>(fn, n, src, nelem, dstLocal, dstPush, nPush, aligned);
+    }
+    // one release covers both: AG data ready at each destination; RS slots consumed (ack to senders)
+    if (tid < NCCL_AMD_MAX_RANKS) {
+      bool peer = tid < n && tid != me;
+      bool dstPeer = peer && push && pushesTo(tid);
+      sh.sigVal[tid] = dstPeer ? ctr(CTR_SEND_AG, tid) + 1 : 0;
+      sh.sigPtr[tid] = dstPeer ? dc.flags[tid] + flagIndex(c, FLG_AG_READY, me) : nullptr;
+      bool ack = peer && COLL != COLL_AG;
+      sh.sigVal[NCCL_AMD_MAX_RANKS + tid] = ack ? ctr(CTR_RECV_RS, tid) + 1 : 0;
+      sh.sigPtr[NCCL_AMD_MAX_RANKS + tid] = ack ? dc.flags[tid] + flagIndex(c, FLG_RS_ACK, me) : nullptr;
+    }
+    __syncthreads();
+    if (push) signalAll<true>(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS);
+    else signalAll<false>(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS);
+    if (tid < n && tid != me) {
+      if (COLL != COLL_AG) ctr(CTR_RECV_RS, tid)++;
+      if (push && pushesTo(tid)) ctr(CTR_SEND_AG, tid)++;
+    }
+    __syncthreads();
+    return true;
+  }
+
+  // C: gather the other blocks from my AG staging into the output (AR, AG, REDUCE at root)
+  __device__ bool phaseC(int step) {
+    int tid = threadIdx.x;
+    if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_AG, tid) + 1 : 0;
+    __syncthreads();
+    if (!waitAll<true>(dc, sh.st, myFlags(FLG_AG_READY), sh.want)) return false;
+    for (int k = 1; k < n; k++) {
+      int q = (me + n - k) % n;
+      uint64_t lo, hi;
+      sliceRange(a, c, step, blockLen(q), lo, hi);
+      const char* src = dc.staging[me] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_RECV_AG, q) % nSlots), q);
+      char* dst = (char*)a.recvbuff + ((uint64_t)q * a.chunk + lo) * ts;
+      copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
+    }
+    if (tid < NCCL_AMD_MAX_RANKS) {
+      bool peer = tid < n && tid != me;
+      sh.sigVal[tid] = peer ? ctr(CTR_RECV_AG, tid) + 1 : 0;
+      sh.sigPtr[tid] = peer ? dc.flags[tid] + flagIndex(c, FLG_AG_ACK, me) : nullptr;
+    }
+    __syncthreads();
+    signalAll<false>(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS);  // credits only
+    if (tid < n && tid != me) ctr(CTR_RECV_AG, tid)++;
+    __syncthreads();
+    return true;
+  }
+};
+
+template <typename T, int OP, int COLL>
+__global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
+  __shared__ Shared sh;
+  const DevComm& dc = *a.comm;
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x;
+  if (tid < CTR_KINDS * NCCL_AMD_MAX_RANKS) {
+    int k = tid / NCCL_AMD_MAX_RANKS, r = tid % NCCL_AMD_MAX_RANKS;
+    sh.st.ctr[k][r] = dc.counters[ctrIndex(c, k, r)];
+  }
+  if (tid == 0) sh.st.abort = 0;
+  __syncthreads();
+
+  uint64_t opArg = a.redArg;
+  if (a.redArgPtr) {  // ncclScalarDevice PreMulSum: dereference at run time (reference onerank.cu:31-41)
+    opArg = 0;
+    __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
+  }
+  const Red<T, OP> fn(opArg);
+  Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
+                          (COLL != COLL_REDUCE) || dc.rank == a.root};
+  constexpr bool hasA = COLL != COLL_AG;
+  const bool hasC = COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && ch.isRoot);
+  // Pipeline: A(0); for s: B(s); A(s+1); C(s). Hoisting A(s+1) above C(s) lets the owners start
+  // reducing step s+1 while this rank still drains step s (they are independent).
+  bool ok = !hasA || a.nSteps == 0 || ch.phaseA(0);
+  for (int s = 0; ok && s < a.nSteps; s++) {
+    ok = ch.phaseB(s);
+    if (ok && hasA && s + 1 < a.nSteps) ok = ch.phaseA(s + 1);
+    if (ok && hasC) ok = ch.phaseC(s);
+  }
+  __syncthreads();
+  if (tid < CTR_KINDS * NCCL_AMD_MAX_RANKS) {
+    int k = tid / NCCL_AMD_MAX_RANKS, r = tid % NCCL_AMD_MAX_RANKS;
+    dc.counters[ctrIndex(c, k, r)] = sh.st.ctr[k][r];
+  }
+}
+
+// ------------------------------------------------------------------------------------ nRanks == 1
+
+// PreMulSum on one rank (reference onerank.cu:14-47): out = post(pre(in)).
+template <typename T, int OP>
+__global__ void __launch_bounds__(256) oneRankKernel(T* dst, const T* src, uint64_t n, uint64_t arg,
+                                                     const void* argPtr) {
+  uint64_t a = arg;
+  if (argPtr) {
+    a = 0;
+    __builtin_memcpy(&a, argPtr, sizeof(T));
+  }
+  const Red<T, OP> fn(a);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    dst[i] = fn.post(fn.pre(src[i]));
+}
+
+// ------------------------------------------------------------------------------------ host launcher
+
+template <typename T, int OP>
+inline ncclResult_t launchTyped(const LaunchPlan& p) {
+  if (p.algo == ALGO_ONERANK) {
+    int grid = (int)std::min<uint64_t>(1024, (p.args.count + 255) / 256);
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((oneRankKernel<T, OP>), dim3(grid), dim3(256), 0, p.stream, (T*)p.args.recvbuff,
+                       (const T*)p.args.sendbuff, p.args.count, p.args.redArg, p.args.redArgPtr);
+    HIPCHECK(hipGetLastError());
+    return ncclSuccess;
+  }
+  switch (p.func) {
+    case FUNC_ALLREDUCE:
+      hipLaunchKernelGGL((collKernel<T, OP, COLL_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      break;
+    case FUNC_REDUCESCATTER:
+      hipLaunchKernelGGL((collKernel<T, OP, COLL_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      break;
+    case FUNC_REDUCE:
+      hipLaunchKernelGGL((collKernel<T, OP, COLL_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      break;
+    case FUNC_ALLGATHER:
+      hipLaunchKernelGGL((collKernel<T, 0, COLL_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      break;
+  }
+  HIPCHECK(hipGetLastError());
+  return ncclSuccess;
+}
+
+template <typename T>
+inline ncclResult_t launchOp(const LaunchPlan& p) {
+  switch (p.devOp) {
+    case DEV_SUM: return launchTyped<T, DEV_SUM>(p);
+    case DEV_PROD: return launchTyped<T, DEV_PROD>(p);
+    case DEV_MINMAX: return launchTyped<T, DEV_MINMAX>(p);
+    case DEV_PREMULSUM: return launchTyped<T, DEV_PREMULSUM>(p);
+    default: break;
+  }
+  WARN("internal: op %d unsupported for this type", p.devOp);
+  return ncclInternalError;
+}
+template <typename T>
+inline ncclResult_t launchIntOp(const LaunchPlan& p) {
+  if (p.devOp == DEV_SUMPOSTDIV) return launchTyped<T, DEV_SUMPOSTDIV>(p);
+  return launchOp<T>(p);
+}
+
+}  // namespace ncclamd
