@@ -195,7 +195,13 @@ def main(argv=None):
     step()
     torch.cuda.synchronize()
     want = base * (n * (n + 1) / 2)
-    ok = bool(torch.equal(recv, want)) and err == 0
+    err2 = comm.async_error()
+    ok = bool(torch.equal(recv, want)) and err == 0 and err2 == 0
+    if not ok:
+        bad = (recv != want).nonzero().flatten()
+        print(f"[rank {rank}] CHECK FAILED: async errors {err}/{err2}, {bad.numel()} mismatches of {count}; "
+              f"first idx {bad[:8].tolist()} got {recv[bad[:4]].tolist()} want {want[bad[:4]].tolist()}; "
+              f"block size {count // n}", file=sys.stderr, flush=True)
     if dist is not None:
         t = torch.tensor([0 if ok else 1], dtype=torch.int32)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -21,7 +21,7 @@
 #include <stdint.h>
 
 #define NCCL_AMD_MAX_RANKS 16
-#define NCCL_AMD_MAX_CHANNELS 128
+#define NCCL_AMD_MAX_CHANNELS 256
 
 namespace ncclamd {
 
@@ -64,6 +64,7 @@ struct CollArgs {
   int nSteps;
   int root;
   int aligned;         // send/recv base pointers are 16-byte aligned
+  int protoFlags;      // NCCL_AMD_PROTO_FLAGS diagnostics (kernels.h collKernel)
 };
 
 __host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int kind, int slot, int from) {

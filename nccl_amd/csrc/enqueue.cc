@@ -198,7 +198,9 @@ ncclResult_t launchColl(const CollInfo& info) {
   uintptr_t bases = (uintptr_t)info.sendbuff | (uintptr_t)info.recvbuff;
   bool aligned = (bases & 15) == 0;
   if (info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER) aligned = aligned && ((count * ts) & 15) == 0;
+  if (paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0)) aligned = false;  // diagnostics: T-sized accesses only
   p.args.aligned = aligned ? 1 : 0;
+  p.args.protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0);
   planChannels(comm, blockElems * ts, ts, p);
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,

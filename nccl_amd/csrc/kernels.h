@@ -66,8 +66,8 @@ struct ChanState {
 // Wave 0 waits until every selected flag word reaches its target (target[r] == 0: no wait on r).
 // ACQ: follow with a system-scope acquire (needed before reading data the flags publish; not for
 // credit/ack words, which guard no data). All threads must call it (it ends in a barrier).
-template <bool ACQ>
-__device__ bool waitAll(const DevComm& dc, ChanState& st, const uint64_t* flagBase, const uint64_t* target) {
+__device__ bool waitAll(const DevComm& dc, ChanState& st, const uint64_t* flagBase, const uint64_t* target,
+                        bool ACQ) {
   if (threadIdx.x < 64) {
     int lane = threadIdx.x;
     bool need = lane < dc.nRanks && target[lane] != 0;
@@ -106,8 +106,7 @@ __device__ bool waitAll(const DevComm& dc, ChanState& st, const uint64_t* flagBa
 // with a system-scope store. REL: precede with a system release fence (publishing data); without it
 // the stores are credits/acks: our loads of the consumed slot have completed (vmcnt(0)) and nothing
 // we wrote needs to be visible.
-template <bool REL>
-__device__ void signalAll(uint64_t* const* ptr, const uint64_t* val, int nsig) {
+__device__ void signalAll(uint64_t* const* ptr, const uint64_t* val, int nsig, bool REL) {
   drainStores();
   __syncthreads();
   if (threadIdx.x < 64) {
@@ -169,41 +168,60 @@ union PackU {
 
 // Fold n sources into dst (and optionally into nPush remote copies). src[k] is the k-th source in
 // fold order: acc = pre(src[0]); acc = red(pre(src[k]), acc) ...; out = post(acc).
+// Source/destination pointer lists live in LDS (uniform, read by broadcast). Each thread owns U packs
+// per batch and walks the sources with the next source's loads in flight while it reduces the
+// current one (U*16 B x 2 per lane outstanding), so memory parallelism does not depend on n and the
+// per-source loop needs no predication.
 template <typename T, int OP>
-__device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const void* const* src, uint64_t nelem,
-                                          void* dstLocal, void* const* dstPush, int nPush, bool aligned) {
+__device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const char* const* src, uint64_t nelem,
+                                          char* dstLocal, char* const* dstPush, int nPush, bool aligned) {
   constexpr int EPP = 16 / sizeof(T);
+  constexpr int U = 4;
   if (aligned) {
-    uint64_t npk = nelem / EPP;
-    for (uint64_t i = threadIdx.x; i < npk; i += kThreads) {
-      PackU<T> v[NCCL_AMD_MAX_RANKS];
+    const uint64_t npk = nelem / EPP;
+    for (uint64_t base = threadIdx.x; base < npk; base += (uint64_t)U * kThreads) {
+      PackU<T> acc[U], cur[U], nxt[U];
 #pragma unroll
-      for (int k = 0; k < NCCL_AMD_MAX_RANKS; k++)
-        if (k < n) v[k].v = __builtin_nontemporal_load((const u32x4*)src[k] + i);
-      PackU<T> acc;
+      for (int u = 0; u < U; u++) {
+        uint64_t i = base + (uint64_t)u * kThreads;
+        if (i < npk) cur[u].v = __builtin_nontemporal_load((const u32x4*)src[0] + i);
+      }
+      for (int k = 0; k < n; k++) {
+        if (k + 1 < n) {
+          const u32x4* s = (const u32x4*)src[k + 1];
 #pragma unroll
-      for (int e = 0; e < EPP; e++) acc.e[e] = fn.pre(v[0].e[e]);
-#pragma unroll
-      for (int k = 1; k < NCCL_AMD_MAX_RANKS; k++)
-        if (k < n) {
-#pragma unroll
-          for (int e = 0; e < EPP; e++) acc.e[e] = fn.red(fn.pre(v[k].e[e]), acc.e[e]);
+          for (int u = 0; u < U; u++) {
+            uint64_t i = base + (uint64_t)u * kThreads;
+            if (i < npk) nxt[u].v = __builtin_nontemporal_load(s + i);
+          }
         }
 #pragma unroll
-      for (int e = 0; e < EPP; e++) acc.e[e] = fn.post(acc.e[e]);
-      if (dstLocal) ((u32x4*)dstLocal)[i] = acc.v;
+        for (int u = 0; u < U; u++) {
 #pragma unroll
-      for (int p = 0; p < NCCL_AMD_MAX_RANKS - 1; p++)
-        if (p < nPush) storeRemote((u32x4*)dstPush[p] + i, acc.v);
+          for (int e = 0; e < EPP; e++) {
+            T x = fn.pre(cur[u].e[e]);
+            acc[u].e[e] = k == 0 ? x : fn.red(x, acc[u].e[e]);
+          }
+          cur[u] = nxt[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t i = base + (uint64_t)u * kThreads;
+        if (i >= npk) continue;
+#pragma unroll
+        for (int e = 0; e < EPP; e++) acc[u].e[e] = fn.post(acc[u].e[e]);
+        if (dstLocal) ((u32x4*)dstLocal)[i] = acc[u].v;
+        for (int p = 0; p < nPush; p++) storeRemote((u32x4*)dstPush[p] + i, acc[u].v);
+      }
     }
-    uint64_t done = npk * EPP;
-    uint64_t t = done + threadIdx.x;
+    const uint64_t t = npk * EPP + threadIdx.x;  // < 16-byte tail of the range
     if (t < nelem) {
       T acc = fn.pre(((const T*)src[0])[t]);
       for (int k = 1; k < n; k++) acc = fn.red(fn.pre(((const T*)src[k])[t]), acc);
       acc = fn.post(acc);
       if (dstLocal) ((T*)dstLocal)[t] = acc;
-      for (int p = 0; p < nPush; p++) ((T*)dstPush[p])[t] = acc;  // < 16 B: plain store, fenced below
+      for (int p = 0; p < nPush; p++) ((T*)dstPush[p])[t] = acc;  // plain store, covered by the release
     }
   } else {
     for (uint64_t t = threadIdx.x; t < nelem; t += kThreads) {
@@ -215,6 +233,7 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const voi
     }
   }
 }
+
 
 // ------------------------------------------------------------------------------------ collective kernel
 
@@ -231,6 +250,9 @@ __device__ __forceinline__ void sliceRange(const CollArgs& a, int c, int s, uint
 // Per-workgroup (channel) LDS scratch for the handshake arrays.
 struct Shared {
   ChanState st;
+  const char* srcPtr[NCCL_AMD_MAX_RANKS];   // phase-B fold sources, in fold order
+  char* pushPtr[NCCL_AMD_MAX_RANKS];        // phase-B remote destinations
+  int nPush;
   uint64_t want[NCCL_AMD_MAX_RANKS];
   uint64_t* sigPtr[2 * NCCL_AMD_MAX_RANKS];
   uint64_t sigVal[2 * NCCL_AMD_MAX_RANKS];
@@ -243,7 +265,7 @@ struct Channel {
   Shared& sh;
   const Red<T, OP>& fn;
   int c, me, n, nSlots;
-  bool aligned, isRoot;
+  bool aligned, isRoot, forceAcq, forceRel;
   static constexpr uint64_t ts = sizeof(T);
 
   __device__ uint64_t blockLen(int q) const {
@@ -268,7 +290,7 @@ struct Channel {
       sh.want[tid] = (tid < n && tid != me && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
     }
     __syncthreads();
-    if (!waitAll<false>(dc, sh.st, myFlags(FLG_RS_ACK), sh.want)) return false;
+    if (!waitAll(dc, sh.st, myFlags(FLG_RS_ACK), sh.want, forceAcq)) return false;
     for (int k = 1; k < n; k++) {
       int p = (me + k) % n;
       uint64_t lo, hi;
@@ -284,7 +306,7 @@ struct Channel {
       sh.sigPtr[tid] = act ? dc.flags[tid] + flagIndex(c, FLG_RS_READY, me) : nullptr;
     }
     __syncthreads();
-    signalAll<true>(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS);
+    signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, true);
     if (tid < n && tid != me) ctr(CTR_SEND_RS, tid)++;
     __syncthreads();
     return true;
@@ -297,7 +319,7 @@ struct Channel {
     if (COLL != COLL_AG) {
       if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
       __syncthreads();
-      if (!waitAll<true>(dc, sh.st, myFlags(FLG_RS_READY), sh.want)) return false;
+      if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, true)) return false;
     }
     if (push) {
       if (tid < NCCL_AMD_MAX_RANKS) {
@@ -306,38 +328,38 @@ struct Channel {
         sh.want[tid] = (dstPeer && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
       }
       __syncthreads();
-      if (!waitAll<false>(dc, sh.st, myFlags(FLG_AG_ACK), sh.want)) return false;
+      if (!waitAll(dc, sh.st, myFlags(FLG_AG_ACK), sh.want, forceAcq)) return false;
     }
     uint64_t lo, hi;
     sliceRange(a, c, step, blockLen(me), lo, hi);
     const uint64_t nelem = hi - lo;
-    void* dstPush[NCCL_AMD_MAX_RANKS];
-    int nPush = 0;
-    for (int k = 1; k < n; k++) {
-      int p = (me + k) % n;
-      if (pushesTo(p)) {
-        int slot = (int)(ctr(CTR_SEND_AG, p) % nSlots);
-        dstPush[nPush++] = dc.staging[p] + stagingOffset(dc, c, STG_AG, slot, me);
+    if (tid == 0) {
+      int np = 0;
+      for (int k = 1; k < n; k++) {
+        int p = (me + k) % n;
+        if (pushesTo(p))
+          sh.pushPtr[np++] = dc.staging[p] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_SEND_AG, p) % nSlots), me);
+      }
+      sh.nPush = np;
+      // fold order: owner+1, ..., owner (AR/RS, all_reduce.h:43-66) or root+1, ..., root (reduce.h:34-52)
+      int first = (COLL == COLL_REDUCE ? a.root + 1 : me + 1) % n;
+      for (int k = 0; k < n; k++) {
+        int q = (first + k) % n;
+        sh.srcPtr[k] = q == me ? (const char*)a.sendbuff + ((uint64_t)me * a.chunk + lo) * ts
+                               : dc.staging[me] + stagingOffset(dc, c, STG_RS, (int)(ctr(CTR_RECV_RS, q) % nSlots), q);
       }
     }
+    __syncthreads();
     if (COLL == COLL_AG) {
       const char* src = (const char*)a.sendbuff + lo * ts;
-      for (int i = 0; i < nPush; i++) copyRange<T, true>(dstPush[i], src, nelem * ts, aligned);
+      for (int i = 0; i < sh.nPush; i++) copyRange<T, true>(sh.pushPtr[i], src, nelem * ts, aligned);
       char* dst = (char*)a.recvbuff + ((uint64_t)me * a.chunk + lo) * ts;
       if (dst != src) copyRange<T, false>(dst, src, nelem * ts, aligned);
     } else {
-      // fold order: owner+1, ..., owner (AR/RS, all_reduce.h:43-66) or root+1, ..., root (reduce.h:34-52)
-      int first = (COLL == COLL_REDUCE ? a.root + 1 : me + 1) % n;
-      const void* src[NCCL_AMD_MAX_RANKS];
-      for (int k = 0; k < n; k++) {
-        int q = (first + k) % n;
-        if (q == me) src[k] = (const char*)a.sendbuff + ((uint64_t)me * a.chunk + lo) * ts;
-        else src[k] = dc.staging[me] + stagingOffset(dc, c, STG_RS, (int)(ctr(CTR_RECV_RS, q) % nSlots), q);
-      }
-      void* dstLocal = nullptr;
+      char* dstLocal = nullptr;
       if (COLL == COLL_RS) dstLocal = (char*)a.recvbuff + lo * ts;
       else if (COLL == COLL_AR || isRoot) dstLocal = (char*)a.recvbuff + ((uint64_t)me * a.chunk + lo) * ts;
-      foldRange<T, OP>(fn, n, src, nelem, dstLocal, dstPush, nPush, aligned);
+      foldRange<T, OP>(fn, n, sh.srcPtr, nelem, dstLocal, sh.pushPtr, sh.nPush, aligned);
     }
     // one release covers both: AG data ready at each destination; RS slots consumed (ack to senders)
     if (tid < NCCL_AMD_MAX_RANKS) {
@@ -350,8 +372,7 @@ struct Channel {
       sh.sigPtr[NCCL_AMD_MAX_RANKS + tid] = ack ? dc.flags[tid] + flagIndex(c, FLG_RS_ACK, me) : nullptr;
     }
     __syncthreads();
-    if (push) signalAll<true>(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS);
-    else signalAll<false>(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS);
+    signalAll(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS, push || forceRel);
     if (tid < n && tid != me) {
       if (COLL != COLL_AG) ctr(CTR_RECV_RS, tid)++;
       if (push && pushesTo(tid)) ctr(CTR_SEND_AG, tid)++;
@@ -365,7 +386,7 @@ struct Channel {
     int tid = threadIdx.x;
     if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_AG, tid) + 1 : 0;
     __syncthreads();
-    if (!waitAll<true>(dc, sh.st, myFlags(FLG_AG_READY), sh.want)) return false;
+    if (!waitAll(dc, sh.st, myFlags(FLG_AG_READY), sh.want, true)) return false;
     for (int k = 1; k < n; k++) {
       int q = (me + n - k) % n;
       uint64_t lo, hi;
@@ -380,7 +401,7 @@ struct Channel {
       sh.sigPtr[tid] = peer ? dc.flags[tid] + flagIndex(c, FLG_AG_ACK, me) : nullptr;
     }
     __syncthreads();
-    signalAll<false>(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS);  // credits only
+    signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, forceRel);  // credits only
     if (tid < n && tid != me) ctr(CTR_RECV_AG, tid)++;
     __syncthreads();
     return true;
@@ -406,17 +427,22 @@ __global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
     __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
   }
   const Red<T, OP> fn(opArg);
+  // protoFlags (NCCL_AMD_PROTO_FLAGS, diagnostics): 1 = acquire on credit waits too, 2 = release on
+  // credit signals too, 4 = C(s) before A(s+1)
   Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
-                          (COLL != COLL_REDUCE) || dc.rank == a.root};
+                          (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
+                          (a.protoFlags & 2) != 0};
   constexpr bool hasA = COLL != COLL_AG;
   const bool hasC = COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && ch.isRoot);
   // Pipeline: A(0); for s: B(s); A(s+1); C(s). Hoisting A(s+1) above C(s) lets the owners start
   // reducing step s+1 while this rank still drains step s (they are independent).
   bool ok = !hasA || a.nSteps == 0 || ch.phaseA(0);
+  const bool cFirst = (a.protoFlags & 4) != 0;
   for (int s = 0; ok && s < a.nSteps; s++) {
     ok = ch.phaseB(s);
+    if (ok && hasC && cFirst) ok = ch.phaseC(s);
     if (ok && hasA && s + 1 < a.nSteps) ok = ch.phaseA(s + 1);
-    if (ok && hasC) ok = ch.phaseC(s);
+    if (ok && hasC && !cFirst) ok = ch.phaseC(s);
   }
   __syncthreads();
   if (tid < CTR_KINDS * NCCL_AMD_MAX_RANKS) {

@@ -18,8 +18,9 @@ ncclResult_t launchKernGather(const LaunchPlan& p);
 
 
 // Streaming copy (reference onerank.cu:52-56 uses cudaMemcpyAsync; this is the hand-written
-// replacement): 16 B per lane, U packs in flight per lane, grid-stride over 1 KiB wave tiles.
-template <int U>
+// replacement): 16 B per lane, U packs in flight per lane, grid-stride over 256*U*16-byte tiles.
+// NTL/NTS select nontemporal loads/stores (measured variants).
+template <int U, bool NTL, bool NTS>
 __global__ void __launch_bounds__(256) copyKernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
                                                   uint64_t npk) {
   uint64_t stride = (uint64_t)gridDim.x * 256 * U;
@@ -27,10 +28,13 @@ __global__ void __launch_bounds__(256) copyKernel(u32x4* __restrict__ dst, const
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; u++)
-      if (base + u * 256 < npk) v[u] = __builtin_nontemporal_load(src + base + u * 256);
+      if (base + u * 256 < npk) v[u] = NTL ? __builtin_nontemporal_load(src + base + u * 256) : src[base + u * 256];
 #pragma unroll
     for (int u = 0; u < U; u++)
-      if (base + u * 256 < npk) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+      if (base + u * 256 < npk) {
+        if (NTS) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+        else dst[base + u * 256] = v[u];
+      }
   }
 }
 
@@ -43,11 +47,20 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
   if (bytes == 0 || dst == src) return ncclSuccess;
   if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
     uint64_t npk = bytes >> 4;
-    constexpr int U = 4;
     if (npk) {
+      // variant (NCCL_AMD_COPY_VARIANT): 0 nt/nt U4 (default), 1 plain/plain U4, 2 plain/nt U4, 3 nt/nt U8
+      int var = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
+      int U = var == 3 ? 8 : 4;
       uint64_t tiles = (npk + 256 * U - 1) / (256 * U);
       int grid = (int)std::min<uint64_t>(tiles, (uint64_t)paramInt("NCCL_AMD_COPY_GRID", 2048));
-      hipLaunchKernelGGL((copyKernel<U>), dim3(grid), dim3(256), 0, stream, (u32x4*)dst, (const u32x4*)src, npk);
+      u32x4* d = (u32x4*)dst;
+      const u32x4* s = (const u32x4*)src;
+      switch (var) {
+        case 1: hipLaunchKernelGGL((copyKernel<4, false, false>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 2: hipLaunchKernelGGL((copyKernel<4, false, true>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 3: hipLaunchKernelGGL((copyKernel<8, true, true>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        default: hipLaunchKernelGGL((copyKernel<4, true, true>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+      }
       HIPCHECK(hipGetLastError());
     }
     uint64_t done = npk << 4;

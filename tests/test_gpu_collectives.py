@@ -58,9 +58,10 @@ def test_single_process_multirank(built, nranks):
     assert not errs, "\n".join(errs[:20])
 
 
-def _mp_worker(rank, nranks, uid, quick, q):
+def _mp_worker(rank, nranks, uid, quick, q, env=None):
     try:
         os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "30000"
+        os.environ.update(env or {})
         import torch
         import nccl_amd
         from tests import gpu_cases as G
@@ -79,14 +80,22 @@ def _mp_worker(rank, nranks, uid, quick, q):
         q.put((rank, [f"rank {rank} exception: {e!r}"]))
 
 
-@pytest.mark.parametrize("nranks", [2, 4])
-def test_multi_process(built, nranks):
+# (nranks, env): the second group forces tiny staging slots so every channel runs many pipeline
+# steps with slot reuse (credit protocol, A(s+1)-before-C(s) ordering) at test sizes.
+MP_CASES = [(2, {}), (4, {}),
+            (2, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
+            (3, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
+            (4, {"NCCL_AMD_SLOT_BYTES": "8192", "NCCL_AMD_NSLOTS": "3", "NCCL_MAX_CTAS": "7"})]
+
+
+@pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
+def test_multi_process(built, nranks, env):
     _torch()
     import nccl_amd
     uid = nccl_amd.get_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_mp_worker, args=(r, nranks, uid, nranks > 2, q)) for r in range(nranks)]
+    ps = [ctx.Process(target=_mp_worker, args=(r, nranks, uid, nranks > 2 or bool(env), q, env)) for r in range(nranks)]
     for p in ps:
         p.start()
     import queue
