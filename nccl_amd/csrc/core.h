@@ -89,6 +89,7 @@ struct PeerInfo {  // exchanged once at init (reference: struct ncclPeerInfo, sr
   int pid;
   uint64_t hostHash;
   char busId[32];
+  int numCUs;
   hipIpcMemHandle_t stagingHandle;
   hipIpcMemHandle_t flagsHandle;
   uint64_t stagingPtr;  // raw pointers, valid only inside the same process
@@ -131,6 +132,7 @@ struct ncclComm {
   size_t slotBytes = 0;
   int nSlots = 0;
   int maxChannels = 0;
+  int chanCap = 0;  // channels per launch that stay co-resident even with several ranks per GPU
   hipStream_t internalStream = nullptr;
 
   std::vector<ncclamd::UserRedOp> userOps;

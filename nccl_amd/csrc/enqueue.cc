@@ -126,7 +126,7 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
   const size_t minPart = (size_t)paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
   int nch = (int)((blockBytes + minPart - 1) / minPart);
   if (nch < comm->minCTAs) nch = comm->minCTAs;
-  if (nch > comm->maxChannels) nch = comm->maxChannels;
+  if (nch > comm->chanCap) nch = comm->chanCap;
   if (nch < 1) nch = 1;
   const uint64_t epp = 16 / eltSize;
   uint64_t blockElems = blockBytes / eltSize;
@@ -200,7 +200,9 @@ ncclResult_t launchColl(const CollInfo& info) {
   if (info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER) aligned = aligned && ((count * ts) & 15) == 0;
   if (paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0)) aligned = false;  // diagnostics: T-sized accesses only
   p.args.aligned = aligned ? 1 : 0;
-  p.args.protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0);
+  // NCCL_AMD_P2P_FENCE=0 drops the system release fence before data flags (all published bytes are
+  // already stored write-through at system scope and drained). Default: keep it.
+  p.args.protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 1) ? 0 : 8);
   planChannels(comm, blockElems * ts, ts, p);
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,

@@ -51,7 +51,7 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   c->device = dev;
   c->blocking = true;
   c->minCTAs = 1;
-  c->maxCTAs = (int)paramInt("NCCL_MAX_CTAS", paramInt("NCCL_MAX_NCHANNELS", 64));
+  c->maxCTAs = (int)paramInt("NCCL_MAX_CTAS", paramInt("NCCL_MAX_NCHANNELS", 256));
   if (cfg) {
     if (cfg->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = cfg->blocking != 0;
     if (cfg->minCTAs != NCCL_CONFIG_UNDEF_INT) c->minCTAs = cfg->minCTAs;
@@ -65,7 +65,14 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   c->maxChannels = c->maxCTAs;
   c->nSlots = (int)paramInt("NCCL_AMD_NSLOTS", 2);
   if (c->nSlots < 1) c->nSlots = 1;
-  int64_t sb = paramInt("NCCL_AMD_SLOT_BYTES", 128 << 10);
+  // Slot size: the staging slab (maxChannels x 2 kinds x nSlots x nRanks x slot) is sized to a fixed
+  // HBM budget (NCCL_AMD_STAGING_MIB, default 1 GiB of the 288 GB), so fewer ranks get bigger slots
+  // (fewer handshakes per byte). NCCL_AMD_SLOT_BYTES overrides.
+  int64_t budget = paramInt("NCCL_AMD_STAGING_MIB", 1024) << 20;
+  int64_t sb = budget / ((int64_t)c->maxChannels * 2 * c->nSlots * (nranks > 1 ? nranks : 2));
+  if (sb > (1 << 20)) sb = 1 << 20;
+  if (sb < (16 << 10)) sb = 16 << 10;
+  sb = paramInt("NCCL_AMD_SLOT_BYTES", sb);
   sb = (sb + 4095) / 4096 * 4096;
   if (sb < 4096) sb = 4096;
   c->slotBytes = (size_t)sb;
@@ -99,8 +106,27 @@ static ncclResult_t fillPeerInfo(ncclComm* comm, PeerInfo* p) {
   p->pid = getpid();
   p->hostHash = hostHash();
   HIPCHECK(hipDeviceGetPCIBusId(p->busId, sizeof(p->busId), comm->device));
+  HIPCHECK(hipDeviceGetAttribute(&p->numCUs, hipDeviceAttributeMultiprocessorCount, comm->device));
   NCCLCHECK(exportHandles(comm, p));
   return ncclSuccess;
+}
+
+// Channels of one launch must all be resident at once on every GPU (a channel spins on the same
+// channel of its peers). With several ranks on one GPU (NCCL_MULTI_RANK_GPU_ENABLE / test boxes) the
+// launches share the CUs, so cap channels at 2 workgroups per CU divided by the most ranks any device
+// hosts. Every rank computes this from the same peer table, so all agree.
+static void computeChannelCap(ncclComm* c) {
+  int minCU = 1 << 30, maxPer = 1;
+  for (size_t i = 0; i < c->peers.size(); i++) {
+    int same = 0;
+    for (size_t j = 0; j < c->peers.size(); j++) same += strcmp(c->peers[i].busId, c->peers[j].busId) == 0;
+    if (same > maxPer) maxPer = same;
+    if (c->peers[i].numCUs > 0 && c->peers[i].numCUs < minCU) minCU = c->peers[i].numCUs;
+  }
+  if (minCU == (1 << 30)) minCU = 256;
+  int cap = 2 * minCU / maxPer;
+  if (cap < 1) cap = 1;
+  c->chanCap = cap < c->maxChannels ? cap : c->maxChannels;
 }
 
 // Shape parameters every rank must agree on (exchanged with the PeerInfo block).
@@ -135,6 +161,7 @@ static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id,
   if ((res = bootstrapAllGather(comm->bootstrap, blobs.data(), sizeof(Blob))) != ncclSuccess) goto fail;
   comm->peers.resize(nranks);
   for (int r = 0; r < nranks; r++) comm->peers[r] = blobs[r].info;
+  computeChannelCap(comm);
   if ((res = transportConnect(comm)) != ncclSuccess) goto fail;
   if ((res = commAllocDevState(comm)) != ncclSuccess) goto fail;
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
@@ -260,6 +287,7 @@ NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
   }
   for (int i = 0; i < ndev && res == ncclSuccess; i++) {
     cs[i]->peers = infos;
+    computeChannelCap(cs[i]);
     res = transportConnect(cs[i]);
     if (res == ncclSuccess) res = commAllocDevState(cs[i]);
   }

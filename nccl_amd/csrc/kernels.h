@@ -43,6 +43,28 @@ __device__ __forceinline__ void storeRemote(void* p, u32x4 v) {
 }
 __device__ __forceinline__ void drainStores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// One element stored system-scope write-through (tails and unaligned ranges of published data).
+template <typename T>
+__device__ __forceinline__ void storeRemoteElt(T* p, T v) {
+  if constexpr (sizeof(T) == 1) {
+    uint32_t x = 0;
+    __builtin_memcpy(&x, &v, 1);
+    asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+  } else if constexpr (sizeof(T) == 2) {
+    uint32_t x = 0;
+    __builtin_memcpy(&x, &v, 2);
+    asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+  } else if constexpr (sizeof(T) == 4) {
+    uint32_t x;
+    __builtin_memcpy(&x, &v, 4);
+    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+  } else {
+    uint64_t x;
+    __builtin_memcpy(&x, &v, 8);
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+  }
+}
+
 __device__ __forceinline__ uint64_t loadFlag(const uint64_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -137,26 +159,30 @@ __device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t n
 #pragma unroll
       for (int u = 0; u < U; u++) {
         if (REMOTE) storeRemote(d + i + u * kThreads, v[u]);
-        else d[i + u * kThreads] = v[u];
+        else __builtin_nontemporal_store(v[u], d + i + u * kThreads);
       }
     }
     for (; i < npk; i += kThreads) {
       u32x4 v = __builtin_nontemporal_load(s + i);
       if (REMOTE) storeRemote(d + i, v);
-      else d[i] = v;
+      else __builtin_nontemporal_store(v, d + i);
     }
     uint64_t done = npk << 4;
     uint64_t tail = (nbytes - done) / sizeof(T);
     if (threadIdx.x < tail) {
       const T* st = (const T*)((const char*)src + done);
       T* dt = (T*)((char*)dst + done);
-      dt[threadIdx.x] = st[threadIdx.x];
+      if (REMOTE) storeRemoteElt(dt + threadIdx.x, st[threadIdx.x]);
+      else dt[threadIdx.x] = st[threadIdx.x];
     }
   } else {
     uint64_t n = nbytes / sizeof(T);
     const T* s = (const T*)src;
     T* d = (T*)dst;
-    for (uint64_t i = threadIdx.x; i < n; i += kThreads) d[i] = s[i];
+    for (uint64_t i = threadIdx.x; i < n; i += kThreads) {
+      if (REMOTE) storeRemoteElt(d + i, s[i]);
+      else d[i] = s[i];
+    }
   }
 }
 
@@ -211,7 +237,7 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
         if (i >= npk) continue;
 #pragma unroll
         for (int e = 0; e < EPP; e++) acc[u].e[e] = fn.post(acc[u].e[e]);
-        if (dstLocal) ((u32x4*)dstLocal)[i] = acc[u].v;
+        if (dstLocal) __builtin_nontemporal_store(acc[u].v, (u32x4*)dstLocal + i);
         for (int p = 0; p < nPush; p++) storeRemote((u32x4*)dstPush[p] + i, acc[u].v);
       }
     }
@@ -221,7 +247,7 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
       for (int k = 1; k < n; k++) acc = fn.red(fn.pre(((const T*)src[k])[t]), acc);
       acc = fn.post(acc);
       if (dstLocal) ((T*)dstLocal)[t] = acc;
-      for (int p = 0; p < nPush; p++) ((T*)dstPush[p])[t] = acc;  // plain store, covered by the release
+      for (int p = 0; p < nPush; p++) storeRemoteElt((T*)dstPush[p] + t, acc);
     }
   } else {
     for (uint64_t t = threadIdx.x; t < nelem; t += kThreads) {
@@ -229,7 +255,7 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
       for (int k = 1; k < n; k++) acc = fn.red(fn.pre(((const T*)src[k])[t]), acc);
       acc = fn.post(acc);
       if (dstLocal) ((T*)dstLocal)[t] = acc;
-      for (int p = 0; p < nPush; p++) ((T*)dstPush[p])[t] = acc;
+      for (int p = 0; p < nPush; p++) storeRemoteElt((T*)dstPush[p] + t, acc);
     }
   }
 }
@@ -265,7 +291,7 @@ struct Channel {
   Shared& sh;
   const Red<T, OP>& fn;
   int c, me, n, nSlots;
-  bool aligned, isRoot, forceAcq, forceRel;
+  bool aligned, isRoot, forceAcq, forceRel, noRel;
   static constexpr uint64_t ts = sizeof(T);
 
   __device__ uint64_t blockLen(int q) const {
@@ -306,7 +332,7 @@ struct Channel {
       sh.sigPtr[tid] = act ? dc.flags[tid] + flagIndex(c, FLG_RS_READY, me) : nullptr;
     }
     __syncthreads();
-    signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, true);
+    signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, !noRel);
     if (tid < n && tid != me) ctr(CTR_SEND_RS, tid)++;
     __syncthreads();
     return true;
@@ -372,7 +398,7 @@ struct Channel {
       sh.sigPtr[NCCL_AMD_MAX_RANKS + tid] = ack ? dc.flags[tid] + flagIndex(c, FLG_RS_ACK, me) : nullptr;
     }
     __syncthreads();
-    signalAll(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS, push || forceRel);
+    signalAll(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS, (push && !noRel) || forceRel);
     if (tid < n && tid != me) {
       if (COLL != COLL_AG) ctr(CTR_RECV_RS, tid)++;
       if (push && pushesTo(tid)) ctr(CTR_SEND_AG, tid)++;
@@ -428,10 +454,11 @@ __global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
   }
   const Red<T, OP> fn(opArg);
   // protoFlags (NCCL_AMD_PROTO_FLAGS, diagnostics): 1 = acquire on credit waits too, 2 = release on
-  // credit signals too, 4 = C(s) before A(s+1)
+  // credit signals too, 4 = C(s) before A(s+1), 8 = NO release fence before data flags (unsafe, measures
+  // the fence cost only)
   Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
                           (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
-                          (a.protoFlags & 2) != 0};
+                          (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0};
   constexpr bool hasA = COLL != COLL_AG;
   const bool hasC = COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && ch.isRoot);
   // Pipeline: A(0); for s: B(s); A(s+1); C(s). Hoisting A(s+1) above C(s) lets the owners start

@@ -1,0 +1,9 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+source scripts/tune_lib.sh
+if [ -z "$SKIP_TESTS" ]; then timeout -k 10 600 python -m pytest tests -m gpu -x -v -s > gpurun_out/pytest_gpu.log 2>&1 && echo PYTEST_OK || exit 1; fi
+run default
+run nofence NCCL_AMD_P2P_FENCE=0
+NP=4 run np4
+NP=8 run np8
