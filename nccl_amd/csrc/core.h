@@ -167,7 +167,7 @@ struct CollInfo {  // reference: struct ncclInfo, src/include/info.h:17-41
   hipStream_t stream;
 };
 
-enum Algo { ALGO_COPY = 0, ALGO_ONERANK = 1, ALGO_DIRECT = 2 };
+enum Algo { ALGO_COPY = 0, ALGO_ONERANK = 1, ALGO_DIRECT = 2, ALGO_ONESHOT = 3 };
 
 struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src/include/comm.h)
   CollFunc func;

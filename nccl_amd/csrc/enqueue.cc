@@ -122,10 +122,12 @@ static ncclResult_t argsCheck(CollInfo* info) {
 // One node, full xGMI mesh: the only algorithm is the direct scatter-reduce-gather; what is tuned is
 // the channel (workgroup) count and the pipeline slice. Every rank computes the same plan from the
 // same (count, type, nRanks, params), which the protocol requires.
-static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchPlan& p) {
-  const size_t minPart = (size_t)paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
+static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchPlan& p, size_t minPart,
+                         int maxCh) {
+  if (minPart < 16) minPart = 16;
   int nch = (int)((blockBytes + minPart - 1) / minPart);
   if (nch < comm->minCTAs) nch = comm->minCTAs;
+  if (nch > maxCh) nch = maxCh;
   if (nch > comm->chanCap) nch = comm->chanCap;
   if (nch < 1) nch = 1;
   const uint64_t epp = 16 / eltSize;
@@ -203,7 +205,24 @@ ncclResult_t launchColl(const CollInfo& info) {
   // NCCL_AMD_P2P_FENCE=0 drops the system release fence before data flags (all published bytes are
   // already stored write-through at system scope and drained). Default: keep it.
   p.args.protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 1) ? 0 : 8);
-  planChannels(comm, blockElems * ts, ts, p);
+  // Algorithm choice (reference: NCCL_ALGO / tuning.cc cost model): one-shot for small AllReduce
+  // (latency: one handshake), direct scatter-reduce-gather otherwise (bandwidth). NCCL_ALGO may force
+  // either: ONESHOT or DIRECT (the reference's RING/TREE names map to DIRECT).
+  bool oneShot = false;
+  if (info.func == FUNC_ALLREDUCE) {
+    const char* algo = paramStr("NCCL_ALGO");
+    size_t bytes = count * (size_t)ts;
+    oneShot = bytes <= (size_t)paramInt("NCCL_AMD_ONESHOT_BYTES", 256 << 10);
+    if (algo && !strcasecmp(algo, "ONESHOT")) oneShot = true;
+    if (algo && (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE"))) oneShot = false;
+  }
+  if (oneShot) {
+    p.algo = ALGO_ONESHOT;
+    planChannels(comm, count * ts, ts, p, (size_t)paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10), 32);
+  } else {
+    planChannels(comm, blockElems * ts, ts, p, (size_t)paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10),
+                 comm->chanCap);
+  }
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,
         p.args.nSteps, p.args.aligned);

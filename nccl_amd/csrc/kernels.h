@@ -263,7 +263,10 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
 
 // ------------------------------------------------------------------------------------ collective kernel
 
-enum Coll { COLL_AR = 0, COLL_RS = 1, COLL_AG = 2, COLL_REDUCE = 3 };
+// COLL_AR1 = one-shot AllReduce for small buffers: every rank publishes its whole channel portion to
+// every peer and folds all n contributions itself (one handshake instead of three; (n-1)*S link bytes
+// instead of 2(n-1)/n*S). Same fold order as the two-shot path, so results are identical.
+enum Coll { COLL_AR = 0, COLL_RS = 1, COLL_AG = 2, COLL_REDUCE = 3, COLL_AR1 = 4 };
 
 // Element range [lo,hi) of a block handled by channel c at pipeline step s (offsets inside the block).
 __device__ __forceinline__ void sliceRange(const CollArgs& a, int c, int s, uint64_t blockLen, uint64_t& lo,
@@ -407,6 +410,74 @@ struct Channel {
     return true;
   }
 
+  // One-shot A: publish my portion [lo,hi) of the whole buffer to every peer's RS staging.
+  __device__ bool oneShotA(int step) {
+    int tid = threadIdx.x;
+    if (tid < NCCL_AMD_MAX_RANKS) {
+      uint64_t s = ctr(CTR_SEND_RS, tid);
+      sh.want[tid] = (tid < n && tid != me && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
+    }
+    __syncthreads();
+    if (!waitAll(dc, sh.st, myFlags(FLG_RS_ACK), sh.want, forceAcq)) return false;
+    uint64_t lo, hi;
+    sliceRange(a, c, step, a.count, lo, hi);
+    const char* src = (const char*)a.sendbuff + lo * ts;
+    for (int k = 1; k < n; k++) {
+      int p = (me + k) % n;
+      int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
+      copyRange<T, true>(dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me), src, (hi - lo) * ts, aligned);
+    }
+    if (tid < NCCL_AMD_MAX_RANKS) {
+      bool act = tid < n && tid != me;
+      sh.sigVal[tid] = act ? ctr(CTR_SEND_RS, tid) + 1 : 0;
+      sh.sigPtr[tid] = act ? dc.flags[tid] + flagIndex(c, FLG_RS_READY, me) : nullptr;
+    }
+    __syncthreads();
+    signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, !noRel);
+    if (tid < n && tid != me) ctr(CTR_SEND_RS, tid)++;
+    __syncthreads();
+    return true;
+  }
+
+  // One-shot B: fold all n contributions of my portion, owner by owner (the portion may straddle
+  // rank blocks; block q folds q+1, ..., q like the two-shot path), then return the credits.
+  __device__ bool oneShotB(int step) {
+    int tid = threadIdx.x;
+    if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
+    __syncthreads();
+    if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, true)) return false;
+    uint64_t lo, hi;
+    sliceRange(a, c, step, a.count, lo, hi);
+    for (uint64_t x = lo; x < hi;) {
+      const int owner = (int)(x / a.chunk);
+      const uint64_t end = min(hi, (uint64_t)(owner + 1) * a.chunk);
+      if (tid == 0) {
+        int first = (owner + 1) % n;
+        for (int k = 0; k < n; k++) {
+          int q = (first + k) % n;
+          sh.srcPtr[k] = q == me ? (const char*)a.sendbuff + x * ts
+                                 : dc.staging[me] + stagingOffset(dc, c, STG_RS, (int)(ctr(CTR_RECV_RS, q) % nSlots), q) +
+                                       (x - lo) * ts;
+        }
+      }
+      __syncthreads();
+      // sub-range starts inside a slot are 16-byte aligned: rank blocks are multiples of 16 bytes
+      foldRange<T, OP>(fn, n, sh.srcPtr, end - x, (char*)a.recvbuff + x * ts, sh.pushPtr, 0, aligned);
+      __syncthreads();
+      x = end;
+    }
+    if (tid < NCCL_AMD_MAX_RANKS) {
+      bool peer = tid < n && tid != me;
+      sh.sigVal[tid] = peer ? ctr(CTR_RECV_RS, tid) + 1 : 0;
+      sh.sigPtr[tid] = peer ? dc.flags[tid] + flagIndex(c, FLG_RS_ACK, me) : nullptr;
+    }
+    __syncthreads();
+    signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, forceRel);  // credits only
+    if (tid < n && tid != me) ctr(CTR_RECV_RS, tid)++;
+    __syncthreads();
+    return true;
+  }
+
   // C: gather the other blocks from my AG staging into the output (AR, AG, REDUCE at root)
   __device__ bool phaseC(int step) {
     int tid = threadIdx.x;
@@ -459,6 +530,10 @@ __global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
   Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
                           (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
                           (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0};
+  if (COLL == COLL_AR1) {
+    bool ok1 = true;
+    for (int s = 0; ok1 && s < a.nSteps; s++) ok1 = ch.oneShotA(s) && ch.oneShotB(s);
+  } else {
   constexpr bool hasA = COLL != COLL_AG;
   const bool hasC = COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && ch.isRoot);
   // Pipeline: A(0); for s: B(s); A(s+1); C(s). Hoisting A(s+1) above C(s) lets the owners start
@@ -470,6 +545,7 @@ __global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
     if (ok && hasC && cFirst) ok = ch.phaseC(s);
     if (ok && hasA && s + 1 < a.nSteps) ok = ch.phaseA(s + 1);
     if (ok && hasC && !cFirst) ok = ch.phaseC(s);
+  }
   }
   __syncthreads();
   if (tid < CTR_KINDS * NCCL_AMD_MAX_RANKS) {
@@ -508,7 +584,10 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
   }
   switch (p.func) {
     case FUNC_ALLREDUCE:
-      hipLaunchKernelGGL((collKernel<T, OP, COLL_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_ONESHOT)
+        hipLaunchKernelGGL((collKernel<T, OP, COLL_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      else
+        hipLaunchKernelGGL((collKernel<T, OP, COLL_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
     case FUNC_REDUCESCATTER:
       hipLaunchKernelGGL((collKernel<T, OP, COLL_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);

@@ -85,7 +85,9 @@ def _mp_worker(rank, nranks, uid, quick, q, env=None):
 MP_CASES = [(2, {}), (4, {}),
             (2, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
             (3, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
-            (4, {"NCCL_AMD_SLOT_BYTES": "8192", "NCCL_AMD_NSLOTS": "3", "NCCL_MAX_CTAS": "7"})]
+            (4, {"NCCL_AMD_SLOT_BYTES": "8192", "NCCL_AMD_NSLOTS": "3", "NCCL_MAX_CTAS": "7"}),
+            (3, {"NCCL_ALGO": "ONESHOT", "NCCL_AMD_SLOT_BYTES": "16384"}),
+            (2, {"NCCL_ALGO": "DIRECT"})]
 
 
 @pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
