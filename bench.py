@@ -87,7 +87,139 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-extra", action="store_true", help="skip the secondary 256 MiB n=1 measurement")
+    p.add_argument("--no-suite", action="store_true", help="N>1: skip BASELINE configs 3-5 + link probes")
+    p.add_argument("--quick-suite", action="store_true", help="N>1: smaller suite (rehearsal on one GPU)")
     return p.parse_args(argv)
+
+
+def _time_ms(fn, stream, iters: int, warmup: int = 3) -> float:
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for _ in range(iters):
+        fn()
+    b.record(stream)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dict:
+    """The other BASELINE.json configs at this N (the driver runs bench.py on the 8-GPU node, so this is
+    where they get measured): RS+AG bf16 1 GiB bucket (configs[2]), AllReduce fp16 8 B..256 MiB sweep,
+    one-shot vs direct (configs[3]), Reduce int32 min/max 128 MiB root 0 (configs[4]); each with a
+    size-independent exactness check, plus xGMI peer-copy probes for the roofline denominator."""
+    import torch
+    import nccl_amd
+    out = {}
+    sp = stream.cuda_stream
+
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([0 if ok else 1], dtype=torch.int32)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return int(t[0]) == 0
+
+    def tmax(ms: float) -> float:
+        return max_over_ranks(dist, [ms])[0]
+
+    # --- configs[2]: ZeRO bucket, bf16, 1 GiB ---
+    bucket = (64 if quick else 1024) * MIB
+    cnt = bucket // 2
+    g = torch.Generator(device="cuda")
+    g.manual_seed(77)
+    base = torch.randint(-4, 5, (cnt,), device="cuda", generator=g, dtype=torch.int32).to(torch.bfloat16)
+    send = base * (rank + 1)
+    shard = torch.empty(cnt // n, dtype=torch.bfloat16, device="cuda")
+    full = torch.empty(cnt, dtype=torch.bfloat16, device="cuda")
+    rs = lambda: comm.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp)
+    ag = lambda: comm.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp)
+    ms_rs = tmax(_time_ms(rs, stream, 10))
+    ms_ag = tmax(_time_ms(ag, stream, 10))
+    rs()
+    ag()
+    torch.cuda.synchronize()
+    ok = bool(torch.equal(full, base * (n * (n + 1) // 2)))
+    bw = lambda ms: round(bucket / (ms * 1e-3) / 1e9 * (n - 1) / n, 2)
+    out["rs_ag_bf16"] = {"config": f"ncclReduceScatter + ncclAllGather bf16, {bucket // MIB} MiB bucket, n={n}",
+                         "rs_ms": round(ms_rs, 4), "rs_busbw_GBps": bw(ms_rs), "ag_ms": round(ms_ag, 4),
+                         "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(ok) else "FAIL"}
+    del send, shard, full, base
+
+    # --- configs[3]: fp16 AllReduce sweep, one-shot vs direct ---
+    top = (16 if quick else 256) * MIB
+    buf = torch.empty(top // 2, dtype=torch.float16, device="cuda").uniform_(-1, 1)
+    res = torch.empty_like(buf)
+    sweep = []
+    size = 8
+    old = os.environ.get("NCCL_ALGO")
+    while size <= top:
+        c = size // 2
+        row = {"bytes": size}
+        for algo in ("ONESHOT", "DIRECT"):
+            if algo == "ONESHOT" and size > 64 * MIB:
+                continue
+            os.environ["NCCL_ALGO"] = algo
+            it = 50 if size <= 4 * MIB else 10
+            ms = tmax(_time_ms(lambda: comm.all_reduce_raw(buf.data_ptr(), res.data_ptr(), c, 6, 0, sp), stream, it))
+            row[algo.lower() + "_us"] = round(ms * 1e3, 2)
+            row[algo.lower() + "_busbw_GBps"] = round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)
+        sweep.append(row)
+        size *= 2
+    if old is None:
+        os.environ.pop("NCCL_ALGO", None)
+    else:
+        os.environ["NCCL_ALGO"] = old
+    out["ar_fp16_sweep"] = sweep
+    del buf, res
+
+    # --- configs[4]: Reduce int32 min / max, 128 MiB, root 0 ---
+    S = (16 if quick else 128) * MIB
+    c = S // 4
+    g.manual_seed(99)
+    base = torch.randint(-2**31 + 64, 2**31 - 64, (c,), device="cuda", generator=g, dtype=torch.int64).to(torch.int32)
+    send = base + rank
+    recv = torch.empty_like(send) if rank == 0 else None
+    red = {}
+    okr = True
+    for name, op, want in (("min", 3, 0), ("max", 2, n - 1)):
+        fn = lambda: comm.reduce_raw(send.data_ptr(), recv.data_ptr() if recv is not None else None, c, 2, op, 0, sp)
+        ms = tmax(_time_ms(fn, stream, 10))
+        fn()
+        torch.cuda.synchronize()
+        if rank == 0:
+            okr = okr and bool(torch.equal(recv, base + want))
+        red[name + "_ms"] = round(ms, 4)
+        red[name + "_busbw_GBps"] = round(S / (ms * 1e-3) / 1e9, 2)
+    red["config"] = f"ncclReduce min/max int32, {S // MIB} MiB, root 0, n={n}"
+    red["check"] = "pass (bit-exact)" if agree(okr) else "FAIL"
+    out["reduce_int32"] = red
+    del send, recv, base
+
+    # --- xGMI probes (rank 0, peer copies via hipMemcpyPeerAsync) ---
+    ndev = torch.cuda.device_count()
+    if rank == 0 and ndev > 1:
+        probe = {}
+        nbytes = 256 * MIB
+        src = torch.empty(nbytes // 4, device="cuda:0")
+        dsts = [torch.empty(nbytes // 4, device=f"cuda:{d}") for d in range(1, ndev)]
+        ms = _time_ms(lambda: dsts[0].copy_(src), stream, 5)
+        probe["one_link_0to1_GBps"] = round(nbytes / (ms * 1e-3) / 1e9, 1)
+        streams = [torch.cuda.Stream(device=0) for _ in dsts]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            for s, d in zip(streams, dsts):
+                with torch.cuda.stream(s):
+                    d.copy_(src)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / 3
+        probe["fanout_0toall_GBps"] = round(len(dsts) * nbytes / dt / 1e9, 1)
+        probe["method"] = "torch copy_ (hipMemcpyPeerAsync); fan-out = concurrent copies on separate streams"
+        out["xgmi_probe"] = probe
+        del src, dsts
+    return out
 
 
 def cpu_baseline(n: int, count: int, budget_s: float):
@@ -251,6 +383,14 @@ def main(argv=None):
         ms = a.elapsed_time(b) / 20
         extra["n1_256MiB_hipMemcpyD2D_GBps"] = round(2 * 256 * MIB / (ms * 1e-3) / 1e9, 1)
         del s2, r2
+
+    if n > 1 and not args.no_suite:
+        try:
+            extra["suite"] = run_suite(comm, n, rank, dist, stream, quick=args.quick_suite)
+        except Exception as e:  # secondary measurements never fail the headline line
+            extra["suite"] = {"error": repr(e)}
+        torch.cuda.synchronize()
+        barrier()
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
