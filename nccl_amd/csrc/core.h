@@ -149,6 +149,7 @@ ncclResult_t commCheck(const ncclComm* comm, const char* opname, const char* wha
 ncclResult_t transportSetup(ncclComm* comm);     // allocate staging/flags + IPC export
 ncclResult_t transportConnect(ncclComm* comm);   // map peers after the PeerInfo exchange
 ncclResult_t transportFree(ncclComm* comm);
+ncclResult_t transportDrainCredits(ncclComm* comm);  // wait for acks peers still owe (destroy)
 ncclResult_t commAllocDevState(ncclComm* comm);  // counters, DevComm upload, abort/error words
 
 // ---------------------------------------------------------------- enqueue (reference src/enqueue.cc)
@@ -185,6 +186,7 @@ ncclResult_t enqueueCheck(CollInfo* info);
 ncclResult_t launchColl(const CollInfo& info);  // plan + launch (enqueue.cc)
 ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
 ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream);
+ncclResult_t warmKernels();  // load all kernel code objects on the current device (kernels.hip)
 int typeSize(ncclDataType_t t);
 
 // ---------------------------------------------------------------- groups (reference src/group.cc)

@@ -344,11 +344,12 @@ NCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   int old = 0;
   (void)hipGetDevice(&old);
   (void)hipSetDevice(comm->device);
-  if (!comm->finalized) {
-    // Wait for this rank's kernels, then for every peer (no peer may still write into our slab).
-    (void)hipDeviceSynchronize();
-    if (comm->bootstrap) (void)bootstrapBarrier(comm->bootstrap);
-  }
+  // Local, like the reference (init.cc:2879-2911): wait for this rank's kernels, then for the credit
+  // words peers still owe us (the only writes a peer can make after our kernels finished), so no
+  // peer store lands in freed memory. No bootstrap barrier: one thread may destroy every comm of a
+  // clique in turn (the reference's single-process pattern).
+  (void)hipDeviceSynchronize();
+  if (!comm->finalized) (void)transportDrainCredits(comm);
   commFree(comm);
   (void)hipSetDevice(old);
   return ncclSuccess;

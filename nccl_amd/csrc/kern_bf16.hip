@@ -4,4 +4,9 @@ namespace ncclamd {
 ncclResult_t launchKernBF16(const LaunchPlan& p) {
   return launchOp<bf16_t>(p);
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernBF16() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<bf16_t, 0, COLL_AR>);
+}
 }  // namespace ncclamd

@@ -4,4 +4,9 @@ namespace ncclamd {
 ncclResult_t launchKernF16(const LaunchPlan& p) {
   return launchOp<half_t>(p);
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernF16() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<half_t, 0, COLL_AR>);
+}
 }  // namespace ncclamd

@@ -4,4 +4,9 @@ namespace ncclamd {
 ncclResult_t launchKernF32(const LaunchPlan& p) {
   return launchOp<float>(p);
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernF32() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<float, 0, COLL_AR>);
+}
 }  // namespace ncclamd

@@ -4,4 +4,9 @@ namespace ncclamd {
 ncclResult_t launchKernF64(const LaunchPlan& p) {
   return launchOp<double>(p);
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernF64() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<double, 0, COLL_AR>);
+}
 }  // namespace ncclamd

@@ -4,4 +4,9 @@ namespace ncclamd {
 ncclResult_t launchKernFp8(const LaunchPlan& p) {
   return p.datatype == ncclFloat8e4m3 ? launchOp<e4m3_t>(p) : launchOp<e5m2_t>(p);
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernFp8() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<e4m3_t, 0, COLL_AR>);
+}
 }  // namespace ncclamd

@@ -9,4 +9,9 @@ ncclResult_t launchKernGather(const LaunchPlan& p) {
     default: return launchTyped<uint64_t, 0>(p);
   }
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernGather() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<uint32_t, 0, COLL_AG>);
+}
 }  // namespace ncclamd

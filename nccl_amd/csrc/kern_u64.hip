@@ -4,4 +4,9 @@ namespace ncclamd {
 ncclResult_t launchKernU64(const LaunchPlan& p) {
   return launchIntOp<uint64_t>(p);
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernU64() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<uint64_t, 0, COLL_AR>);
+}
 }  // namespace ncclamd

@@ -4,4 +4,9 @@ namespace ncclamd {
 ncclResult_t launchKernU8(const LaunchPlan& p) {
   return launchIntOp<uint8_t>(p);
 }
+// Force this code object to load now (see warmKernels in kernels.hip).
+hipError_t warmKernU8() {
+  hipFuncAttributes attr;
+  return hipFuncGetAttributes(&attr, (const void*)&collKernel<uint8_t, 0, COLL_AR>);
+}
 }  // namespace ncclamd

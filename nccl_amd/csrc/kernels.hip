@@ -13,6 +13,27 @@ ncclResult_t launchKernF32(const LaunchPlan& p);
 ncclResult_t launchKernF64(const LaunchPlan& p);
 ncclResult_t launchKernFp8(const LaunchPlan& p);
 ncclResult_t launchKernGather(const LaunchPlan& p);
+hipError_t warmKernU8();
+hipError_t warmKernU32();
+hipError_t warmKernU64();
+hipError_t warmKernF16();
+hipError_t warmKernBF16();
+hipError_t warmKernF32();
+hipError_t warmKernF64();
+hipError_t warmKernFp8();
+hipError_t warmKernGather();
+
+// Load every kernel code object of this library on the current device at communicator init. With
+// lazy code-object loading, the first launch of a kernel from a not-yet-loaded object may wait for
+// the device to go idle; when several ranks share one GPU inside one process (ncclCommInitAll with a
+// repeated device) the peer rank's already-running, spinning kernel would then never see its partner
+// launch. Loading up front removes that stall from the collective launch path.
+ncclResult_t warmKernels() {
+  hipError_t (*fns[])() = {warmKernU8, warmKernU32, warmKernU64, warmKernF16, warmKernBF16,
+                           warmKernF32, warmKernF64, warmKernFp8, warmKernGather};
+  for (auto f : fns) HIPCHECK(f());
+  return ncclSuccess;
+}
 
 // ------------------------------------------------------------------------------------ nRanks == 1
 

@@ -84,6 +84,35 @@ ncclResult_t transportConnect(ncclComm* comm) {
   return ncclSuccess;
 }
 
+// Before freeing: every slice this rank sent must have been acknowledged (RS_ACK == sendRS and
+// AG_ACK == sendAG per channel and peer). Acks are written by peers' kernels after they consumed our
+// data, possibly after our own kernels finished; waiting for them (bounded) keeps those stores out of
+// freed memory. Returns ncclSuccess or ncclTimeout; the caller frees either way.
+ncclResult_t transportDrainCredits(ncclComm* comm) {
+  if (comm->nRanks == 1 || !comm->counters || !comm->flags) return ncclSuccess;
+  const size_t nc = (size_t)comm->maxChannels * CTR_KINDS * NCCL_AMD_MAX_RANKS;
+  const size_t nf = (size_t)comm->maxChannels * FLG_KINDS * NCCL_AMD_MAX_RANKS;
+  std::vector<uint64_t> ctr(nc), flg(nf);
+  HIPCHECK(hipMemcpy(ctr.data(), comm->counters, nc * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  const int64_t limitMs = paramInt("NCCL_AMD_DESTROY_TIMEOUT_MS", 10000);
+  for (int64_t waited = 0;; waited++) {
+    HIPCHECK(hipMemcpy(flg.data(), comm->flags, nf * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    bool done = true;
+    for (int c = 0; c < comm->maxChannels && done; c++)
+      for (int p = 0; p < comm->nRanks && done; p++) {
+        if (p == comm->rank) continue;
+        done = flg[flagIndex(c, FLG_RS_ACK, p)] >= ctr[ctrIndex(c, CTR_SEND_RS, p)] &&
+               flg[flagIndex(c, FLG_AG_ACK, p)] >= ctr[ctrIndex(c, CTR_SEND_AG, p)];
+      }
+    if (done) return ncclSuccess;
+    if (waited >= limitMs) {
+      WARN("rank %d: peers still owe credits after %ld ms; freeing anyway", comm->rank, (long)limitMs);
+      return ncclTimeout;
+    }
+    usleep(1000);
+  }
+}
+
 ncclResult_t transportFree(ncclComm* comm) {
   (void)hipSetDevice(comm->device);
   for (int r = 0; r < comm->nRanks && r < NCCL_AMD_MAX_RANKS; r++) {
@@ -142,6 +171,7 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
   HIPCHECK(hipMalloc((void**)&comm->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(comm->devComm, &d, sizeof(DevComm), hipMemcpyHostToDevice));
   HIPCHECK(hipStreamCreateWithFlags(&comm->internalStream, hipStreamNonBlocking));
+  NCCLCHECK(warmKernels());
   return ncclSuccess;
 }
 

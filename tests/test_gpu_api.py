@@ -1,0 +1,203 @@
+"""GPU tests of the API semantics around the hot path: group deferral, custom PreMulSum operators
+(host-immediate and device scalars), hipGraph capture/replay, ncclCommInitRank inside a group from one
+thread, and failure detection (spin timeout -> async error, ncclCommAbort of a stuck collective).
+All ranks share the box's single GPU (reference NCCL_MULTI_RANK_GPU_ENABLE, init.cc:68)."""
+import ctypes
+import os
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def two_comms(built):
+    import torch
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0])
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    yield comms, streams
+    for c in comms:
+        if c.ptr:
+            c.destroy()
+
+
+def _inputs(n, count, seed=5):
+    import oracle
+    return [oracle.fill(7, seed + r, count) for r in range(n)]
+
+
+def test_group_defers_launch_until_end(two_comms):
+    import torch
+    import nccl_amd
+    import oracle
+    comms, streams = two_comms
+    count = 100_003
+    ins = _inputs(2, count)
+    sends = [torch.from_numpy(x).cuda() for x in ins]
+    recvs = [torch.zeros(count, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    nccl_amd.group_start()
+    for c, s, x, y in zip(comms, streams, sends, recvs):
+        c.allreduce(x, y, nccl_amd.SUM, stream=s)
+    torch.cuda.synchronize()
+    assert not recvs[0].any() and not recvs[1].any(), "work started before ncclGroupEnd"
+    nccl_amd.group_end()
+    torch.cuda.synchronize()
+    want = oracle.all_reduce(ins, 7, 0)
+    for r, y in enumerate(recvs):
+        got = y.cpu().numpy()
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (f"rank {r}: {bad.size} mismatches, first {bad[:6].tolist()}, "
+                               f"got {got[bad[:4]].tolist()} want {want[bad[:4]].tolist()}, "
+                               f"async {[c.async_error() for c in comms]}")
+
+
+def test_group_of_mixed_collectives(two_comms):
+    import torch
+    import nccl_amd
+    import oracle
+    comms, streams = two_comms
+    n, count = 2, 65_536
+    ins = _inputs(n, count, seed=9)
+    sends = [torch.from_numpy(x).cuda() for x in ins]
+    ar = [torch.empty(count, device="cuda") for _ in range(n)]
+    rs = [torch.empty(count // n, device="cuda") for _ in range(n)]
+    ag = [torch.empty(count * n, device="cuda") for _ in range(n)]
+    mx = [torch.empty(count, device="cuda") for _ in range(n)]
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for r in range(n):
+            comms[r].allreduce(sends[r], ar[r], nccl_amd.SUM, stream=streams[r])
+            comms[r].reduce_scatter(sends[r], rs[r], nccl_amd.SUM, stream=streams[r])
+            comms[r].allgather(sends[r], ag[r], stream=streams[r])
+            comms[r].reduce(sends[r], mx[r], nccl_amd.MAX, root=1, stream=streams[r])
+    torch.cuda.synchronize()
+    assert np.array_equal(ar[0].cpu().numpy(), oracle.all_reduce(ins, 7, 0))
+    want_rs = oracle.reduce_scatter(ins, 7, 0)
+    for r in range(n):
+        assert np.array_equal(rs[r].cpu().numpy(), want_rs[r])
+        assert np.array_equal(ag[r].cpu().numpy(), np.concatenate(ins))
+    assert np.array_equal(mx[1].cpu().numpy(), oracle.reduce(ins, 7, 2, 1))
+
+
+@pytest.mark.parametrize("device_scalar", [False, True])
+def test_premulsum_custom_op(two_comms, device_scalar):
+    import torch
+    import nccl_amd
+    import oracle
+    comms, streams = two_comms
+    count = 50_001
+    ins = _inputs(2, count, seed=13)
+    scal = np.float32(0.375)
+    dev_scal = torch.tensor([scal], device="cuda")
+    ops = [c.create_pre_mul_sum(float(scal), 7, dev_scal.data_ptr() if device_scalar else None) for c in comms]
+    sends = [torch.from_numpy(x).cuda() for x in ins]
+    recvs = [torch.empty(count, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for c, s, x, y, op in zip(comms, streams, sends, recvs, ops):
+            c.allreduce(x, y, op, stream=s)
+    torch.cuda.synchronize()
+    want = oracle.all_reduce(ins, 7, premul_scalar_bits=int(scal.view(np.uint32)))
+    for y in recvs:
+        assert np.array_equal(y.cpu().numpy(), want)
+    for c, op in zip(comms, ops):
+        c.destroy_op(op)
+    with pytest.raises(nccl_amd.NcclError):
+        comms[0].destroy_op(ops[0])
+
+
+def test_hipgraph_capture_and_replay(two_comms):
+    import torch
+    import oracle
+    comms, streams = two_comms
+    count = 1 << 20
+    x = [torch.empty(count, device="cuda") for _ in range(2)]
+    y = [torch.empty(count, device="cuda") for _ in range(2)]
+    graphs = [torch.cuda.CUDAGraph() for _ in range(2)]
+    torch.cuda.synchronize()
+    for r in range(2):  # capture each rank's collective on its own stream (launches never block)
+        with torch.cuda.graph(graphs[r], stream=streams[r]):
+            comms[r].all_reduce_raw(x[r].data_ptr(), y[r].data_ptr(), count, 7, 0, streams[r].cuda_stream)
+    for it in range(3):
+        ins = _inputs(2, count, seed=100 + it)
+        for r in range(2):
+            x[r].copy_(torch.from_numpy(ins[r]))
+        torch.cuda.synchronize()
+        for r in range(2):  # replay each rank's graph on its own stream (both must run concurrently)
+            with torch.cuda.stream(streams[r]):
+                graphs[r].replay()
+        torch.cuda.synchronize()
+        want = oracle.all_reduce(ins, 7, 0)
+        for r in range(2):
+            assert np.array_equal(y[r].cpu().numpy(), want), f"replay {it} rank {r}"
+
+
+def test_init_rank_in_group_single_thread(built):
+    import torch
+    import nccl_amd
+    torch.cuda.set_device(0)
+    lib = nccl_amd.load()
+    uid = nccl_amd._uid(nccl_amd.get_unique_id())
+    cs = [ctypes.c_void_p(), ctypes.c_void_p()]
+    assert lib.ncclGroupStart() == 0
+    for r in range(2):
+        assert lib.ncclCommInitRank(ctypes.byref(cs[r]), 2, uid, r) == 0
+    assert lib.ncclGroupEnd() == 0
+    comms = [nccl_amd.Communicator(c.value) for c in cs]
+    assert [c.rank for c in comms] == [0, 1] and all(c.nranks == 2 for c in comms)
+    from tests import gpu_cases as G
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    errs = G.run_case(list(zip(comms, streams)), "allreduce", 9, 0, 123_457, 0, seed=3)
+    for c in comms:
+        c.destroy()
+    assert not errs, errs
+
+
+def test_spin_timeout_reports_async_error(built):
+    """Only one rank launches: its kernel must give up after NCCL_AMD_SPIN_TIMEOUT_MS and the comm
+    must report ncclSystemError, then refuse further work (reference async-error semantics)."""
+    import torch
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    old = os.environ.get("NCCL_AMD_SPIN_TIMEOUT_MS")
+    os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "1500"
+    try:
+        torch.cuda.set_device(0)
+        comms = nccl_amd.Communicator.init_all([0, 0])
+    finally:
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = old or "30000"
+    x = torch.ones(1 << 20, device="cuda")
+    y = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    t0 = time.time()
+    comms[0].allreduce(x, y, nccl_amd.SUM, stream=s)
+    s.synchronize()
+    assert time.time() - t0 < 30
+    assert comms[0].async_error() == 2  # ncclSystemError
+    with pytest.raises(nccl_amd.NcclError):
+        comms[0].allreduce(x, y, nccl_amd.SUM, stream=s)
+    comms[0].abort()
+    comms[1].abort()
+
+
+def test_abort_unblocks_stuck_collective(built):
+    import torch
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0])
+    x = torch.ones(1 << 20, device="cuda")
+    y = torch.empty_like(x)
+    s = torch.cuda.Stream()
+    comms[0].allreduce(x, y, nccl_amd.SUM, stream=s)  # peer never joins
+    time.sleep(0.5)
+    t0 = time.time()
+    comms[0].abort()  # sets the abort word, waits for the kernel to notice
+    assert time.time() - t0 < 20
+    comms[1].destroy()
