@@ -6,10 +6,10 @@
          --master-port P bench.py --gpus N --steps K --warmup W
 
 One "step" = one ncclAllReduce(sum, fp32) of the per-rank buffer, inputs already resident in HBM.
-Workload (BASELINE.json configs):
-  N == 1: configs[0] — 64 MiB fp32, world_size 1 loopback (the reference's nranks==1 out-of-place copy,
+Workload (BASELINE.json metric: 256 MiB fp32 at 1/2/4/8 GPUs):
+  N == 1: 256 MiB fp32, world_size 1 (the reference's nranks==1 out-of-place copy,
           src/device/onerank.cu:52-56). busBW is 0 by definition at n=1, so `value` is the HBM rate
-          2*S/t (read S + write S), as BASELINE.md §2 prescribes for this config.
+          2*S/t (read S + write S), as BASELINE.md §2 prescribes; configs[0] (64 MiB) is reported beside.
   N >= 2: the metric's 256 MiB fp32 per rank (configs[1] at N=2). `value` = whole-job bus bytes / time
           = N * busBW, busBW = algBW * 2(n-1)/n (reference plugins/profiler/inspector/inspector.cc:1450-1492).
           Per-rank busBW (the nccl-tests figure) is printed as `busbw_GBps`.
@@ -222,6 +222,30 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dic
     return out
 
 
+def host_staged(comm, n: int, count: int, stream, dist) -> dict:
+    """Buckets that start and end in pinned host memory: H2D copy + AllReduce + D2H copy per step."""
+    import torch
+    S = count * 4
+    h_in = torch.empty(count, dtype=torch.float32, pin_memory=True).uniform_(-1, 1)
+    h_out = torch.empty(count, dtype=torch.float32, pin_memory=True)
+    d_in = torch.empty(count, dtype=torch.float32, device="cuda")
+    d_out = torch.empty_like(d_in)
+
+    def step():
+        d_in.copy_(h_in, non_blocking=True)
+        comm.all_reduce_raw(d_in.data_ptr(), d_out.data_ptr(), count, 7, 0, stream.cuda_stream)
+        h_out.copy_(d_out, non_blocking=True)
+
+    ms = _time_ms(step, stream, 5, warmup=2)
+    ms = max_over_ranks(dist, [ms])[0]
+    ms_dev = _time_ms(lambda: comm.all_reduce_raw(d_in.data_ptr(), d_out.data_ptr(), count, 7, 0,
+                                                  stream.cuda_stream), stream, 5, warmup=2)
+    ms_dev = max_over_ranks(dist, [ms_dev])[0]
+    return {"bytes_per_rank": S, "ms_per_step": round(ms, 4), "algbw_GBps_incl_pcie": round(S / (ms * 1e-3) / 1e9, 2),
+            "device_resident_ms": round(ms_dev, 4),
+            "method": "pinned hipMemcpyAsync H2D + ncclAllReduce + D2H on one stream, HIP events"}
+
+
 def cpu_baseline(n: int, count: int, budget_s: float):
     """Naive OpenMP host reduction of n synthetic buffers, bounded to ~budget_s."""
     import numpy as np
@@ -284,10 +308,10 @@ def main(argv=None):
     else:
         comm = nccl_amd.Communicator.init_all([dev])[0]
 
-    size_mib = args.size_mib or (64 if n == 1 else 256)
+    size_mib = args.size_mib or 256
     S = size_mib * MIB
     count = S // 4
-    workload = (f"ncclAllReduce sum fp32, {size_mib} MiB, world_size=1 loopback" if n == 1 else
+    workload = (f"ncclAllReduce sum fp32, {size_mib} MiB, world_size=1 (the metric's size at N=1)" if n == 1 else
                 f"ncclAllReduce sum fp32, {size_mib} MiB per rank, {n}xMI355X direct scatter-reduce-gather")
     stream = torch.cuda.current_stream()
     send = torch.empty(count, dtype=torch.float32, device="cuda").uniform_(-1, 1)
@@ -359,30 +383,24 @@ def main(argv=None):
 
     extra = {}
     if n == 1 and not args.no_extra and rank == 0:
-        # secondary: the metric's 256 MiB at n=1 (> Infinity Cache, so HBM-bound)
-        big = 256 * MIB // 4
-        s2 = torch.empty(big, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+        # configs[0] (64 MiB loopback, fits the 256 MiB Infinity Cache) and hipMemcpyAsync D2D of the
+        # headline size (the reference's own nranks==1 implementation, onerank.cu:52-56) side by side
+        small = 64 * MIB // 4
+        s2 = torch.empty(small, dtype=torch.float32, device="cuda").uniform_(-1, 1)
         r2 = torch.empty_like(s2)
-        for _ in range(5):
-            comm.all_reduce_raw(s2.data_ptr(), r2.data_ptr(), big, 7, 0, stream.cuda_stream)
-        torch.cuda.synchronize()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record(stream)
-        for _ in range(20):
-            comm.all_reduce_raw(s2.data_ptr(), r2.data_ptr(), big, 7, 0, stream.cuda_stream)
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(b) / 20
-        extra["n1_256MiB_hbm_GBps"] = round(2 * 256 * MIB / (ms * 1e-3) / 1e9, 1)
-        # hipMemcpyAsync D2D of the same 256 MiB (the reference's nranks==1 implementation)
-        a.record(stream)
-        for _ in range(20):
-            r2.copy_(s2)
-        b.record(stream)
-        torch.cuda.synchronize()
-        ms = a.elapsed_time(b) / 20
-        extra["n1_256MiB_hipMemcpyD2D_GBps"] = round(2 * 256 * MIB / (ms * 1e-3) / 1e9, 1)
+        ms = _time_ms(lambda: comm.all_reduce_raw(s2.data_ptr(), r2.data_ptr(), small, 7, 0, stream.cuda_stream),
+                      stream, 20, warmup=5)
+        extra["n1_64MiB_hbm_GBps"] = round(2 * 64 * MIB / (ms * 1e-3) / 1e9, 1)
         del s2, r2
+        ms = _time_ms(lambda: recv.copy_(send), stream, 20, warmup=5)
+        extra[f"n1_{size_mib}MiB_hipMemcpyD2D_GBps"] = round(2 * S / (ms * 1e-3) / 1e9, 1)
+    if not args.no_extra:
+        # host-staged bucket (the proxy/network-staged path analogue, reference src/proxy.cc:954-1012):
+        # pinned host -> HBM, AllReduce, HBM -> pinned host, all on the launch stream
+        try:
+            extra["host_staged"] = host_staged(comm, n, count, stream, dist)
+        except Exception as e:  # secondary measurement
+            extra["host_staged"] = {"error": repr(e)}
 
     if n > 1 and not args.no_suite:
         try:

@@ -222,6 +222,33 @@ def _stream_ptr(stream, device: int) -> int:
     return stream.cuda_stream
 
 
+_HIP = None
+
+
+def dedicated_stream(device: int = 0):
+    """A torch ExternalStream with a hardware queue of its own (created with a full CU mask).
+
+    Only needed when several ranks share one GPU inside one process AND the caller replays captured
+    graphs of their collectives on its own streams: HIP multiplexes a process's streams onto a few
+    hardware queues, and two ranks' kernels on one queue would serialise (each spins on the other).
+    Direct ncclAllReduce/... calls handle this inside the library (ncclComm::internalStream)."""
+    global _HIP
+    import torch
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so", mode=ctypes.RTLD_GLOBAL)
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)(*([0xFFFFFFFF] * words))
+    if ncu % 32:
+        mask[words - 1] = (1 << (ncu % 32)) - 1
+    s = ctypes.c_void_p()
+    with torch.cuda.device(device):
+        rc = _HIP.hipExtStreamCreateWithCUMask(ctypes.byref(s), ctypes.c_uint32(words), mask)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed: {rc}")
+    return torch.cuda.ExternalStream(s.value, device=device)
+
+
 def _ptr(t) -> Optional[int]:
     if t is None:
         return None

@@ -133,7 +133,14 @@ struct ncclComm {
   int nSlots = 0;
   int maxChannels = 0;
   int chanCap = 0;  // channels per launch that stay co-resident even with several ranks per GPU
+  // Several ranks of this process on this GPU (test mode): their spinning kernels must run concurrently,
+  // but HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware queues, so two user streams
+  // can share one queue and serialise the ranks (deadlock until the spin timeout). Such comms launch on
+  // internalStream — created with a full CU mask, which always gets a hardware queue of its own — joined
+  // to the user stream by evIn/evOut (graph capture follows the fork/join).
+  bool sharedDevInProcess = false;
   hipStream_t internalStream = nullptr;
+  hipEvent_t evIn = nullptr, evOut = nullptr;
 
   std::vector<ncclamd::UserRedOp> userOps;
   std::atomic<int> asyncResult{ncclSuccess};
@@ -183,7 +190,10 @@ struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src
 };
 
 ncclResult_t enqueueCheck(CollInfo* info);
-ncclResult_t launchColl(const CollInfo& info);  // plan + launch (enqueue.cc)
+// plan + launch (enqueue.cc); forkJoin=false: the caller (group end) forks/joins shared-GPU comms itself
+ncclResult_t launchColl(const CollInfo& info, bool forkJoin = true);
+ncclResult_t collFork(const CollInfo& info);
+ncclResult_t collJoin(const CollInfo& info);
 ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
 ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 ncclResult_t warmKernels();  // load all kernel code objects on the current device (kernels.hip)

@@ -144,7 +144,7 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
   p.args.nSteps = (int)((part + slice - 1) / slice);
 }
 
-ncclResult_t launchColl(const CollInfo& info) {
+ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   ncclComm* comm = info.comm;
   HIPCHECK(hipSetDevice(comm->device));
   const int ts = typeSize(info.datatype);
@@ -226,7 +226,35 @@ ncclResult_t launchColl(const CollInfo& info) {
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,
         p.args.nSteps, p.args.aligned);
-  return launchPlan(p);
+  if (!comm->sharedDevInProcess) return launchPlan(p);
+  // on the comm's own hardware queue, between a fork and a join (see ncclComm::internalStream)
+  if (forkJoin) NCCLCHECK(collFork(info));
+  p.stream = comm->internalStream;
+  NCCLCHECK(launchPlan(p));
+  if (forkJoin) NCCLCHECK(collJoin(info));
+  return ncclSuccess;
+}
+
+// Fork / join of a shared-GPU comm's internal stream with the caller's stream. A group issues every
+// fork, then every launch, then every join: a join makes the user stream wait for the collective, and
+// if two ranks' user streams share a hardware queue, a join enqueued before the peer's fork would
+// hold that fork (and with it the peer's kernel) behind our unfinished kernel.
+ncclResult_t collFork(const CollInfo& info) {
+  ncclComm* comm = info.comm;
+  if (!comm->sharedDevInProcess) return ncclSuccess;
+  HIPCHECK(hipSetDevice(comm->device));
+  HIPCHECK(hipEventRecord(comm->evIn, info.stream));
+  HIPCHECK(hipStreamWaitEvent(comm->internalStream, comm->evIn, 0));
+  return ncclSuccess;
+}
+
+ncclResult_t collJoin(const CollInfo& info) {
+  ncclComm* comm = info.comm;
+  if (!comm->sharedDevInProcess) return ncclSuccess;
+  HIPCHECK(hipSetDevice(comm->device));
+  HIPCHECK(hipEventRecord(comm->evOut, comm->internalStream));
+  HIPCHECK(hipStreamWaitEvent(info.stream, comm->evOut, 0));
+  return ncclSuccess;
 }
 
 ncclResult_t enqueueCheck(CollInfo* info) {

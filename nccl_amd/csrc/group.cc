@@ -71,15 +71,12 @@ ncclResult_t groupEndInternal() {
   }
   int dev = 0;
   (void)hipGetDevice(&dev);
-  for (const CollInfo& c : colls) {
-    ncclResult_t r = launchColl(c);
-    if (r != ncclSuccess) {
-      (void)hipSetDevice(dev);
-      return r;
-    }
-  }
+  ncclResult_t r = ncclSuccess;
+  for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = collFork(colls[i]);
+  for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = launchColl(colls[i], false);
+  for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = collJoin(colls[i]);
   (void)hipSetDevice(dev);
-  return ncclSuccess;
+  return r;
 }
 
 }  // namespace ncclamd

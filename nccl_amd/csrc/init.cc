@@ -330,6 +330,8 @@ NCCL_ALIAS(ncclResult_t, ncclCommFinalize, ncclComm_t)
 
 static ncclResult_t commFree(ncclComm* comm) {
   if (comm->internalStream) (void)hipStreamDestroy(comm->internalStream);
+  if (comm->evIn) (void)hipEventDestroy(comm->evIn);
+  if (comm->evOut) (void)hipEventDestroy(comm->evOut);
   transportFree(comm);
   bootstrapClose(comm->bootstrap);
   comm->bootstrap = nullptr;

@@ -170,7 +170,17 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
   d.errorWord = (uint32_t*)dErr;
   HIPCHECK(hipMalloc((void**)&comm->devComm, sizeof(DevComm)));
   HIPCHECK(hipMemcpy(comm->devComm, &d, sizeof(DevComm), hipMemcpyHostToDevice));
-  HIPCHECK(hipStreamCreateWithFlags(&comm->internalStream, hipStreamNonBlocking));
+  const PeerInfo& me = comm->peers[comm->rank];
+  for (int r = 0; r < comm->nRanks; r++)
+    if (r != comm->rank && comm->peers[r].pid == me.pid && strcmp(comm->peers[r].busId, me.busId) == 0)
+      comm->sharedDevInProcess = true;
+  if (comm->sharedDevInProcess) {
+    std::vector<uint32_t> mask((me.numCUs + 31) / 32, 0u);
+    for (int cu = 0; cu < me.numCUs; cu++) mask[cu / 32] |= 1u << (cu % 32);
+    HIPCHECK(hipExtStreamCreateWithCUMask(&comm->internalStream, (uint32_t)mask.size(), mask.data()));
+    HIPCHECK(hipEventCreateWithFlags(&comm->evIn, hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&comm->evOut, hipEventDisableTiming));
+  }
   NCCLCHECK(warmKernels());
   return ncclSuccess;
 }

@@ -114,8 +114,11 @@ def test_premulsum_custom_op(two_comms, device_scalar):
 
 def test_hipgraph_capture_and_replay(two_comms):
     import torch
+    import nccl_amd
     import oracle
-    comms, streams = two_comms
+    comms, _ = two_comms
+    # replayed graphs run on the replay stream: give each rank a hardware queue of its own
+    streams = [nccl_amd.dedicated_stream(0), nccl_amd.dedicated_stream(0)]
     count = 1 << 20
     x = [torch.empty(count, device="cuda") for _ in range(2)]
     y = [torch.empty(count, device="cuda") for _ in range(2)]
