@@ -82,7 +82,7 @@ def _mp_worker(rank, nranks, uid, quick, q, env=None):
 
 # (nranks, env): the second group forces tiny staging slots so every channel runs many pipeline
 # steps with slot reuse (credit protocol, A(s+1)-before-C(s) ordering) at test sizes.
-MP_CASES = [(2, {}), (4, {}),
+MP_CASES = [(2, {}), (4, {}), (8, {}),
             (2, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
             (3, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
             (4, {"NCCL_AMD_SLOT_BYTES": "8192", "NCCL_AMD_NSLOTS": "3", "NCCL_MAX_CTAS": "7"}),
