@@ -197,6 +197,44 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dic
     out["reduce_int32"] = red
     del send, recv, base
 
+    # --- symmetric windows (zero-copy pull kernels): the headline AllReduce and the
+    #     fp16 latency curve with send/recv inside an NCCL_WIN_COLL_SYMMETRIC window ---
+    S = (16 if quick else 256) * MIB
+    c = S // 4
+    win_t = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
+    win = comm.register_window(win_t.data_ptr(), 2 * S)
+    sendw = win_t[:S].view(torch.float32)
+    recvw = win_t[S:].view(torch.float32)
+    g.manual_seed(4321)
+    base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
+    sendw.copy_(base * (rank + 1))
+    fn = lambda: comm.all_reduce_raw(sendw.data_ptr(), recvw.data_ptr(), c, 7, 0, sp)
+    ms = tmax(_time_ms(fn, stream, 20, warmup=5))
+    recvw.zero_()
+    fn()
+    torch.cuda.synchronize()
+    oks = bool(torch.equal(recvw, base * (n * (n + 1) / 2)))
+    sym = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, buffers in symmetric windows, n={n}",
+           "ms": round(ms, 4), "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+           "value_equiv_GBps": round(n * S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+           "check": "pass (dyadic, exact)" if agree(oks) else "FAIL"}
+    lat = []
+    hbuf = win_t[:S].view(torch.float16)
+    hres = win_t[S:].view(torch.float16)
+    size = 8
+    while size <= (16 if quick else 64) * MIB:
+        cc = size // 2
+        it = 50 if size <= 4 * MIB else 10
+        ms = tmax(_time_ms(lambda: comm.all_reduce_raw(hbuf.data_ptr(), hres.data_ptr(), cc, 6, 0, sp), stream, it))
+        lat.append({"bytes": size, "us": round(ms * 1e3, 2),
+                    "busbw_GBps": round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)})
+        size *= 4
+    sym["ar_fp16_sweep"] = lat
+    out["symmetric_window"] = sym
+    torch.cuda.synchronize()
+    comm.deregister_window(win)
+    del win_t, sendw, recvw, base, hbuf, hres
+
     # --- xGMI probes (rank 0, peer copies via hipMemcpyPeerAsync) ---
     ndev = torch.cuda.device_count()
     if rank == 0 and ndev > 1:

@@ -37,6 +37,17 @@ extern "C" {
 typedef struct ncclComm* ncclComm_t;
 #define NCCL_COMM_NULL NULL
 
+/* Opaque registered-memory window (nccl.h.in:37). */
+typedef struct ncclWindow_vidmem* ncclWindow_t;
+
+/* Window flags (nccl.h.in:64-68). NCCL_WIN_COLL_SYMMETRIC: every rank registers a buffer of the same size
+ * and passes buffers at the same offset inside it to collectives, which may then read and write peers'
+ * windows directly (zero-copy symmetric kernels). */
+#define NCCL_WIN_DEFAULT 0x00
+#define NCCL_WIN_COLL_SYMMETRIC 0x01
+#define NCCL_WIN_STRICT_ORDERING 0x02
+#define NCCL_WIN_REQUIRED_ALIGNMENT 4096
+
 /* 128-byte opaque rendezvous id (nccl.h.in:40-41). */
 #define NCCL_UNIQUE_ID_BYTES 128
 typedef struct {
@@ -192,6 +203,23 @@ ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device);
 ncclResult_t pncclCommCuDevice(const ncclComm_t comm, int* device);
 ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank);
 ncclResult_t pncclCommUserRank(const ncclComm_t comm, int* rank);
+
+/* ---- Buffer registration (nccl.h.in:301-307, 350-360) ---- */
+/* nccl.h.in:302 — local (non-collective) registration hint; see DESIGN.md §10. */
+ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
+ncclResult_t pncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
+/* nccl.h.in:306 */
+ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle);
+ncclResult_t pncclCommDeregister(const ncclComm_t comm, void* handle);
+/* nccl.h.in:351 — collective over the communicator (inside a group when one thread drives several ranks). */
+ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, size_t size, ncclWindow_t* win, int winFlags);
+ncclResult_t pncclCommWindowRegister(ncclComm_t comm, void* buff, size_t size, ncclWindow_t* win, int winFlags);
+/* nccl.h.in:355 */
+ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win);
+ncclResult_t pncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win);
+/* nccl.h.in:359 */
+ncclResult_t ncclWinGetUserPtr(ncclComm_t comm, ncclWindow_t win, void** outUserPtr);
+ncclResult_t pncclWinGetUserPtr(ncclComm_t comm, ncclWindow_t win, void** outUserPtr);
 
 /* ---- Custom reduction operators (nccl.h.in:418-431) ---- */
 ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,

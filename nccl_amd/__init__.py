@@ -111,7 +111,15 @@ EXPORTED = [
     "ncclGetErrorString", "ncclGetLastError", "ncclCommGetAsyncError", "ncclCommCount", "ncclCommCuDevice",
     "ncclCommUserRank", "ncclRedOpCreatePreMulSum", "ncclRedOpDestroy", "ncclReduce", "ncclAllReduce",
     "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
+    "ncclCommRegister", "ncclCommDeregister", "ncclCommWindowRegister", "ncclCommWindowDeregister",
+    "ncclWinGetUserPtr",
 ]
+
+
+WIN_DEFAULT = 0x00          # nccl.h.in:64-68
+WIN_COLL_SYMMETRIC = 0x01
+WIN_STRICT_ORDERING = 0x02
+WIN_REQUIRED_ALIGNMENT = 4096
 
 
 def load(path: Optional[str] = None) -> ctypes.CDLL:
@@ -149,6 +157,11 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ncclGroupStart": (R, []),
         "ncclGroupEnd": (R, []),
         "ncclMemAlloc": (R, [ctypes.POINTER(P), S]),
+        "ncclCommRegister": (R, [P, P, S, ctypes.POINTER(P)]),
+        "ncclCommDeregister": (R, [P, P]),
+        "ncclCommWindowRegister": (R, [P, P, S, ctypes.POINTER(P), I]),
+        "ncclCommWindowDeregister": (R, [P, P]),
+        "ncclWinGetUserPtr": (R, [P, P, ctypes.POINTER(P)]),
         "ncclMemFree": (R, [P]),
     }
     for name, (res, args) in sig.items():
@@ -255,6 +268,18 @@ def _ptr(t) -> Optional[int]:
     return t.data_ptr()
 
 
+class Window:
+    """An ncclWindow_t; the handle storage stays alive until the (possibly deferred) registration ends."""
+
+    def __init__(self, comm: "Communicator"):
+        self.comm = comm
+        self._h = ctypes.c_void_p()
+
+    @property
+    def handle(self) -> int:
+        return self._h.value or 0
+
+
 class Communicator:
     """Mirror of nccl4py's Communicator (bindings/nccl4py/nccl/core/communicator.py:223)."""
 
@@ -355,6 +380,34 @@ class Communicator:
     def reduce_raw(self, send: int, recv: Optional[int], count: int, dtype: int, op: int, root: int,
                    stream: int) -> None:
         _check(load().ncclReduce(send, recv, count, dtype, op, root, self._comm, stream), "ncclReduce")
+
+    # ---- registration (nccl.h.in:301-360; nccl4py Communicator.register_buffer / register_window) ----
+    def register_buffer(self, ptr: int, size: int) -> int:
+        """ncclCommRegister (local); returns the handle."""
+        h = ctypes.c_void_p()
+        _check(load().ncclCommRegister(self._comm, ptr, size, ctypes.byref(h)), "ncclCommRegister")
+        return h.value or 0
+
+    def deregister_buffer(self, handle: int) -> None:
+        _check(load().ncclCommDeregister(self._comm, handle), "ncclCommDeregister")
+
+    def register_window(self, ptr: int, size: int, flags: int = WIN_COLL_SYMMETRIC) -> "Window":
+        """ncclCommWindowRegister (collective: every rank calls it; one thread driving several ranks
+        calls it inside group(), and the handle is filled in when the group ends)."""
+        w = Window(self)
+        _check(load().ncclCommWindowRegister(self._comm, ptr, size, ctypes.byref(w._h), flags),
+               "ncclCommWindowRegister")
+        return w
+
+    def deregister_window(self, win) -> None:
+        h = win.handle if isinstance(win, Window) else win
+        _check(load().ncclCommWindowDeregister(self._comm, h), "ncclCommWindowDeregister")
+
+    def window_user_ptr(self, win) -> int:
+        h = win.handle if isinstance(win, Window) else win
+        p = ctypes.c_void_p()
+        _check(load().ncclWinGetUserPtr(self._comm, h, ctypes.byref(p)), "ncclWinGetUserPtr")
+        return p.value or 0
 
     # ---- custom operators ----
     def create_pre_mul_sum(self, scalar, dtype: int, device_scalar_ptr: Optional[int] = None) -> int:

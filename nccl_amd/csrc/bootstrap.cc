@@ -20,6 +20,9 @@
 
 #include <chrono>
 #include <random>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -222,6 +225,45 @@ ncclResult_t bootstrapAllGather(Bootstrap* b, void* data, size_t bytesPerRank) {
 ncclResult_t bootstrapBarrier(Bootstrap* b) {
   std::vector<char> tmp(b->nranks);
   return bootstrapAllGather(b, tmp.data(), 1);
+}
+
+// In-process all-gather for the comms of one ncclCommInitAll (no sockets: they share this object).
+// Two generation-counted barriers per round: all blocks are in, then all copies are out, so a fast rank
+// cannot start the next round while a slow one still reads this one.
+struct LocalClique {
+  std::mutex m;
+  std::condition_variable cv;
+  int n = 0;
+  int arrived = 0;
+  uint64_t gen = 0;
+  std::vector<char> buf;
+};
+
+std::shared_ptr<LocalClique> cliqueCreate(int nranks) {
+  auto c = std::make_shared<LocalClique>();
+  c->n = nranks;
+  return c;
+}
+
+static void cliqueBarrier(LocalClique* c, std::unique_lock<std::mutex>& lk) {
+  uint64_t g = c->gen;
+  if (++c->arrived == c->n) {
+    c->arrived = 0;
+    c->gen++;
+    c->cv.notify_all();
+  } else {
+    c->cv.wait(lk, [&] { return c->gen != g; });
+  }
+}
+
+ncclResult_t cliqueAllGather(LocalClique* c, int rank, void* data, size_t bytesPerRank) {
+  std::unique_lock<std::mutex> lk(c->m);
+  if (c->buf.size() < bytesPerRank * c->n) c->buf.resize(bytesPerRank * c->n);
+  memcpy(c->buf.data() + (size_t)rank * bytesPerRank, (char*)data + (size_t)rank * bytesPerRank, bytesPerRank);
+  cliqueBarrier(c, lk);
+  memcpy(data, c->buf.data(), bytesPerRank * c->n);
+  cliqueBarrier(c, lk);
+  return ncclSuccess;
 }
 
 void bootstrapClose(Bootstrap* b) {

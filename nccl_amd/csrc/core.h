@@ -9,6 +9,7 @@
 
 #include <atomic>
 #include <functional>
+#include <memory>
 #include <cstdint>
 #include <cstdio>
 #include <mutex>
@@ -74,11 +75,14 @@ const char* paramStr(const char* name);  // nullptr when unset
 
 // ---------------------------------------------------------------- bootstrap (reference src/bootstrap.cc)
 struct Bootstrap;
+struct LocalClique;
 ncclResult_t bootstrapGetUniqueId(ncclUniqueId* id);
 ncclResult_t bootstrapInit(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out);
 ncclResult_t bootstrapAllGather(Bootstrap* b, void* data, size_t bytesPerRank);
 ncclResult_t bootstrapBarrier(Bootstrap* b);
 void bootstrapClose(Bootstrap* b);
+std::shared_ptr<LocalClique> cliqueCreate(int nranks);
+ncclResult_t cliqueAllGather(LocalClique* c, int rank, void* data, size_t bytesPerRank);
 
 // ---------------------------------------------------------------- communicator (reference src/include/comm.h)
 constexpr uint64_t kCommMagic = 0x4d493335584e4343ull;  // "MI35XNCC"
@@ -104,8 +108,27 @@ struct UserRedOp {  // ncclRedOpCreatePreMulSum state (reference src/enqueue.cc:
   const void* scalarPtr;   // device scalar (ncclScalarDevice), read by the kernel
 };
 
+
+// One peer mapping of a registered allocation (HIP IPC, refcounted per comm: a segment is opened once).
+struct IpcMapping {
+  int peer;
+  uint64_t base;   // allocation base in the peer's address space
+  void* mapped;    // the same allocation as mapped here
+  int refs;
+};
+
 struct ncclCommImpl;
 }  // namespace ncclamd
+
+// A registered window (reference struct ncclWindow_vidmem / ncclDevrWindow, src/dev_runtime.cc).
+struct ncclWindow_vidmem {
+  ncclComm* comm;
+  void* userPtr;
+  size_t size;
+  int flags;
+  char* peerPtr[NCCL_AMD_MAX_RANKS];  // every rank's window base as mapped in this process
+  uint64_t peerBase[NCCL_AMD_MAX_RANKS];  // allocation bases of IPC-mapped peers (0: direct pointer)
+};
 
 // The opaque handle type of the public header.
 struct ncclComm {
@@ -141,6 +164,11 @@ struct ncclComm {
   bool sharedDevInProcess = false;
   hipStream_t internalStream = nullptr;
   hipEvent_t evIn = nullptr, evOut = nullptr;
+
+  std::shared_ptr<ncclamd::LocalClique> clique;  // ncclCommInitAll comms: in-process all-gather
+  std::vector<ncclWindow_vidmem*> windows;        // registered windows (register.cc)
+  std::vector<ncclamd::IpcMapping> ipcMaps;
+  std::vector<void*> regHandles;                   // ncclCommRegister handles
 
   std::vector<ncclamd::UserRedOp> userOps;
   std::atomic<int> asyncResult{ncclSuccess};
@@ -195,6 +223,22 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin = true);
 ncclResult_t collFork(const CollInfo& info);
 ncclResult_t collJoin(const CollInfo& info);
 ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
+
+struct SymPlan {  // one symmetric (window) kernel launch
+  int coll;       // SymColl (kernels.h)
+  ncclDataType_t datatype;
+  int eltSize;
+  int devOp;
+  int nChannels;
+  hipStream_t stream;
+  SymArgs args;
+};
+ncclResult_t launchSymPlan(const SymPlan& plan);  // kernels.hip
+// window lookup: the window holding [p, p+bytes) with NCCL_WIN_COLL_SYMMETRIC, or nullptr (register.cc)
+ncclWindow_vidmem* findSymWindow(ncclComm* comm, const void* p, size_t bytes);
+void windowsFree(ncclComm* comm);  // release every window and IPC mapping (destroy/abort)
+// all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
+ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);
 ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream);
 ncclResult_t warmKernels();  // load all kernel code objects on the current device (kernels.hip)
 int typeSize(ncclDataType_t t);

@@ -11,10 +11,12 @@
 //       RS_READY[c][from]  = number of RS slices `from` has written into my staging (monotonic)
 //       RS_ACK[c][from]    = number of my RS slices `from` has consumed from ITS staging
 //       AG_READY / AG_ACK  = the same for the all-gather direction
+//       SYM_ENTER / SYM_MID / SYM_DONE[c][from] = epoch of the last symmetric (window) collective in
+//                          which `from` entered / published its reduced block / finished reading peers
 //     A word is written by exactly one remote rank and polled only by its owner.
 //
 //   counters (plain device memory, local)
-//     uint64 [channel][ctr kind < 4 (sendRS, recvRS, sendAG, recvAG)][peer < NCCL_AMD_MAX_RANKS]
+//     uint64 [channel][ctr kind < 5 (sendRS, recvRS, sendAG, recvAG, sym)][peer < NCCL_AMD_MAX_RANKS]
 //     Per-connection step counters (reference: conn->step, src/device/prims_simple.h:100-173),
 //     kept in device memory so a captured hipGraph replays correctly.
 #pragma once
@@ -26,8 +28,11 @@
 namespace ncclamd {
 
 enum StagingKind { STG_RS = 0, STG_AG = 1, STG_KINDS = 2 };
-enum FlagKind { FLG_RS_READY = 0, FLG_RS_ACK = 1, FLG_AG_READY = 2, FLG_AG_ACK = 3, FLG_KINDS = 4 };
-enum CtrKind { CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_KINDS = 4 };
+enum FlagKind {
+  FLG_RS_READY = 0, FLG_RS_ACK = 1, FLG_AG_READY = 2, FLG_AG_ACK = 3,
+  FLG_SYM_ENTER = 4, FLG_SYM_MID = 5, FLG_SYM_DONE = 6, FLG_KINDS = 7
+};
+enum CtrKind { CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_SYM = 4, CTR_KINDS = 5 };
 
 // Device reduction kinds (reference ncclDevRedOp_t subset, src/include/device.h)
 enum DevRedOp { DEV_SUM = 0, DEV_PROD = 1, DEV_MINMAX = 2, DEV_PREMULSUM = 3, DEV_SUMPOSTDIV = 4, DEV_NUMOPS = 5 };
@@ -65,6 +70,20 @@ struct CollArgs {
   int root;
   int aligned;         // send/recv base pointers are 16-byte aligned
   int protoFlags;      // NCCL_AMD_PROTO_FLAGS diagnostics (kernels.h collKernel)
+};
+
+// Symmetric (window) collective arguments: every rank's buffers as mapped in this process (reference
+// ncclSymPtr::peerPtr, src/device/symmetric/kernel.cuh), so peers are read and written directly.
+struct SymArgs {
+  const DevComm* comm;
+  const char* send[NCCL_AMD_MAX_RANKS];  // rank r's sendbuff
+  char* recv[NCCL_AMD_MAX_RANKS];        // rank r's recvbuff
+  uint64_t count;      // AR: elements; RS: recvcount; AG: sendcount
+  uint64_t chunk;      // elements per rank block
+  uint64_t part;       // elements per channel (AR two-shot / RS / AG: within a block; one-shot: of the buffer)
+  uint64_t redArg;
+  const void* redArgPtr;
+  int aligned;
 };
 
 __host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int kind, int slot, int from) {

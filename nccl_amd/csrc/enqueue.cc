@@ -216,6 +216,75 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     if (algo && !strcasecmp(algo, "ONESHOT")) oneShot = true;
     if (algo && (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE"))) oneShot = false;
   }
+  const bool oneShotAR = oneShot;
+  // Symmetric windows (reference: symmetric kernels for buffers in NCCL_WIN_COLL_SYMMETRIC windows,
+  // src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*): zero-copy pull kernels.
+  if (info.func != FUNC_REDUCE && !paramInt("NCCL_AMD_SYM_DISABLE", 0)) {
+    size_t sb = count * ts, rb = count * ts;
+    if (info.func == FUNC_REDUCESCATTER) sb *= n;
+    if (info.func == FUNC_ALLGATHER) rb *= n;
+    ncclWindow_vidmem* ws = findSymWindow(comm, info.sendbuff, sb);
+    ncclWindow_vidmem* wr = ws ? findSymWindow(comm, info.recvbuff, rb) : nullptr;
+    if (ws && wr) {
+      SymPlan sp;
+      memset(&sp, 0, sizeof(sp));
+      sp.datatype = info.datatype;
+      sp.eltSize = ts;
+      sp.devOp = p.devOp;
+      sp.args.comm = comm->devComm;
+      sp.args.count = count;
+      sp.args.chunk = blockElems;
+      sp.args.redArg = p.args.redArg;
+      sp.args.redArgPtr = p.args.redArgPtr;
+      uintptr_t al = 0;
+      // in-place AllGather: rank r's input is block r of ITS output, not the offset of mine
+      const bool agInPlace = info.func == FUNC_ALLGATHER &&
+                             (const char*)info.sendbuff == (const char*)info.recvbuff + (size_t)comm->rank * count * ts;
+      for (int r = 0; r < n; r++) {
+        sp.args.send[r] = ws->peerPtr[r] + ((const char*)info.sendbuff - (const char*)ws->userPtr);
+        sp.args.recv[r] = wr->peerPtr[r] + ((char*)info.recvbuff - (char*)wr->userPtr);
+        if (agInPlace) sp.args.send[r] = sp.args.recv[r] + (size_t)r * count * ts;
+        al |= (uintptr_t)sp.args.send[r] | (uintptr_t)sp.args.recv[r];
+      }
+      bool symAligned = (al & 15) == 0 && !paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0);
+      if (info.func != FUNC_ALLREDUCE) symAligned = symAligned && ((count * ts) & 15) == 0;
+      sp.args.aligned = symAligned ? 1 : 0;
+      size_t spanBytes = blockElems * ts;  // what one channel plan divides
+      size_t minPart = (size_t)paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
+      int maxCh = comm->chanCap;
+      if (info.func == FUNC_ALLREDUCE) {
+        // one-shot needs out-of-place buffers: in place, peers would still read what this rank overwrites
+        bool out = info.sendbuff != info.recvbuff;
+        sp.coll = (oneShotAR && out) ? 1 /*SYM_AR1*/ : 0 /*SYM_AR*/;
+        if (sp.coll == 1) {
+          spanBytes = count * ts;
+          minPart = (size_t)paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
+          maxCh = maxCh < 32 ? maxCh : 32;
+        }
+      } else {
+        sp.coll = info.func == FUNC_REDUCESCATTER ? 2 /*SYM_RS*/ : 3 /*SYM_AG*/;
+      }
+      int nch = (int)((spanBytes + minPart - 1) / minPart);
+      if (nch < comm->minCTAs) nch = comm->minCTAs;
+      if (nch > maxCh) nch = maxCh;
+      if (nch < 1) nch = 1;
+      uint64_t spanElems = spanBytes / ts;
+      uint64_t part = (spanElems + nch - 1) / nch;
+      part = (part + epp - 1) / epp * epp;
+      if (part == 0) part = epp;
+      sp.args.part = part;
+      sp.nChannels = nch;
+      sp.stream = info.stream;
+      TRACE("%s: symmetric coll %d nch %d part %lu aligned %d", info.opName, sp.coll, nch, (unsigned long)part,
+            sp.args.aligned);
+      if (!comm->sharedDevInProcess) return launchSymPlan(sp);
+      if (forkJoin) NCCLCHECK(collFork(info));
+      sp.stream = comm->internalStream;
+      NCCLCHECK(launchSymPlan(sp));
+      if (forkJoin) NCCLCHECK(collJoin(info));
+      return ncclSuccess;
+    }
+  }
   if (oneShot) {
     p.algo = ALGO_ONESHOT;
     planChannels(comm, count * ts, ts, p, (size_t)paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10), 32);

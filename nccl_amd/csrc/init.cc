@@ -300,7 +300,11 @@ NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
       }
     return res;
   }
-  for (int i = 0; i < ndev; i++) comms[i] = cs[i];
+  auto clique = cliqueCreate(ndev);
+  for (int i = 0; i < ndev; i++) {
+    cs[i]->clique = clique;
+    comms[i] = cs[i];
+  }
   INFO("ncclCommInitAll COMPLETE: %d ranks", ndev);
   return ncclSuccess;
 }
@@ -329,6 +333,7 @@ NCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
 NCCL_ALIAS(ncclResult_t, ncclCommFinalize, ncclComm_t)
 
 static ncclResult_t commFree(ncclComm* comm) {
+  windowsFree(comm);
   if (comm->internalStream) (void)hipStreamDestroy(comm->internalStream);
   if (comm->evIn) (void)hipEventDestroy(comm->evIn);
   if (comm->evOut) (void)hipEventDestroy(comm->evOut);

@@ -9,4 +9,7 @@ hipError_t warmKernBF16() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<bf16_t, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernBF16(const SymPlan& p) {
+  return launchSymOp<bf16_t>(p);
+}
 }  // namespace ncclamd

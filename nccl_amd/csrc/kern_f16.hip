@@ -9,4 +9,7 @@ hipError_t warmKernF16() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<half_t, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernF16(const SymPlan& p) {
+  return launchSymOp<half_t>(p);
+}
 }  // namespace ncclamd

@@ -9,4 +9,7 @@ hipError_t warmKernF32() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<float, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernF32(const SymPlan& p) {
+  return launchSymOp<float>(p);
+}
 }  // namespace ncclamd

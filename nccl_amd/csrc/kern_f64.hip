@@ -9,4 +9,7 @@ hipError_t warmKernF64() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<double, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernF64(const SymPlan& p) {
+  return launchSymOp<double>(p);
+}
 }  // namespace ncclamd

@@ -9,4 +9,7 @@ hipError_t warmKernFp8() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<e4m3_t, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernFp8(const SymPlan& p) {
+  return p.datatype == ncclFloat8e4m3 ? launchSymOp<e4m3_t>(p) : launchSymOp<e5m2_t>(p);
+}
 }  // namespace ncclamd

@@ -14,4 +14,12 @@ hipError_t warmKernGather() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<uint32_t, 0, COLL_AG>);
 }
+ncclResult_t launchSymKernGather(const SymPlan& p) {
+  switch (p.eltSize) {
+    case 1: return launchSymTyped<uint8_t, 0>(p);
+    case 2: return launchSymTyped<uint16_t, 0>(p);
+    case 4: return launchSymTyped<uint32_t, 0>(p);
+    default: return launchSymTyped<uint64_t, 0>(p);
+  }
+}
 }  // namespace ncclamd

@@ -9,4 +9,7 @@ hipError_t warmKernU32() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<uint32_t, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernU32(const SymPlan& p) {
+  return launchSymIntOp<uint32_t>(p);
+}
 }  // namespace ncclamd

@@ -9,4 +9,7 @@ hipError_t warmKernU64() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<uint64_t, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernU64(const SymPlan& p) {
+  return launchSymIntOp<uint64_t>(p);
+}
 }  // namespace ncclamd

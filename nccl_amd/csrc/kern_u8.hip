@@ -9,4 +9,7 @@ hipError_t warmKernU8() {
   hipFuncAttributes attr;
   return hipFuncGetAttributes(&attr, (const void*)&collKernel<uint8_t, 0, COLL_AR>);
 }
+ncclResult_t launchSymKernU8(const SymPlan& p) {
+  return launchSymIntOp<uint8_t>(p);
+}
 }  // namespace ncclamd

@@ -554,6 +554,165 @@ __global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------ symmetric windows
+//
+// Zero-copy collectives over registered symmetric windows (reference src/device/symmetric/all_reduce.cuh,
+// reduce_scatter.cuh, all_gather.cuh: LSA barrier arrive at entry, wait before touching peers, sync at
+// exit). Every rank's buffers are mapped here, so there is no staging: per channel
+//   ENTER  tell every peer my inputs are ready (my kernel started: stream order), wait for theirs;
+//   RS     the owner of block q pulls block q's channel part from all n inputs, folds it in the
+//          reference's ring order (q+1, ..., q) and stores it in its own output;
+//   MID    (AllReduce) publish that part (system release) and wait until every owner has published;
+//   AG     pull the other n-1 reduced parts from the owners' outputs into my output;
+//   DONE   tell every peer I finished reading its buffers and wait until all peers have: only then
+//          may the stream reuse my buffers.
+// Only remote LOADS cross xGMI (plus flag stores): user buffers are never written remotely, so no
+// peer's L2 can hold a stale copy of bytes written behind its back; remote bytes are read after a
+// system-scope acquire. Link bytes are those of the staged path, local HBM traffic drops from
+// 2S + 4(n-1)S/n to about 3S, and one handshake round replaces the per-slice credit protocol.
+// The epoch of each channel lives in device memory (counters[c][CTR_SYM]), so graphs replay.
+enum SymColl { SYM_AR = 0, SYM_AR1 = 1, SYM_RS = 2, SYM_AG = 3 };
+
+struct SymShared {
+  ChanState st;
+  const char* srcPtr[NCCL_AMD_MAX_RANKS];
+  uint64_t want[NCCL_AMD_MAX_RANKS];
+  uint64_t* sigPtr[NCCL_AMD_MAX_RANKS];
+  uint64_t sigVal[NCCL_AMD_MAX_RANKS];
+};
+
+// Every lane i < n (i != me) stores `e` into peer i's flag word [c][kind][me]; REL publishes my prior stores.
+__device__ __forceinline__ void symSignal(const DevComm& dc, SymShared& sh, int c, int kind, uint64_t e, bool REL) {
+  const int tid = threadIdx.x, me = dc.rank;
+  if (tid < NCCL_AMD_MAX_RANKS) {
+    bool peer = tid < dc.nRanks && tid != me;
+    sh.sigVal[tid] = peer ? e : 0;
+    sh.sigPtr[tid] = peer ? dc.flags[tid] + flagIndex(c, kind, me) : nullptr;
+  }
+  __syncthreads();
+  signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, REL);
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool symWait(const DevComm& dc, SymShared& sh, int c, int kind, uint64_t e, bool ACQ) {
+  const int tid = threadIdx.x, me = dc.rank;
+  if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < dc.nRanks && tid != me) ? e : 0;
+  __syncthreads();
+  return waitAll(dc, sh.st, dc.flags[me] + flagIndex(c, kind, 0), sh.want, ACQ);
+}
+
+template <typename T, int OP, int COLL>
+__global__ void __launch_bounds__(kThreads) symKernel(SymArgs a) {
+  __shared__ SymShared sh;
+  const DevComm& dc = *a.comm;
+  const int tid = threadIdx.x, c = blockIdx.x, me = dc.rank, n = dc.nRanks;
+  constexpr uint64_t ts = sizeof(T);
+  if (tid == 0) sh.st.abort = 0;
+  const uint64_t e = dc.counters[ctrIndex(c, CTR_SYM, 0)] + 1;
+  uint64_t opArg = a.redArg;
+  if (a.redArgPtr) {
+    opArg = 0;
+    __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
+  }
+  const Red<T, OP> fn(opArg);
+  const bool aligned = a.aligned != 0;
+  auto blockLen = [&](int q) -> uint64_t {
+    if (COLL == SYM_RS || COLL == SYM_AG) return a.chunk;
+    uint64_t b = (uint64_t)q * a.chunk;
+    return b >= a.count ? 0 : min(a.chunk, a.count - b);
+  };
+  auto partOf = [&](uint64_t len, uint64_t& lo, uint64_t& hi) {
+    lo = min((uint64_t)c * a.part, len);
+    hi = min(lo + a.part, len);
+  };
+  bool ok;
+  symSignal(dc, sh, c, FLG_SYM_ENTER, e, false);
+  ok = symWait(dc, sh, c, FLG_SYM_ENTER, e, true);
+  if (ok && COLL == SYM_AR1) {
+    // one-shot: fold my channel's portion of the whole buffer from all n inputs, owner block by block
+    uint64_t lo, hi;
+    partOf(a.count, lo, hi);
+    for (uint64_t x = lo; x < hi;) {
+      const int owner = (int)(x / a.chunk);
+      const uint64_t end = min(hi, (uint64_t)(owner + 1) * a.chunk);
+      if (tid == 0)
+        for (int k = 0; k < n; k++) sh.srcPtr[k] = a.send[(owner + 1 + k) % n] + x * ts;
+      __syncthreads();
+      foldRange<T, OP>(fn, n, sh.srcPtr, end - x, a.recv[me] + x * ts, nullptr, 0, aligned);
+      __syncthreads();
+      x = end;
+    }
+  } else if (ok && COLL != SYM_AG) {
+    // RS: fold my block's channel part; fold order owner+1, ..., owner (all_reduce.h:43-66)
+    uint64_t lo, hi;
+    partOf(blockLen(me), lo, hi);
+    if (tid == 0)
+      for (int k = 0; k < n; k++) sh.srcPtr[k] = a.send[(me + 1 + k) % n] + ((uint64_t)me * a.chunk + lo) * ts;
+    __syncthreads();
+    char* dst = COLL == SYM_RS ? a.recv[me] + lo * ts : a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
+    foldRange<T, OP>(fn, n, sh.srcPtr, hi - lo, dst, nullptr, 0, aligned);
+    __syncthreads();
+  }
+  if (ok && COLL == SYM_AR) {
+    symSignal(dc, sh, c, FLG_SYM_MID, e, true);  // my reduced part is in my output: publish it
+    ok = symWait(dc, sh, c, FLG_SYM_MID, e, true);
+  }
+  if (ok && (COLL == SYM_AR || COLL == SYM_AG)) {
+    // AG: pull every other rank's block part (AR: its reduced output; AG: its input)
+    for (int k = 1; k < n; k++) {
+      const int q = (me + n - k) % n;
+      uint64_t lo, hi;
+      partOf(blockLen(q), lo, hi);
+      const char* src = COLL == SYM_AR ? a.recv[q] + ((uint64_t)q * a.chunk + lo) * ts : a.send[q] + lo * ts;
+      copyRange<T, false>(a.recv[me] + ((uint64_t)q * a.chunk + lo) * ts, src, (hi - lo) * ts, aligned);
+    }
+    if (COLL == SYM_AG) {  // my own block (skipped in place)
+      uint64_t lo, hi;
+      partOf(a.chunk, lo, hi);
+      char* dst = a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
+      const char* src = a.send[me] + lo * ts;
+      if (dst != src) copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
+    }
+    __syncthreads();
+  }
+  if (ok) {
+    symSignal(dc, sh, c, FLG_SYM_DONE, e, false);  // drained: I no longer read any peer's buffers
+    ok = symWait(dc, sh, c, FLG_SYM_DONE, e, false);
+  }
+  (void)ok;  // on failure the error word is set and the epoch still advances (the comm is unusable)
+  if (tid == 0) dc.counters[ctrIndex(c, CTR_SYM, 0)] = e;
+}
+
+template <typename T, int OP>
+inline ncclResult_t launchSymTyped(const SymPlan& p) {
+  switch (p.coll) {
+    case SYM_AR: hipLaunchKernelGGL((symKernel<T, OP, SYM_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+    case SYM_AR1: hipLaunchKernelGGL((symKernel<T, OP, SYM_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+    case SYM_RS: hipLaunchKernelGGL((symKernel<T, OP, SYM_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+    case SYM_AG: hipLaunchKernelGGL((symKernel<T, 0, SYM_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+  }
+  HIPCHECK(hipGetLastError());
+  return ncclSuccess;
+}
+
+template <typename T>
+inline ncclResult_t launchSymOp(const SymPlan& p) {
+  switch (p.devOp) {
+    case DEV_SUM: return launchSymTyped<T, DEV_SUM>(p);
+    case DEV_PROD: return launchSymTyped<T, DEV_PROD>(p);
+    case DEV_MINMAX: return launchSymTyped<T, DEV_MINMAX>(p);
+    case DEV_PREMULSUM: return launchSymTyped<T, DEV_PREMULSUM>(p);
+    default: break;
+  }
+  WARN("internal: op %d unsupported for this type", p.devOp);
+  return ncclInternalError;
+}
+template <typename T>
+inline ncclResult_t launchSymIntOp(const SymPlan& p) {
+  if (p.devOp == DEV_SUMPOSTDIV) return launchSymTyped<T, DEV_SUMPOSTDIV>(p);
+  return launchSymOp<T>(p);
+}
+
 // ------------------------------------------------------------------------------------ nRanks == 1
 
 // PreMulSum on one rank (reference onerank.cu:14-47): out = post(pre(in)).

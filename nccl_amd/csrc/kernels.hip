@@ -13,6 +13,15 @@ ncclResult_t launchKernF32(const LaunchPlan& p);
 ncclResult_t launchKernF64(const LaunchPlan& p);
 ncclResult_t launchKernFp8(const LaunchPlan& p);
 ncclResult_t launchKernGather(const LaunchPlan& p);
+ncclResult_t launchSymKernU8(const SymPlan& p);
+ncclResult_t launchSymKernU32(const SymPlan& p);
+ncclResult_t launchSymKernU64(const SymPlan& p);
+ncclResult_t launchSymKernF16(const SymPlan& p);
+ncclResult_t launchSymKernBF16(const SymPlan& p);
+ncclResult_t launchSymKernF32(const SymPlan& p);
+ncclResult_t launchSymKernF64(const SymPlan& p);
+ncclResult_t launchSymKernFp8(const SymPlan& p);
+ncclResult_t launchSymKernGather(const SymPlan& p);
 hipError_t warmKernU8();
 hipError_t warmKernU32();
 hipError_t warmKernU64();
@@ -110,6 +119,22 @@ ncclResult_t launchPlan(const LaunchPlan& p) {
     case ncclFloat32: return launchKernF32(p);
     case ncclFloat64: return launchKernF64(p);
     case ncclFloat8e4m3: case ncclFloat8e5m2: return launchKernFp8(p);
+    default: break;
+  }
+  return ncclInvalidArgument;
+}
+
+ncclResult_t launchSymPlan(const SymPlan& p) {
+  if (p.coll == SYM_AG) return launchSymKernGather(p);
+  switch (p.datatype) {
+    case ncclInt8: case ncclUint8: return launchSymKernU8(p);
+    case ncclInt32: case ncclUint32: return launchSymKernU32(p);
+    case ncclInt64: case ncclUint64: return launchSymKernU64(p);
+    case ncclFloat16: return launchSymKernF16(p);
+    case ncclBfloat16: return launchSymKernBF16(p);
+    case ncclFloat32: return launchSymKernF32(p);
+    case ncclFloat64: return launchSymKernF64(p);
+    case ncclFloat8e4m3: case ncclFloat8e5m2: return launchSymKernFp8(p);
     default: break;
   }
   return ncclInvalidArgument;

@@ -1,0 +1,207 @@
+"""GPU parity tests of the symmetric-window (zero-copy) kernels: ncclCommWindowRegister with
+NCCL_WIN_COLL_SYMMETRIC, then AllReduce (two-shot and one-shot), ReduceScatter and AllGather whose buffers
+lie in the windows run kernels.h symKernel, which pulls peers' buffers directly. Results must be
+bit-identical to the oracle (same fold order as the staged path). Reduce and non-symmetric windows fall
+back to the staged path. All ranks share the box's one GPU (single process: raw pointers; multi-process:
+HIP IPC of the window allocations)."""
+import multiprocessing as mp
+import os
+
+import numpy as np
+import pytest
+
+os.environ.setdefault("NCCL_AMD_SPIN_TIMEOUT_MS", "30000")
+pytestmark = pytest.mark.gpu
+
+WIN_BYTES = 8 << 20          # per-rank window; send at [0, half), recv at [half, WIN_BYTES)
+HALF = WIN_BYTES // 2
+
+
+def _cases(n, quick=False):
+    """(collective, dtype, op, count, elem_offset, inplace)"""
+    out = []
+    counts = [1, 7, 4096 + 5, 200_003] if not quick else [7, 70_001]
+    for dtype, op in ((7, 0), (9, 0), (6, 0), (2, 3), (3, 2), (4, 1), (0, 0), (8, 4), (2, 4), (10, 0)):
+        for count in counts:
+            out.append(("allreduce", dtype, op, count, 0, False))
+        out.append(("reducescatter", dtype, op, 50_001 * n, 0, False))
+        out.append(("allgather", dtype, 0, 30_001, 0, False))
+    for coll in ("allreduce", "reducescatter", "allgather"):
+        out.append((coll, 7, 0, 100_000 * (n if coll == "reducescatter" else 1), 0, True))
+        out.append((coll, 7, 0, 64_000 * (n if coll == "reducescatter" else 1), 3, False))  # unaligned
+    out.append(("allreduce", 7, 0, 300_000, 0, True))  # large in-place (two-shot even when small)
+    out.append(("reduce", 2, 3, 100_003, 0, False))    # no symmetric Reduce: staged fallback
+    return out
+
+
+def _run(comms_streams, bases, coll, dtype, op, count, off, inplace, seed, root=0):
+    """bases[i] = device pointer of rank i's window (same layout on every rank)."""
+    import torch
+    import oracle
+    from tests import gpu_cases as G
+    n = comms_streams[0][0].nranks
+    npdt = oracle.NP_STORAGE[dtype]
+    es = np.dtype(npdt).itemsize
+    inputs = G.make_inputs(n, dtype, count, seed)
+    exp = G.expected(coll, inputs, dtype, op, root)
+    ocount = G.out_count(coll, n, count)
+    views = []
+    for (comm, stream), (base_t, base) in zip(comms_streams, bases):
+        r = comm.rank
+        raw = base_t.view(torch.uint8)
+        send_off = off * es
+        recv_off = HALF + off * es
+        if inplace:
+            recv_off = send_off
+        if coll == "allgather" and inplace:
+            full = np.zeros(count * n, dtype=npdt)
+            full[r * count:(r + 1) * count] = inputs[r]
+            raw[recv_off:recv_off + full.nbytes].copy_(torch.from_numpy(full.view(np.uint8).copy()))
+            send_ptr = base + recv_off + r * count * es
+        else:
+            data = np.ascontiguousarray(inputs[r]).view(np.uint8)
+            raw[send_off:send_off + data.size].copy_(torch.from_numpy(data.copy()))
+            send_ptr = base + send_off
+            if not inplace:
+                raw[recv_off:recv_off + ocount * es].zero_()
+        recv_ptr = base + recv_off
+        if coll == "reducescatter" and inplace:
+            recv_ptr = base + send_off + r * (count // n) * es
+        views.append((comm, stream, send_ptr, recv_ptr, raw, base))
+    torch.cuda.synchronize()
+    import nccl_amd
+    with nccl_amd.group():
+        for comm, stream, sp, rp, _, _ in views:
+            sid = stream.cuda_stream
+            if coll == "allreduce":
+                comm.all_reduce_raw(sp, rp, count, dtype, op, sid)
+            elif coll == "reducescatter":
+                comm.reduce_scatter_raw(sp, rp, count // n, dtype, op, sid)
+            elif coll == "allgather":
+                comm.all_gather_raw(sp, rp, count, dtype, sid)
+            else:
+                comm.reduce_raw(sp, rp if comm.rank == root else None, count, dtype, op, root, sid)
+    errs = []
+    for comm, stream, sp, rp, raw, base in views:
+        stream.synchronize()
+        if comm.async_error():
+            errs.append(f"rank {comm.rank}: async error {comm.async_error()}")
+            continue
+        if coll == "reduce" and comm.rank != root:
+            continue
+        start = rp - base  # offset of recv inside the window
+        got = raw[start:start + ocount * es].cpu().numpy().view(npdt)
+        want = exp[0] if coll == "reduce" else exp[comm.rank]
+        if not G.same_bits(got, want, dtype):
+            bad = np.nonzero(got != want)[0]
+            errs.append(f"rank {comm.rank} {coll} dt={dtype} op={op} count={count} off={off} inplace={inplace}: "
+                        f"{bad.size} mismatches, first {bad[:5].tolist()} got {got[bad[:3]].tolist()} "
+                        f"want {want[bad[:3]].tolist()}")
+    return errs
+
+
+def _windows(comms, streams_dev=0):
+    import torch
+    import nccl_amd
+    bufs = [torch.empty(WIN_BYTES, dtype=torch.uint8, device=f"cuda:{c.device}") for c in comms]
+    with nccl_amd.group():
+        wins = [c.register_window(b.data_ptr(), WIN_BYTES) for c, b in zip(comms, bufs)]
+    assert all(w.handle for w in wins)
+    for c, w, b in zip(comms, wins, bufs):
+        assert c.window_user_ptr(w) == b.data_ptr()
+    return bufs, wins
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_windows_single_process(built, nranks):
+    import torch
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0] * nranks)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    bufs, wins = _windows(comms)
+    cs = list(zip(comms, streams))
+    bases = [(b, b.data_ptr()) for b in bufs]
+    errs = []
+    for i, case in enumerate(_cases(nranks, quick=nranks > 2)):
+        errs += _run(cs, bases, *case, seed=i, root=i % nranks)
+        if errs:
+            break
+    for c, w in zip(comms, wins):
+        c.deregister_window(w)
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
+def test_window_without_symmetric_flag_uses_staged_path(built):
+    import torch
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0])
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    bufs = [torch.empty(WIN_BYTES, dtype=torch.uint8, device="cuda") for _ in comms]
+    with nccl_amd.group():
+        wins = [c.register_window(b.data_ptr(), WIN_BYTES, nccl_amd.WIN_DEFAULT) for c, b in zip(comms, bufs)]
+    errs = _run(list(zip(comms, streams)), [(b, b.data_ptr()) for b in bufs], "allreduce", 7, 0, 123_457, 0, False, 5)
+    h = comms[0].register_buffer(bufs[0].data_ptr(), 1024)
+    comms[0].deregister_buffer(h)
+    with pytest.raises(nccl_amd.NcclError):
+        comms[0].deregister_buffer(h)
+    for c, w in zip(comms, wins):
+        c.deregister_window(w)
+    for c in comms:
+        c.destroy()
+    assert not errs, errs
+
+
+def _mp_worker(rank, nranks, uid, q):
+    try:
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        buf = torch.empty(WIN_BYTES, dtype=torch.uint8, device="cuda")
+        win = comm.register_window(buf.data_ptr(), WIN_BYTES)
+        s = torch.cuda.Stream()
+        errs = []
+        for i, case in enumerate(_cases(nranks, quick=True)):
+            errs += _run([(comm, s)], [(buf, buf.data_ptr())], *case, seed=i, root=i % nranks)
+            if errs:
+                break
+        comm.deregister_window(win)
+        comm.destroy()
+        q.put((rank, errs))
+    except Exception as e:
+        q.put((rank, [f"rank {rank} exception: {e!r}"]))
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_windows_multi_process(built, nranks):
+    import queue
+    import time
+    import nccl_amd
+    uid = nccl_amd.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_mp_worker, args=(r, nranks, uid, q)) for r in range(nranks)]
+    for p in ps:
+        p.start()
+    results = {}
+    t0 = time.time()
+    while len(results) < nranks and time.time() - t0 < 600:
+        try:
+            r, errs = q.get(timeout=30)
+            results[r] = errs
+        except queue.Empty:
+            if not any(p.is_alive() for p in ps):
+                break
+    for p in ps:
+        if p.is_alive() and len(results) < nranks:
+            p.kill()
+        p.join(timeout=60)
+    assert len(results) == nranks, f"only {len(results)} of {nranks} ranks reported"
+    bad = [e for r in sorted(results) for e in results[r]]
+    assert not bad, "\n".join(bad[:20])

@@ -88,3 +88,16 @@ def test_bootstrap_across_processes(built, n):
     env = dict(os.environ, NCCL_AMD_BOOTSTRAP_TIMEOUT_MS="20000")
     r = subprocess.run([exe, str(n), "4"], env=env, capture_output=True, text=True, timeout=60)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_registration_argument_checks_without_gpu(built):
+    lib = nccl_amd.load()
+    P = ctypes.c_void_p
+    h = P()
+    assert lib.ncclCommRegister(None, P(16), 64, ctypes.byref(h)) == 4       # NULL comm
+    assert lib.ncclCommDeregister(None, None) == 4
+    w = P()
+    assert lib.ncclCommWindowRegister(None, P(16), 64, ctypes.byref(w), 1) == 4
+    assert lib.ncclCommWindowDeregister(None, None) == 4
+    out = P()
+    assert lib.ncclWinGetUserPtr(None, None, ctypes.byref(out)) == 4
