@@ -157,16 +157,24 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dic
     while size <= top:
         c = size // 2
         row = {"bytes": size}
-        for algo in ("ONESHOT", "DIRECT"):
+        for algo in ("LL", "ONESHOT", "DIRECT"):
             if algo == "ONESHOT" and size > 64 * MIB:
                 continue
-            os.environ["NCCL_ALGO"] = algo
+            if algo == "LL":
+                if size > 256 * 1024:  # the LL line area holds 256 KiB of payload
+                    continue
+                os.environ.pop("NCCL_ALGO", None)
+                os.environ["NCCL_PROTO"] = "LL"
+            else:
+                os.environ.pop("NCCL_PROTO", None)
+                os.environ["NCCL_ALGO"] = algo
             it = 50 if size <= 4 * MIB else 10
             ms = tmax(_time_ms(lambda: comm.all_reduce_raw(buf.data_ptr(), res.data_ptr(), c, 6, 0, sp), stream, it))
             row[algo.lower() + "_us"] = round(ms * 1e3, 2)
             row[algo.lower() + "_busbw_GBps"] = round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)
         sweep.append(row)
         size *= 2
+    os.environ.pop("NCCL_PROTO", None)
     if old is None:
         os.environ.pop("NCCL_ALGO", None)
     else:

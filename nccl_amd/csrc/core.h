@@ -155,6 +155,8 @@ struct ncclComm {
   size_t slotBytes = 0;
   int nSlots = 0;
   int maxChannels = 0;
+  int llChannels = 32;      // LL protocol: channels and line bytes per (channel, parity, sender)
+  size_t llBytes = 32 << 10;
   int chanCap = 0;  // channels per launch that stay co-resident even with several ranks per GPU
   // Several ranks of this process on this GPU (test mode): their spinning kernels must run concurrently,
   // but HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware queues, so two user streams
@@ -203,7 +205,7 @@ struct CollInfo {  // reference: struct ncclInfo, src/include/info.h:17-41
   hipStream_t stream;
 };
 
-enum Algo { ALGO_COPY = 0, ALGO_ONERANK = 1, ALGO_DIRECT = 2, ALGO_ONESHOT = 3 };
+enum Algo { ALGO_COPY = 0, ALGO_ONERANK = 1, ALGO_DIRECT = 2, ALGO_ONESHOT = 3, ALGO_LL = 4 };
 
 struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src/include/comm.h)
   CollFunc func;

@@ -15,6 +15,11 @@
 //                          which `from` entered / published its reduced block / finished reading peers
 //     A word is written by exactly one remote rank and polled only by its owner.
 //
+//   LL lines (same uncached allocation as the flags, at DevComm::llOffset; reference prims_ll.h:108-158)
+//     [channel < llChannels][parity < 2][from < nRanks][llBytes]: 16-byte lines {data32, flag32, data32,
+//     flag32} written by `from` with one write-through store; the flag is the channel's LL epoch, so the
+//     reader needs neither a flag word nor a fence. Parity = epoch & 1 (double buffering).
+//
 //   counters (plain device memory, local)
 //     uint64 [channel][ctr kind < 5 (sendRS, recvRS, sendAG, recvAG, sym)][peer < NCCL_AMD_MAX_RANKS]
 //     Per-connection step counters (reference: conn->step, src/device/prims_simple.h:100-173),
@@ -32,7 +37,7 @@ enum FlagKind {
   FLG_RS_READY = 0, FLG_RS_ACK = 1, FLG_AG_READY = 2, FLG_AG_ACK = 3,
   FLG_SYM_ENTER = 4, FLG_SYM_MID = 5, FLG_SYM_DONE = 6, FLG_KINDS = 7
 };
-enum CtrKind { CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_SYM = 4, CTR_KINDS = 5 };
+enum CtrKind { CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_SYM = 4, CTR_LL = 5, CTR_KINDS = 6 };
 
 // Device reduction kinds (reference ncclDevRedOp_t subset, src/include/device.h)
 enum DevRedOp { DEV_SUM = 0, DEV_PROD = 1, DEV_MINMAX = 2, DEV_PREMULSUM = 3, DEV_SUMPOSTDIV = 4, DEV_NUMOPS = 5 };
@@ -50,6 +55,9 @@ struct DevComm {
   char* staging[NCCL_AMD_MAX_RANKS];     // every rank's staging base as mapped here
   uint64_t* flags[NCCL_AMD_MAX_RANKS];   // every rank's flag block as mapped here
   uint64_t* counters;                    // local step counters
+  uint64_t llOffset;                     // LL line area inside every rank's flag allocation
+  uint64_t llBytes;                      // line bytes per (channel, parity, sender)
+  int llChannels;
   uint32_t* abortFlag;                   // host-pinned; nonzero = abort
   uint32_t* errorWord;                   // host-pinned; first DevError recorded
 };
@@ -88,6 +96,9 @@ struct SymArgs {
 
 __host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int kind, int slot, int from) {
   return ((((uint64_t)c * STG_KINDS + kind) * dc.nSlots + slot) * dc.nRanks + from) * dc.slotBytes;
+}
+__host__ __device__ inline uint64_t llLineOffset(const DevComm& dc, int c, int parity, int from) {
+  return dc.llOffset + (((uint64_t)c * 2 + parity) * dc.nRanks + from) * dc.llBytes;
 }
 __host__ __device__ inline uint64_t flagIndex(int c, int kind, int from) {
   return ((uint64_t)c * FLG_KINDS + kind) * NCCL_AMD_MAX_RANKS + from;

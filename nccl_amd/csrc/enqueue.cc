@@ -217,6 +217,49 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     if (algo && (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE"))) oneShot = false;
   }
   const bool oneShotAR = oneShot;
+  // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): tiny AllReduce, 8-byte aligned buffers, fits the
+  // comm's line area (llChannels x llBytes/16 payloads of 8 bytes). NCCL_PROTO may force or exclude it.
+  if (info.func == FUNC_ALLREDUCE) {
+    size_t bytes = count * (size_t)ts;
+    size_t npk = (bytes + 7) / 8;
+    size_t cap = (size_t)comm->llChannels * (comm->llBytes / 16);
+    bool llOn = true, simpleOn = true;
+    if (const char* proto = paramStr("NCCL_PROTO")) {  // reference syntax: "LL,Simple" or "^LL128"
+      bool exclude = proto[0] == '^';
+      bool hasLL = false, hasSimple = false;
+      std::string list(proto + (exclude ? 1 : 0));
+      size_t pos = 0;
+      while (pos <= list.size()) {
+        size_t comma = list.find(',', pos);
+        std::string tok = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+        hasLL |= !strcasecmp(tok.c_str(), "LL");
+        hasSimple |= !strcasecmp(tok.c_str(), "Simple");
+        if (comma == std::string::npos) break;
+        pos = comma + 1;
+      }
+      llOn = exclude ? !hasLL : hasLL;
+      simpleOn = exclude ? !hasSimple : hasSimple;
+    }
+    // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
+    // NCCL_PROTO leaves only LL enabled
+    bool useLL = llOn && (!simpleOn || (!paramStr("NCCL_ALGO") && bytes <= (size_t)paramInt("NCCL_AMD_LL_BYTES", 128 << 10)));
+    const bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
+    if (useLL && al8 && npk <= cap) {
+      const uint64_t perCh = (uint64_t)paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096) / 8;
+      int nch = (int)((npk + perCh - 1) / perCh);
+      if (nch < 1) nch = 1;
+      if (nch > comm->llChannels) nch = comm->llChannels;
+      if (nch > comm->chanCap) nch = comm->chanCap;
+      uint64_t part = (npk + nch - 1) / nch;
+      if (part * 16 <= comm->llBytes) {
+        p.algo = ALGO_LL;
+        p.nChannels = nch;
+        p.args.part = part;
+        TRACE("%s: LL count %zu nch %d part %lu payloads", info.opName, count, nch, (unsigned long)part);
+        goto launch;
+      }
+    }
+  }
   // Symmetric windows (reference: symmetric kernels for buffers in NCCL_WIN_COLL_SYMMETRIC windows,
   // src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*): zero-copy pull kernels.
   if (info.func != FUNC_REDUCE && !paramInt("NCCL_AMD_SYM_DISABLE", 0)) {
@@ -295,6 +338,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,
         p.args.nSteps, p.args.aligned);
+launch:
   if (!comm->sharedDevInProcess) return launchPlan(p);
   // on the comm's own hardware queue, between a fork and a join (see ncclComm::internalStream)
   if (forkJoin) NCCLCHECK(collFork(info));

@@ -554,6 +554,124 @@ __global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------ LL one-shot
+//
+// Low-latency AllReduce for small buffers (reference prims_ll.h:108-158, LL protocol). Every 8 bytes of
+// payload travel as half of a 16-byte line {data32, flag32, data32, flag32} stored with ONE system-scope
+// write-through store into each peer's LL area; the flag is the channel's LL epoch. A reader polls the
+// lines themselves (8-byte system-scope atomic loads: each half is single-copy atomic), so neither side
+// needs a flag word, a release fence or an acquire fence — the one-shot path's two handshakes and two
+// cache-maintenance fences become one one-way trip. Line areas are double-buffered by epoch parity: a
+// sender reaches epoch e+2 on a channel only after receiving every peer's e+1 lines, which each peer
+// sends only after finishing epoch e, so parity e's lines are never overwritten while still unread.
+// Fold order per element is the reference ring order of its owner block (owner+1, ..., owner): results
+// are identical to the other AllReduce paths.
+__device__ __forceinline__ uint64_t loadLL(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <typename T, int OP>
+__global__ void __launch_bounds__(kThreads) llKernel(CollArgs a) {
+  __shared__ int abortSh;
+  const DevComm& dc = *a.comm;
+  const int tid = threadIdx.x, c = blockIdx.x, me = dc.rank, n = dc.nRanks;
+  constexpr int EPP = 8 / sizeof(T);  // elements per 8-byte payload
+  if (tid == 0) abortSh = 0;
+  uint64_t opArg = a.redArg;
+  if (a.redArgPtr) {
+    opArg = 0;
+    __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
+  }
+  const Red<T, OP> fn(opArg);
+  const uint64_t e64 = dc.counters[ctrIndex(c, CTR_LL, 0)] + 1;
+  const uint32_t flag = (uint32_t)e64 ? (uint32_t)e64 : 1u;  // never 0 (the area starts zeroed)
+  const int par = (int)(e64 & 1);
+  __syncthreads();
+  const uint64_t nbytes = a.count * sizeof(T);
+  const uint64_t npk = (nbytes + 7) / 8;
+  const uint64_t lo = min((uint64_t)c * a.part, npk), hi = min(lo + a.part, npk);
+  const char* send = (const char*)a.sendbuff;
+  char* recv = (char*)a.recvbuff;
+
+  // send: my payload of [lo,hi) to every peer, 16-byte lines (two 8-byte payloads per line)
+  for (uint64_t i = lo + 2 * tid; i < hi; i += 2 * kThreads) {
+    uint64_t v[2] = {0, 0};
+    for (int h = 0; h < 2; h++) {
+      uint64_t pk = i + h;
+      if (pk >= hi) break;
+      if (pk * 8 + 8 <= nbytes) v[h] = *(const uint64_t*)(send + pk * 8);
+      else for (uint64_t b = pk * 8; b < nbytes; b++) v[h] |= (uint64_t)(unsigned char)send[b] << (8 * (b - pk * 8));
+    }
+    u32x4 line = {(uint32_t)v[0], flag, (uint32_t)(v[0] >> 32), flag};
+    u32x4 line2 = {(uint32_t)v[1], flag, (uint32_t)(v[1] >> 32), flag};
+    const uint64_t off = (i - lo) * 16;  // two payloads = two 16-byte lines
+    for (int k = 1; k < n; k++) {
+      int p = (me + k) % n;
+      char* base = (char*)dc.flags[p] + llLineOffset(dc, c, par, me) + off;
+      storeRemote(base, line);
+      if (i + 1 < hi) storeRemote(base + 16, line2);
+    }
+  }
+  // receive + fold: one 8-byte payload per thread step (after the barrier every input byte has been
+  // sent, so an in-place output cannot overwrite a payload another thread still has to send)
+  __syncthreads();
+  const uint64_t t0 = clockTicks();
+  for (uint64_t pk = lo + tid; pk < hi; pk += kThreads) {
+    const uint64_t firstElt = pk * 8 / sizeof(T);
+    const int owner = (int)(firstElt / a.chunk);  // 8-byte payloads never straddle rank blocks
+    // pass 1: wait until every peer's line for this payload carries this epoch's flag
+    uint32_t pending = 0;
+    for (int q = 0; q < n; q++)
+      if (q != me) pending |= 1u << q;
+    const char* myLL = (const char*)dc.flags[me];
+    uint32_t spins = 0;
+    while (pending) {
+      for (int q = 0; q < n; q++) {
+        if (!(pending & (1u << q))) continue;
+        const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
+        if ((uint32_t)(loadLL(ln) >> 32) == flag && (uint32_t)(loadLL(ln + 1) >> 32) == flag) pending &= ~(1u << q);
+      }
+      if (pending) __builtin_amdgcn_s_sleep(1);
+      if (pending && (++spins & 1023) == 0) {
+        if (__hip_atomic_load(dc.abortFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          reportError(dc, DERR_ABORT);
+          abortSh = 1;
+        } else if (__hip_atomic_load(dc.errorWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                   clockTicks() - t0 > dc.timeoutTicks) {
+          reportError(dc, DERR_TIMEOUT);
+          abortSh = 1;
+        }
+        if (abortSh) break;
+      }
+    }
+    if (pending) break;
+    // pass 2: fold in the owner block's ring order (the lines stay valid until epoch + 2)
+    union { uint64_t u; T e[EPP]; } acc, x;
+    for (int k = 0; k < n; k++) {
+      int q = (owner + 1 + k) % n;
+      if (q == me) {
+        x.u = 0;
+        if (pk * 8 + 8 <= nbytes) x.u = *(const uint64_t*)(send + pk * 8);
+        else for (uint64_t b = pk * 8; b < nbytes; b++) x.u |= (uint64_t)(unsigned char)send[b] << (8 * (b - pk * 8));
+      } else {
+        const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
+        x.u = (loadLL(ln) & 0xffffffffull) | (loadLL(ln + 1) << 32);
+      }
+#pragma unroll
+      for (int j = 0; j < EPP; j++) {
+        T y = fn.pre(x.e[j]);
+        acc.e[j] = k == 0 ? y : fn.red(y, acc.e[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < EPP; j++) acc.e[j] = fn.post(acc.e[j]);
+    if (pk * 8 + 8 <= nbytes) *(uint64_t*)(recv + pk * 8) = acc.u;
+    else for (uint64_t b = pk * 8; b < nbytes; b++) recv[b] = (char)(acc.u >> (8 * (b - pk * 8)));
+  }
+  __syncthreads();
+  if (tid == 0) dc.counters[ctrIndex(c, CTR_LL, 0)] = e64;
+}
+
 // ------------------------------------------------------------------------------------ symmetric windows
 //
 // Zero-copy collectives over registered symmetric windows (reference src/device/symmetric/all_reduce.cuh,
@@ -743,7 +861,9 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
   }
   switch (p.func) {
     case FUNC_ALLREDUCE:
-      if (p.algo == ALGO_ONESHOT)
+      if (p.algo == ALGO_LL)
+        hipLaunchKernelGGL((llKernel<T, OP>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      else if (p.algo == ALGO_ONESHOT)
         hipLaunchKernelGGL((collKernel<T, OP, COLL_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       else
         hipLaunchKernelGGL((collKernel<T, OP, COLL_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);

@@ -20,8 +20,12 @@ namespace ncclamd {
 static size_t stagingBytes(const ncclComm* c) {
   return (size_t)c->maxChannels * STG_KINDS * c->nSlots * c->nRanks * c->slotBytes;
 }
-static size_t flagsBytes(const ncclComm* c) {
+static size_t flagWordBytes(const ncclComm* c) {
   return (size_t)c->maxChannels * FLG_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
+}
+static size_t llOffset(const ncclComm* c) { return (flagWordBytes(c) + 4095) / 4096 * 4096; }
+static size_t flagsBytes(const ncclComm* c) {
+  return llOffset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes;
 }
 
 ncclResult_t transportSetup(ncclComm* comm) {
@@ -91,7 +95,7 @@ ncclResult_t transportConnect(ncclComm* comm) {
 ncclResult_t transportDrainCredits(ncclComm* comm) {
   if (comm->nRanks == 1 || !comm->counters || !comm->flags) return ncclSuccess;
   const size_t nc = (size_t)comm->maxChannels * CTR_KINDS * NCCL_AMD_MAX_RANKS;
-  const size_t nf = (size_t)comm->maxChannels * FLG_KINDS * NCCL_AMD_MAX_RANKS;
+  const size_t nf = flagWordBytes(comm) / sizeof(uint64_t);
   std::vector<uint64_t> ctr(nc), flg(nf);
   HIPCHECK(hipMemcpy(ctr.data(), comm->counters, nc * sizeof(uint64_t), hipMemcpyDeviceToHost));
   const int64_t limitMs = paramInt("NCCL_AMD_DESTROY_TIMEOUT_MS", 10000);
@@ -162,6 +166,9 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
     d.flags[r] = comm->peerFlags[r];
   }
   d.counters = comm->counters;
+  d.llOffset = llOffset(comm);
+  d.llBytes = comm->llBytes;
+  d.llChannels = comm->llChannels;
   void* dAbort = nullptr;
   void* dErr = nullptr;
   HIPCHECK(hipHostGetDevicePointer(&dAbort, comm->hostAbort, 0));

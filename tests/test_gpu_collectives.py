@@ -87,6 +87,8 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (3, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
             (4, {"NCCL_AMD_SLOT_BYTES": "8192", "NCCL_AMD_NSLOTS": "3", "NCCL_MAX_CTAS": "7"}),
             (3, {"NCCL_ALGO": "ONESHOT", "NCCL_AMD_SLOT_BYTES": "16384"}),
+            (3, {"NCCL_PROTO": "LL"}),
+            (2, {"NCCL_PROTO": "^LL"}),
             (2, {"NCCL_ALGO": "DIRECT"})]
 
 

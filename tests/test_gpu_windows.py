@@ -13,6 +13,13 @@ import pytest
 os.environ.setdefault("NCCL_AMD_SPIN_TIMEOUT_MS", "30000")
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _no_ll(monkeypatch):
+    """Small AllReduce would take the LL protocol (which needs no window); exclude it so the symmetric
+    one-shot kernel is what these tests exercise."""
+    monkeypatch.setenv("NCCL_PROTO", "^LL")
+
 WIN_BYTES = 8 << 20          # per-rank window; send at [0, half), recv at [half, WIN_BYTES)
 HALF = WIN_BYTES // 2
 
@@ -159,6 +166,7 @@ def test_window_without_symmetric_flag_uses_staged_path(built):
 
 def _mp_worker(rank, nranks, uid, q):
     try:
+        os.environ["NCCL_PROTO"] = "^LL"
         import torch
         import nccl_amd
         torch.cuda.set_device(0)
