@@ -217,12 +217,16 @@ struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src
   size_t bytes;
   hipStream_t stream;
   CollArgs args;
+  LLBatchArgs ll;  // ALGO_LL
 };
 
 ncclResult_t enqueueCheck(CollInfo* info);
 // plan + launch (enqueue.cc); forkJoin=false: the caller (group end) forks/joins shared-GPU comms itself
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin = true);
 ncclResult_t collFork(const CollInfo& info);
+bool llPlan(const CollInfo& info, LLOp* op);                  // LL eligibility + plan (enqueue.cc)
+bool llBatchable(const CollInfo& a, const CollInfo& b);
+ncclResult_t launchLLBatch(const std::vector<CollInfo>& ops);  // one LL launch for a group's small ARs
 ncclResult_t collJoin(const CollInfo& info);
 ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
 

@@ -80,6 +80,26 @@ struct CollArgs {
   int protoFlags;      // NCCL_AMD_PROTO_FLAGS diagnostics (kernels.h collKernel)
 };
 
+// LL AllReduce batch: up to kMaxLLBatch small AllReduce ops of one group (same comm, stream, type and
+// op) run by ONE launch (reference: ops of a group aggregated into one kernel plan, enqueue.cc:405-470).
+constexpr int kMaxLLBatch = 32;
+struct LLOp {
+  const void* send;
+  void* recv;
+  uint64_t count;  // elements
+  uint64_t chunk;  // elements per rank block (fold order of each element's owner)
+  uint64_t part;   // 8-byte payloads per channel
+  int nch;         // channels this op uses
+  int pad;
+};
+struct LLBatchArgs {
+  const DevComm* comm;
+  uint64_t redArg;
+  const void* redArgPtr;
+  int nOps;
+  LLOp ops[kMaxLLBatch];
+};
+
 // Symmetric (window) collective arguments: every rank's buffers as mapped in this process (reference
 // ncclSymPtr::peerPtr, src/device/symmetric/kernel.cuh), so peers are read and written directly.
 struct SymArgs {

@@ -144,6 +144,91 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
   p.args.nSteps = (int)((part + slice - 1) / slice);
 }
 
+// LL eligibility and channel plan of one AllReduce (reference tuning: LL for the smallest sizes, or as
+// NCCL_PROTO dictates). Needs 8-byte aligned buffers and room in the comm's line area.
+bool llPlan(const CollInfo& info, LLOp* op) {
+  ncclComm* comm = info.comm;
+  if (info.func != FUNC_ALLREDUCE || comm->nRanks == 1) return false;
+  const int ts = typeSize(info.datatype);
+  const size_t bytes = info.count * (size_t)ts;
+  const size_t npk = (bytes + 7) / 8;
+  bool llOn = true, simpleOn = true;
+  if (const char* proto = paramStr("NCCL_PROTO")) {  // reference syntax: "LL,Simple" or "^LL128"
+    bool exclude = proto[0] == '^';
+    bool hasLL = false, hasSimple = false;
+    std::string list(proto + (exclude ? 1 : 0));
+    size_t pos = 0;
+    while (true) {
+      size_t comma = list.find(',', pos);
+      std::string tok = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+      hasLL |= !strcasecmp(tok.c_str(), "LL");
+      hasSimple |= !strcasecmp(tok.c_str(), "Simple");
+      if (comma == std::string::npos) break;
+      pos = comma + 1;
+    }
+    llOn = exclude ? !hasLL : hasLL;
+    simpleOn = exclude ? !hasSimple : hasSimple;
+  }
+  // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
+  // NCCL_PROTO leaves only LL enabled
+  bool useLL = llOn && (!simpleOn || (!paramStr("NCCL_ALGO") && bytes <= (size_t)paramInt("NCCL_AMD_LL_BYTES", 128 << 10)));
+  const bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
+  if (!useLL || !al8 || npk > (size_t)comm->llChannels * (comm->llBytes / 16)) return false;
+  const uint64_t perCh = (uint64_t)paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096) / 8;
+  int nch = (int)((npk + perCh - 1) / perCh);
+  if (nch < 1) nch = 1;
+  if (nch > comm->llChannels) nch = comm->llChannels;
+  if (nch > comm->chanCap) nch = comm->chanCap;
+  uint64_t part = (npk + nch - 1) / nch;
+  if (part * 16 > comm->llBytes) return false;
+  const int n = comm->nRanks;
+  const uint64_t epp = 16 / ts;
+  uint64_t blockElems = (info.count + n - 1) / n;
+  blockElems = (blockElems + epp - 1) / epp * epp;
+  op->send = info.sendbuff;
+  op->recv = info.recvbuff;
+  op->count = info.count;
+  op->chunk = blockElems ? blockElems : epp;
+  op->part = part;
+  op->nch = nch;
+  op->pad = 0;
+  return true;
+}
+
+// Group aggregation: consecutive small AllReduce ops of one comm with the same stream, type and
+// operator become ONE LL launch (reference: a group's ops aggregated into one kernel plan,
+// enqueue.cc:405-470). ops[0..k) all passed llPlan; the caller forks/joins shared-GPU comms.
+ncclResult_t launchLLBatch(const std::vector<CollInfo>& ops) {
+  const CollInfo& f = ops[0];
+  ncclComm* comm = f.comm;
+  HIPCHECK(hipSetDevice(comm->device));
+  LaunchPlan p;
+  memset(&p, 0, sizeof(p));
+  p.func = FUNC_ALLREDUCE;
+  p.algo = ALGO_LL;
+  p.datatype = f.datatype;
+  p.eltSize = typeSize(f.datatype);
+  p.stream = comm->sharedDevInProcess ? comm->internalStream : f.stream;
+  const void* argPtr = nullptr;
+  NCCLCHECK(hostToDevRedOp(comm, f.op, f.datatype, &p.devOp, &p.ll.redArg, &argPtr));
+  p.ll.redArgPtr = argPtr;
+  p.ll.comm = comm->devComm;
+  p.ll.nOps = (int)ops.size();
+  for (size_t k = 0; k < ops.size(); k++) {
+    if (!llPlan(ops[k], &p.ll.ops[k])) return ncclInternalError;
+    if (p.ll.ops[k].nch > p.nChannels) p.nChannels = p.ll.ops[k].nch;
+    comm->opCount++;
+  }
+  TRACE("LL batch: %d AllReduce ops, %d channels", p.ll.nOps, p.nChannels);
+  return launchPlan(p);
+}
+
+// Can `b` join the LL batch that `a` opened?
+bool llBatchable(const CollInfo& a, const CollInfo& b) {
+  return a.comm == b.comm && a.stream == b.stream && a.datatype == b.datatype && a.op == b.op &&
+         b.func == FUNC_ALLREDUCE && !paramInt("NCCL_AMD_NO_AGGREGATION", 0);
+}
+
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   ncclComm* comm = info.comm;
   HIPCHECK(hipSetDevice(comm->device));
@@ -217,48 +302,17 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     if (algo && (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE"))) oneShot = false;
   }
   const bool oneShotAR = oneShot;
-  // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): tiny AllReduce, 8-byte aligned buffers, fits the
-  // comm's line area (llChannels x llBytes/16 payloads of 8 bytes). NCCL_PROTO may force or exclude it.
-  if (info.func == FUNC_ALLREDUCE) {
-    size_t bytes = count * (size_t)ts;
-    size_t npk = (bytes + 7) / 8;
-    size_t cap = (size_t)comm->llChannels * (comm->llBytes / 16);
-    bool llOn = true, simpleOn = true;
-    if (const char* proto = paramStr("NCCL_PROTO")) {  // reference syntax: "LL,Simple" or "^LL128"
-      bool exclude = proto[0] == '^';
-      bool hasLL = false, hasSimple = false;
-      std::string list(proto + (exclude ? 1 : 0));
-      size_t pos = 0;
-      while (pos <= list.size()) {
-        size_t comma = list.find(',', pos);
-        std::string tok = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
-        hasLL |= !strcasecmp(tok.c_str(), "LL");
-        hasSimple |= !strcasecmp(tok.c_str(), "Simple");
-        if (comma == std::string::npos) break;
-        pos = comma + 1;
-      }
-      llOn = exclude ? !hasLL : hasLL;
-      simpleOn = exclude ? !hasSimple : hasSimple;
-    }
-    // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
-    // NCCL_PROTO leaves only LL enabled
-    bool useLL = llOn && (!simpleOn || (!paramStr("NCCL_ALGO") && bytes <= (size_t)paramInt("NCCL_AMD_LL_BYTES", 128 << 10)));
-    const bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
-    if (useLL && al8 && npk <= cap) {
-      const uint64_t perCh = (uint64_t)paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096) / 8;
-      int nch = (int)((npk + perCh - 1) / perCh);
-      if (nch < 1) nch = 1;
-      if (nch > comm->llChannels) nch = comm->llChannels;
-      if (nch > comm->chanCap) nch = comm->chanCap;
-      uint64_t part = (npk + nch - 1) / nch;
-      if (part * 16 <= comm->llBytes) {
-        p.algo = ALGO_LL;
-        p.nChannels = nch;
-        p.args.part = part;
-        TRACE("%s: LL count %zu nch %d part %lu payloads", info.opName, count, nch, (unsigned long)part);
-        goto launch;
-      }
-    }
+  // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce, one launch, no fences
+  if (info.func == FUNC_ALLREDUCE && llPlan(info, &p.ll.ops[0])) {
+    p.algo = ALGO_LL;
+    p.ll.comm = comm->devComm;
+    p.ll.redArg = p.args.redArg;
+    p.ll.redArgPtr = p.args.redArgPtr;
+    p.ll.nOps = 1;
+    p.nChannels = p.ll.ops[0].nch;
+    TRACE("%s: LL count %zu nch %d part %lu payloads", info.opName, count, p.nChannels,
+          (unsigned long)p.ll.ops[0].part);
+    goto launch;
   }
   // Symmetric windows (reference: symmetric kernels for buffers in NCCL_WIN_COLL_SYMMETRIC windows,
   // src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*): zero-copy pull kernels.

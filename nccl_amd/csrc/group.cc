@@ -8,6 +8,7 @@
 // never block on peers (all connections are made at init), so one thread may drive every device of
 // the node even without a group — the group is still honoured for ordering and error reporting.
 #include <functional>
+#include <map>
 #include <thread>
 #include <vector>
 
@@ -73,7 +74,34 @@ ncclResult_t groupEndInternal() {
   (void)hipGetDevice(&dev);
   ncclResult_t r = ncclSuccess;
   for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = collFork(colls[i]);
-  for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = launchColl(colls[i], false);
+  // launches in group order per comm; runs of small AllReduce ops (same comm/stream/type/op) that all
+  // take the LL protocol become one launch. Every rank of a comm issues the same op sequence, so every
+  // rank forms the same batches.
+  std::map<ncclComm*, std::vector<CollInfo>> open;
+  auto flush = [&](ncclComm* c) -> ncclResult_t {
+    std::vector<CollInfo>& run = open[c];
+    ncclResult_t res = ncclSuccess;
+    if (run.size() == 1) res = launchColl(run[0], false);
+    else if (run.size() > 1) res = launchLLBatch(run);
+    run.clear();
+    return res;
+  };
+  LLOp probe;
+  for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) {
+    const CollInfo& c = colls[i];
+    std::vector<CollInfo>& run = open[c.comm];
+    const bool ll = c.func == FUNC_ALLREDUCE && llPlan(c, &probe);
+    if (ll && !run.empty() && llBatchable(run[0], c) && run.size() < (size_t)kMaxLLBatch) {
+      run.push_back(c);
+      continue;
+    }
+    r = flush(c.comm);
+    if (r != ncclSuccess) break;
+    if (ll) run.push_back(c);
+    else r = launchColl(c, false);
+  }
+  for (auto& kv : open)
+    if (r == ncclSuccess) r = flush(kv.first);
   for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = collJoin(colls[i]);
   (void)hipSetDevice(dev);
   return r;

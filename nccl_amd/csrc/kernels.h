@@ -571,27 +571,17 @@ __device__ __forceinline__ uint64_t loadLL(const uint64_t* p) {
 }
 
 template <typename T, int OP>
-__global__ void __launch_bounds__(kThreads) llKernel(CollArgs a) {
-  __shared__ int abortSh;
-  const DevComm& dc = *a.comm;
-  const int tid = threadIdx.x, c = blockIdx.x, me = dc.rank, n = dc.nRanks;
+__device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>& fn, const LLOp& op, int c,
+                                            uint64_t e64, int& abortSh) {
+  const int tid = threadIdx.x, me = dc.rank, n = dc.nRanks;
   constexpr int EPP = 8 / sizeof(T);  // elements per 8-byte payload
-  if (tid == 0) abortSh = 0;
-  uint64_t opArg = a.redArg;
-  if (a.redArgPtr) {
-    opArg = 0;
-    __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
-  }
-  const Red<T, OP> fn(opArg);
-  const uint64_t e64 = dc.counters[ctrIndex(c, CTR_LL, 0)] + 1;
   const uint32_t flag = (uint32_t)e64 ? (uint32_t)e64 : 1u;  // never 0 (the area starts zeroed)
   const int par = (int)(e64 & 1);
-  __syncthreads();
-  const uint64_t nbytes = a.count * sizeof(T);
+  const uint64_t nbytes = op.count * sizeof(T);
   const uint64_t npk = (nbytes + 7) / 8;
-  const uint64_t lo = min((uint64_t)c * a.part, npk), hi = min(lo + a.part, npk);
-  const char* send = (const char*)a.sendbuff;
-  char* recv = (char*)a.recvbuff;
+  const uint64_t lo = min((uint64_t)c * op.part, npk), hi = min(lo + op.part, npk);
+  const char* send = (const char*)op.send;
+  char* recv = (char*)op.recv;
 
   // send: my payload of [lo,hi) to every peer, 16-byte lines (two 8-byte payloads per line)
   for (uint64_t i = lo + 2 * tid; i < hi; i += 2 * kThreads) {
@@ -604,7 +594,7 @@ __global__ void __launch_bounds__(kThreads) llKernel(CollArgs a) {
     }
     u32x4 line = {(uint32_t)v[0], flag, (uint32_t)(v[0] >> 32), flag};
     u32x4 line2 = {(uint32_t)v[1], flag, (uint32_t)(v[1] >> 32), flag};
-    const uint64_t off = (i - lo) * 16;  // two payloads = two 16-byte lines
+    const uint64_t off = (i - lo) * 16;  // payload pk's line sits at (pk - lo) * 16
     for (int k = 1; k < n; k++) {
       int p = (me + k) % n;
       char* base = (char*)dc.flags[p] + llLineOffset(dc, c, par, me) + off;
@@ -616,9 +606,10 @@ __global__ void __launch_bounds__(kThreads) llKernel(CollArgs a) {
   // sent, so an in-place output cannot overwrite a payload another thread still has to send)
   __syncthreads();
   const uint64_t t0 = clockTicks();
+  bool ok = true;
   for (uint64_t pk = lo + tid; pk < hi; pk += kThreads) {
     const uint64_t firstElt = pk * 8 / sizeof(T);
-    const int owner = (int)(firstElt / a.chunk);  // 8-byte payloads never straddle rank blocks
+    const int owner = (int)(firstElt / op.chunk);  // 8-byte payloads never straddle rank blocks
     // pass 1: wait until every peer's line for this payload carries this epoch's flag
     uint32_t pending = 0;
     for (int q = 0; q < n; q++)
@@ -644,7 +635,10 @@ __global__ void __launch_bounds__(kThreads) llKernel(CollArgs a) {
         if (abortSh) break;
       }
     }
-    if (pending) break;
+    if (pending) {
+      ok = false;
+      break;
+    }
     // pass 2: fold in the owner block's ring order (the lines stay valid until epoch + 2)
     union { uint64_t u; T e[EPP]; } acc, x;
     for (int k = 0; k < n; k++) {
@@ -668,8 +662,32 @@ __global__ void __launch_bounds__(kThreads) llKernel(CollArgs a) {
     if (pk * 8 + 8 <= nbytes) *(uint64_t*)(recv + pk * 8) = acc.u;
     else for (uint64_t b = pk * 8; b < nbytes; b++) recv[b] = (char)(acc.u >> (8 * (b - pk * 8)));
   }
+  __syncthreads();  // every payload of this op is folded before the next op's lines go out
+  return ok && !abortSh;
+}
+
+// One launch runs a batch of LL AllReduce ops in order; a channel takes part in op k if c < nch_k, and
+// its epoch advances once per op it takes part in (all ranks run the same batch, so epochs agree).
+template <typename T, int OP>
+__global__ void __launch_bounds__(kThreads) llKernel(LLBatchArgs a) {
+  __shared__ int abortSh;
+  const DevComm& dc = *a.comm;
+  const int c = blockIdx.x;
+  if (threadIdx.x == 0) abortSh = 0;
+  uint64_t opArg = a.redArg;
+  if (a.redArgPtr) {
+    opArg = 0;
+    __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
+  }
+  const Red<T, OP> fn(opArg);
+  uint64_t e64 = dc.counters[ctrIndex(c, CTR_LL, 0)];
   __syncthreads();
-  if (tid == 0) dc.counters[ctrIndex(c, CTR_LL, 0)] = e64;
+  for (int k = 0; k < a.nOps; k++) {
+    if (c >= a.ops[k].nch) continue;
+    e64++;
+    if (!llChannelOp<T, OP>(dc, fn, a.ops[k], c, e64, abortSh)) break;
+  }
+  if (threadIdx.x == 0) dc.counters[ctrIndex(c, CTR_LL, 0)] = e64;
 }
 
 // ------------------------------------------------------------------------------------ symmetric windows
@@ -862,7 +880,7 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
   switch (p.func) {
     case FUNC_ALLREDUCE:
       if (p.algo == ALGO_LL)
-        hipLaunchKernelGGL((llKernel<T, OP>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+        hipLaunchKernelGGL((llKernel<T, OP>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.ll);
       else if (p.algo == ALGO_ONESHOT)
         hipLaunchKernelGGL((collKernel<T, OP, COLL_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       else

@@ -204,3 +204,48 @@ def test_abort_unblocks_stuck_collective(built):
     comms[0].abort()  # sets the abort word, waits for the kernel to notice
     assert time.time() - t0 < 20
     comms[1].destroy()
+
+
+@pytest.mark.parametrize("dtype,op", [(7, 0), (9, 0), (2, 3), (6, 4)])
+def test_group_aggregates_small_allreduces(two_comms, dtype, op):
+    """A group of many small AllReduce ops (one LL launch per run, group.cc) interleaved with a
+    ReduceScatter that breaks the run; every result bit-exact vs the oracle."""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    comms, streams = two_comms
+    n = 2
+    counts = [1, 3, 100, 4096, 777, 20_000, 8, 12_345] * 5  # 40 ops: more than one 32-op batch
+    rs_count = 4096 * n
+    ins = [G.make_inputs(n, dtype, cnt, seed=300 + i) for i, cnt in enumerate(counts)]
+    rs_in = G.make_inputs(n, dtype, rs_count, seed=999)
+    bufs = []
+    for r in range(n):
+        per = []
+        for i, cnt in enumerate(counts):
+            _, sv = G.to_device(ins[i][r], "cuda")
+            _, rv = G.to_device(np.zeros(cnt, dtype=ins[i][r].dtype), "cuda")
+            per.append((sv, rv))
+        _, rss = G.to_device(rs_in[r], "cuda")
+        _, rsr = G.to_device(np.zeros(rs_count // n, dtype=rs_in[r].dtype), "cuda")
+        bufs.append((per, rss, rsr))
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for r in range(n):
+            per, rss, rsr = bufs[r]
+            s = streams[r].cuda_stream
+            for i, cnt in enumerate(counts):
+                if i == 20:
+                    comms[r].reduce_scatter_raw(rss.data_ptr(), rsr.data_ptr(), rs_count // n, dtype, op, s)
+                comms[r].all_reduce_raw(per[i][0].data_ptr(), per[i][1].data_ptr(), cnt, dtype, op, s)
+    torch.cuda.synchronize()
+    assert all(c.async_error() == 0 for c in comms)
+    npdt = ins[0][0].dtype
+    for i, cnt in enumerate(counts):
+        want = G.expected("allreduce", ins[i], dtype, op)[0]
+        for r in range(n):
+            got = G.from_device(bufs[r][0][i][1], npdt)
+            assert G.same_bits(got, want, dtype), f"op {i} (count {cnt}) rank {r}"
+    want_rs = G.expected("reducescatter", rs_in, dtype, op)
+    for r in range(n):
+        assert G.same_bits(G.from_device(bufs[r][2], npdt), want_rs[r], dtype)
