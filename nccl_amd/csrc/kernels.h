@@ -305,6 +305,10 @@ struct Channel {
     return a.chunk;
   }
   __device__ uint64_t& ctr(int k, int r) const { return sh.st.ctr[k][r]; }
+  // k-th peer (k = 1..n-1) this channel sends to. Staggered by channel: every channel starting with the
+  // same peer would put all of a rank's scatter traffic on ONE xGMI link at a time; rotating the start
+  // spreads the channels evenly over the n-1 links (data placement and fold order are unaffected).
+  __device__ int peerAt(int k) const { return (me + 1 + (k - 1 + c) % (n - 1)) % n; }
   __device__ const uint64_t* myFlags(int kind) const { return dc.flags[me] + flagIndex(c, kind, 0); }
   __device__ bool pushesTo(int p) const {
     if (COLL == COLL_AR || COLL == COLL_AG) return true;
@@ -321,7 +325,7 @@ struct Channel {
     __syncthreads();
     if (!waitAll(dc, sh.st, myFlags(FLG_RS_ACK), sh.want, forceAcq)) return false;
     for (int k = 1; k < n; k++) {
-      int p = (me + k) % n;
+      int p = peerAt(k);
       uint64_t lo, hi;
       sliceRange(a, c, step, blockLen(p), lo, hi);
       int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
@@ -423,7 +427,7 @@ struct Channel {
     sliceRange(a, c, step, a.count, lo, hi);
     const char* src = (const char*)a.sendbuff + lo * ts;
     for (int k = 1; k < n; k++) {
-      int p = (me + k) % n;
+      int p = peerAt(k);
       int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
       copyRange<T, true>(dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me), src, (hi - lo) * ts, aligned);
     }
@@ -796,7 +800,7 @@ __global__ void __launch_bounds__(kThreads) symKernel(SymArgs a) {
   if (ok && (COLL == SYM_AR || COLL == SYM_AG)) {
     // AG: pull every other rank's block part (AR: its reduced output; AG: its input)
     for (int k = 1; k < n; k++) {
-      const int q = (me + n - k) % n;
+      const int q = (me + n - 1 - (k - 1 + c) % (n - 1)) % n;  // staggered by channel: all links busy
       uint64_t lo, hi;
       partOf(blockLen(q), lo, hi);
       const char* src = COLL == SYM_AR ? a.recv[q] + ((uint64_t)q * a.chunk + lo) * ts : a.send[q] + lo * ts;
