@@ -147,39 +147,58 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dic
                          "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(ok) else "FAIL"}
     del send, shard, full, base
 
-    # --- configs[3]: fp16 AllReduce sweep, one-shot vs direct ---
+    # --- configs[3]: fp16 AllReduce sweep: LL vs one-shot vs direct. Protocol/algorithm knobs are read at
+    #     communicator init (like the reference's NCCL_PARAMs), so each column gets its own communicator ---
     top = (16 if quick else 256) * MIB
     buf = torch.empty(top // 2, dtype=torch.float16, device="cuda").uniform_(-1, 1)
     res = torch.empty_like(buf)
-    sweep = []
-    size = 8
-    old = os.environ.get("NCCL_ALGO")
-    while size <= top:
-        c = size // 2
-        row = {"bytes": size}
-        for algo in ("LL", "ONESHOT", "DIRECT"):
-            if algo == "ONESHOT" and size > 64 * MIB:
-                continue
-            if algo == "LL":
-                if size > 256 * 1024:  # the LL line area holds 256 KiB of payload
-                    continue
-                os.environ.pop("NCCL_ALGO", None)
-                os.environ["NCCL_PROTO"] = "LL"
-            else:
-                os.environ.pop("NCCL_PROTO", None)
-                os.environ["NCCL_ALGO"] = algo
-            it = 50 if size <= 4 * MIB else 10
-            ms = tmax(_time_ms(lambda: comm.all_reduce_raw(buf.data_ptr(), res.data_ptr(), c, 6, 0, sp), stream, it))
-            row[algo.lower() + "_us"] = round(ms * 1e3, 2)
-            row[algo.lower() + "_busbw_GBps"] = round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)
-        sweep.append(row)
-        size *= 2
-    os.environ.pop("NCCL_PROTO", None)
-    if old is None:
-        os.environ.pop("NCCL_ALGO", None)
-    else:
-        os.environ["NCCL_ALGO"] = old
-    out["ar_fp16_sweep"] = sweep
+    cols = {"ll": {"NCCL_PROTO": "LL"}, "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
+            "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"}, "default": {}}
+    limits = {"ll": 512 * 1024, "oneshot": 64 * MIB}
+    rows = {}
+    saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION")}
+    for name, env in cols.items():
+        for k in saved:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+        size = 8
+        while size <= top:
+            if size <= limits.get(name, top):
+                c = size // 2
+                it = 50 if size <= 4 * MIB else 10
+                ms = tmax(_time_ms(lambda: cm.all_reduce_raw(buf.data_ptr(), res.data_ptr(), c, 6, 0, sp), stream, it))
+                row = rows.setdefault(size, {"bytes": size})
+                row[name + "_us"] = round(ms * 1e3, 2)
+                row[name + "_busbw_GBps"] = round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)
+            size *= 2
+        torch.cuda.synchronize()
+        cm.destroy()
+    out["ar_fp16_sweep"] = [rows[k] for k in sorted(rows)]
+
+    # --- group aggregation: 32 small AllReduce ops in one ncclGroupStart/End,
+    #     one LL launch vs one launch per op ---
+    agg = {}
+    for name, env in (("aggregated", {}), ("one_launch_per_op", {"NCCL_AMD_NO_AGGREGATION": "1"})):
+        for k in saved:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+
+        def grouped():
+            with nccl_amd.group():
+                for k in range(32):
+                    cm.all_reduce_raw(buf.data_ptr() + k * 8192, res.data_ptr() + k * 8192, 2048, 6, 0, sp)
+        ms = tmax(_time_ms(grouped, stream, 20))
+        agg[name + "_us_per_group"] = round(ms * 1e3, 2)
+        torch.cuda.synchronize()
+        cm.destroy()
+    agg["config"] = "32 x ncclAllReduce fp16 4 KiB in one group"
+    out["group_aggregation"] = agg
+    for k, v in saved.items():
+        os.environ.pop(k, None)
+        if v is not None:
+            os.environ[k] = v
     del buf, res
 
     # --- configs[4]: Reduce int32 min / max, 128 MiB, root 0 ---

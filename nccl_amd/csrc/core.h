@@ -117,6 +117,25 @@ struct IpcMapping {
   int refs;
 };
 
+// Hot-path tuning knobs, read ONCE at communicator init (reference NCCL_PARAM caches its env reads,
+// include/param.h:21-31) and agreed across ranks (rank 0's values win), so every rank takes the same
+// algorithm/protocol decision and no getenv() runs per collective.
+struct CommTuning {
+  int checkPointers;        // NCCL_CHECK_POINTERS
+  int forceElementwise;     // NCCL_AMD_FORCE_ELEMENTWISE (diagnostics)
+  int protoFlags;           // NCCL_AMD_PROTO_FLAGS | (NCCL_AMD_P2P_FENCE=0 ? 8 : 0)
+  int algo;                 // NCCL_ALGO: 0 unset, 1 ONESHOT, 2 DIRECT (RING / TREE)
+  int llOn, simpleOn;       // NCCL_PROTO
+  int symDisable;           // NCCL_AMD_SYM_DISABLE
+  int noAggregation;        // NCCL_AMD_NO_AGGREGATION
+  int64_t oneShotBytes;     // NCCL_AMD_ONESHOT_BYTES
+  int64_t llBytes;          // NCCL_AMD_LL_BYTES
+  int64_t llChannelBytes;   // NCCL_AMD_LL_CHANNEL_BYTES
+  int64_t minChannelBytes;  // NCCL_AMD_MIN_CHANNEL_BYTES
+  int64_t oneShotChannelBytes;  // NCCL_AMD_ONESHOT_CHANNEL_BYTES
+};
+void loadTuning(CommTuning* t);  // enqueue.cc
+
 struct ncclCommImpl;
 }  // namespace ncclamd
 
@@ -155,6 +174,7 @@ struct ncclComm {
   size_t slotBytes = 0;
   int nSlots = 0;
   int maxChannels = 0;
+  ncclamd::CommTuning tune;
   int llChannels = 32;      // LL protocol: channels and line bytes per (channel, parity, sender)
   size_t llBytes = 32 << 10;
   int chanCap = 0;  // channels per launch that stay co-resident even with several ranks per GPU

@@ -90,7 +90,7 @@ struct LLOp {
   uint64_t chunk;  // elements per rank block (fold order of each element's owner)
   uint64_t part;   // 8-byte payloads per channel
   int nch;         // channels this op uses
-  int pad;
+  int chOff;       // first channel (batches spread their ops over the LL channels)
 };
 struct LLBatchArgs {
   const DevComm* comm;

@@ -74,6 +74,47 @@ static ncclResult_t hostToDevRedOp(ncclComm* comm, ncclRedOp_t op, ncclDataType_
   }
 }
 
+void loadTuning(CommTuning* t) {
+  memset(t, 0, sizeof(*t));
+  t->checkPointers = (int)paramInt("NCCL_CHECK_POINTERS", 0);
+  t->forceElementwise = (int)paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0);
+  t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 1) ? 0 : 8);
+  if (const char* algo = paramStr("NCCL_ALGO")) {
+    if (!strcasecmp(algo, "ONESHOT")) t->algo = 1;
+    else if (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE")) t->algo = 2;
+    else WARN("NCCL_ALGO=%s: unknown here (ONESHOT, DIRECT, RING, TREE); using the size table", algo);
+  }
+  t->llOn = t->simpleOn = 1;
+  if (const char* proto = paramStr("NCCL_PROTO")) {  // reference syntax: "LL,Simple" or "^LL128"
+    bool exclude = proto[0] == '^';
+    bool hasLL = false, hasSimple = false;
+    std::string list(proto + (exclude ? 1 : 0));
+    size_t pos = 0;
+    while (true) {
+      size_t comma = list.find(',', pos);
+      std::string tok = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
+      hasLL |= !strcasecmp(tok.c_str(), "LL");
+      hasSimple |= !strcasecmp(tok.c_str(), "Simple");
+      if (comma == std::string::npos) break;
+      pos = comma + 1;
+    }
+    t->llOn = exclude ? !hasLL : hasLL;
+    t->simpleOn = exclude ? !hasSimple : hasSimple;
+    if (!t->llOn && !t->simpleOn) {
+      WARN("NCCL_PROTO=%s leaves no protocol enabled; using Simple", proto);
+      t->simpleOn = 1;
+    }
+  }
+  t->symDisable = (int)paramInt("NCCL_AMD_SYM_DISABLE", 0);
+  t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
+  t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks)
+  t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 128 << 10);
+  t->llChannelBytes = paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096);
+  if (t->llChannelBytes < 8) t->llChannelBytes = 8;
+  t->minChannelBytes = paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
+  t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
+}
+
 // Pointer check (reference argcheck.cc:12-28), active with NCCL_CHECK_POINTERS=1.
 static ncclResult_t ptrCheck(const void* p, ncclComm* comm, const char* name, const char* opname) {
   hipPointerAttribute_t attr;
@@ -110,7 +151,7 @@ static ncclResult_t argsCheck(CollInfo* info) {
     WARN("%s : reduction operation %d unknown to this communicator", info->opName, info->op);
     return ncclInvalidArgument;
   }
-  if (paramInt("NCCL_CHECK_POINTERS", 0) && info->count > 0) {
+  if (comm->tune.checkPointers && info->count > 0) {
     NCCLCHECK(ptrCheck(info->sendbuff, comm, "sendbuff", info->opName));
     if (info->func != FUNC_REDUCE || comm->rank == info->root)
       NCCLCHECK(ptrCheck(info->recvbuff, comm, "recvbuff", info->opName));
@@ -152,29 +193,13 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   const int ts = typeSize(info.datatype);
   const size_t bytes = info.count * (size_t)ts;
   const size_t npk = (bytes + 7) / 8;
-  bool llOn = true, simpleOn = true;
-  if (const char* proto = paramStr("NCCL_PROTO")) {  // reference syntax: "LL,Simple" or "^LL128"
-    bool exclude = proto[0] == '^';
-    bool hasLL = false, hasSimple = false;
-    std::string list(proto + (exclude ? 1 : 0));
-    size_t pos = 0;
-    while (true) {
-      size_t comma = list.find(',', pos);
-      std::string tok = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
-      hasLL |= !strcasecmp(tok.c_str(), "LL");
-      hasSimple |= !strcasecmp(tok.c_str(), "Simple");
-      if (comma == std::string::npos) break;
-      pos = comma + 1;
-    }
-    llOn = exclude ? !hasLL : hasLL;
-    simpleOn = exclude ? !hasSimple : hasSimple;
-  }
+  const CommTuning& t = comm->tune;
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
   // NCCL_PROTO leaves only LL enabled
-  bool useLL = llOn && (!simpleOn || (!paramStr("NCCL_ALGO") && bytes <= (size_t)paramInt("NCCL_AMD_LL_BYTES", 128 << 10)));
+  bool useLL = t.llOn && (!t.simpleOn || (t.algo == 0 && bytes <= (size_t)t.llBytes));
   const bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
   if (!useLL || !al8 || npk > (size_t)comm->llChannels * (comm->llBytes / 16)) return false;
-  const uint64_t perCh = (uint64_t)paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096) / 8;
+  const uint64_t perCh = (uint64_t)t.llChannelBytes / 8;
   int nch = (int)((npk + perCh - 1) / perCh);
   if (nch < 1) nch = 1;
   if (nch > comm->llChannels) nch = comm->llChannels;
@@ -191,7 +216,7 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   op->chunk = blockElems ? blockElems : epp;
   op->part = part;
   op->nch = nch;
-  op->pad = 0;
+  op->chOff = 0;
   return true;
 }
 
@@ -214,11 +239,15 @@ ncclResult_t launchLLBatch(const std::vector<CollInfo>& ops) {
   p.ll.redArgPtr = argPtr;
   p.ll.comm = comm->devComm;
   p.ll.nOps = (int)ops.size();
+  int off = 0, used = 0;
   for (size_t k = 0; k < ops.size(); k++) {
     if (!llPlan(ops[k], &p.ll.ops[k])) return ncclInternalError;
-    if (p.ll.ops[k].nch > p.nChannels) p.nChannels = p.ll.ops[k].nch;
+    p.ll.ops[k].chOff = off;
+    off = (off + p.ll.ops[k].nch) % comm->llChannels;
+    used += p.ll.ops[k].nch;
     comm->opCount++;
   }
+  p.nChannels = used < comm->llChannels ? used : comm->llChannels;
   TRACE("LL batch: %d AllReduce ops, %d channels", p.ll.nOps, p.nChannels);
   return launchPlan(p);
 }
@@ -226,7 +255,7 @@ ncclResult_t launchLLBatch(const std::vector<CollInfo>& ops) {
 // Can `b` join the LL batch that `a` opened?
 bool llBatchable(const CollInfo& a, const CollInfo& b) {
   return a.comm == b.comm && a.stream == b.stream && a.datatype == b.datatype && a.op == b.op &&
-         b.func == FUNC_ALLREDUCE && !paramInt("NCCL_AMD_NO_AGGREGATION", 0);
+         b.func == FUNC_ALLREDUCE && !a.comm->tune.noAggregation;
 }
 
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
@@ -285,21 +314,21 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   uintptr_t bases = (uintptr_t)info.sendbuff | (uintptr_t)info.recvbuff;
   bool aligned = (bases & 15) == 0;
   if (info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER) aligned = aligned && ((count * ts) & 15) == 0;
-  if (paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0)) aligned = false;  // diagnostics: T-sized accesses only
+  if (comm->tune.forceElementwise) aligned = false;  // diagnostics: T-sized accesses only
   p.args.aligned = aligned ? 1 : 0;
   // NCCL_AMD_P2P_FENCE=0 drops the system release fence before data flags (all published bytes are
   // already stored write-through at system scope and drained). Default: keep it.
-  p.args.protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 1) ? 0 : 8);
+  p.args.protoFlags = comm->tune.protoFlags;
   // Algorithm choice (reference: NCCL_ALGO / tuning.cc cost model): one-shot for small AllReduce
   // (latency: one handshake), direct scatter-reduce-gather otherwise (bandwidth). NCCL_ALGO may force
   // either: ONESHOT or DIRECT (the reference's RING/TREE names map to DIRECT).
   bool oneShot = false;
   if (info.func == FUNC_ALLREDUCE) {
-    const char* algo = paramStr("NCCL_ALGO");
+    // one-shot moves (n-1)S link bytes per rank vs 2(n-1)S/n for the direct path, but saves two
+    // handshakes: the crossover shrinks with n (default 2 MiB / n: 1 MiB at n=2, 256 KiB at n=8)
     size_t bytes = count * (size_t)ts;
-    oneShot = bytes <= (size_t)paramInt("NCCL_AMD_ONESHOT_BYTES", 256 << 10);
-    if (algo && !strcasecmp(algo, "ONESHOT")) oneShot = true;
-    if (algo && (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE"))) oneShot = false;
+    size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes : ((size_t)2 << 20) / n;
+    oneShot = comm->tune.algo == 1 || (comm->tune.algo == 0 && bytes <= lim);
   }
   const bool oneShotAR = oneShot;
   // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce, one launch, no fences
@@ -316,7 +345,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   }
   // Symmetric windows (reference: symmetric kernels for buffers in NCCL_WIN_COLL_SYMMETRIC windows,
   // src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*): zero-copy pull kernels.
-  if (info.func != FUNC_REDUCE && !paramInt("NCCL_AMD_SYM_DISABLE", 0)) {
+  if (info.func != FUNC_REDUCE && !comm->tune.symDisable) {
     size_t sb = count * ts, rb = count * ts;
     if (info.func == FUNC_REDUCESCATTER) sb *= n;
     if (info.func == FUNC_ALLGATHER) rb *= n;
@@ -343,11 +372,11 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
         if (agInPlace) sp.args.send[r] = sp.args.recv[r] + (size_t)r * count * ts;
         al |= (uintptr_t)sp.args.send[r] | (uintptr_t)sp.args.recv[r];
       }
-      bool symAligned = (al & 15) == 0 && !paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0);
+      bool symAligned = (al & 15) == 0 && !comm->tune.forceElementwise;
       if (info.func != FUNC_ALLREDUCE) symAligned = symAligned && ((count * ts) & 15) == 0;
       sp.args.aligned = symAligned ? 1 : 0;
       size_t spanBytes = blockElems * ts;  // what one channel plan divides
-      size_t minPart = (size_t)paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
+      size_t minPart = (size_t)comm->tune.minChannelBytes;
       int maxCh = comm->chanCap;
       if (info.func == FUNC_ALLREDUCE) {
         // one-shot needs out-of-place buffers: in place, peers would still read what this rank overwrites
@@ -355,7 +384,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
         sp.coll = (oneShotAR && out) ? 1 /*SYM_AR1*/ : 0 /*SYM_AR*/;
         if (sp.coll == 1) {
           spanBytes = count * ts;
-          minPart = (size_t)paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
+          minPart = (size_t)comm->tune.oneShotChannelBytes;
           maxCh = maxCh < 32 ? maxCh : 32;
         }
       } else {
@@ -384,9 +413,9 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   }
   if (oneShot) {
     p.algo = ALGO_ONESHOT;
-    planChannels(comm, count * ts, ts, p, (size_t)paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10), 32);
+    planChannels(comm, count * ts, ts, p, (size_t)comm->tune.oneShotChannelBytes, 32);
   } else {
-    planChannels(comm, blockElems * ts, ts, p, (size_t)paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10),
+    planChannels(comm, blockElems * ts, ts, p, (size_t)comm->tune.minChannelBytes,
                  comm->chanCap);
   }
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,

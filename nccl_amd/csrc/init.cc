@@ -63,6 +63,7 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   if (c->minCTAs < 1) c->minCTAs = 1;
   if (c->minCTAs > c->maxCTAs) c->minCTAs = c->maxCTAs;
   c->maxChannels = c->maxCTAs;
+  loadTuning(&c->tune);
   c->nSlots = (int)paramInt("NCCL_AMD_NSLOTS", 2);
   if (c->nSlots < 1) c->nSlots = 1;
   // Slot size: the staging slab (maxChannels x 2 kinds x nSlots x nRanks x slot) is sized to a fixed
@@ -133,6 +134,7 @@ static void computeChannelCap(ncclComm* c) {
 struct ShapeInfo {
   int maxChannels, nSlots;
   uint64_t slotBytes;
+  CommTuning tune;
 };
 
 static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id, int rank, int dev,
@@ -149,11 +151,12 @@ static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id,
   // Agree on the channel/slot shape: rank 0's parameters win (env may differ per process).
   {
     std::vector<ShapeInfo> shapes(nranks);
-    shapes[rank] = {comm->maxChannels, comm->nSlots, comm->slotBytes};
+    shapes[rank] = {comm->maxChannels, comm->nSlots, comm->slotBytes, comm->tune};
     if ((res = bootstrapAllGather(comm->bootstrap, shapes.data(), sizeof(ShapeInfo))) != ncclSuccess) goto fail;
     comm->maxChannels = comm->maxCTAs = shapes[0].maxChannels;
     comm->nSlots = shapes[0].nSlots;
     comm->slotBytes = shapes[0].slotBytes;
+    comm->tune = shapes[0].tune;
     if (comm->minCTAs > comm->maxCTAs) comm->minCTAs = comm->maxCTAs;
   }
   if ((res = transportSetup(comm)) != ncclSuccess) goto fail;

@@ -575,15 +575,16 @@ __device__ __forceinline__ uint64_t loadLL(const uint64_t* p) {
 }
 
 template <typename T, int OP>
-__device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>& fn, const LLOp& op, int c,
+__device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>& fn, const LLOp& op, int c, int j,
                                             uint64_t e64, int& abortSh) {
+  // c: physical channel (line area + epoch); j: this op's part index on it
   const int tid = threadIdx.x, me = dc.rank, n = dc.nRanks;
   constexpr int EPP = 8 / sizeof(T);  // elements per 8-byte payload
   const uint32_t flag = (uint32_t)e64 ? (uint32_t)e64 : 1u;  // never 0 (the area starts zeroed)
   const int par = (int)(e64 & 1);
   const uint64_t nbytes = op.count * sizeof(T);
   const uint64_t npk = (nbytes + 7) / 8;
-  const uint64_t lo = min((uint64_t)c * op.part, npk), hi = min(lo + op.part, npk);
+  const uint64_t lo = min((uint64_t)j * op.part, npk), hi = min(lo + op.part, npk);
   const char* send = (const char*)op.send;
   char* recv = (char*)op.recv;
 
@@ -670,8 +671,10 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
   return ok && !abortSh;
 }
 
-// One launch runs a batch of LL AllReduce ops in order; a channel takes part in op k if c < nch_k, and
-// its epoch advances once per op it takes part in (all ranks run the same batch, so epochs agree).
+// One launch runs a batch of LL AllReduce ops; op k occupies channels [chOff_k, chOff_k + nch_k) mod
+// llChannels, so the small ops of a batch land on different channels and run in parallel (one
+// round trip for the batch). A channel runs its ops in batch order and its epoch advances once per op
+// it takes part in; all ranks build the same batch, so epochs agree.
 template <typename T, int OP>
 __global__ void __launch_bounds__(kThreads) llKernel(LLBatchArgs a) {
   __shared__ int abortSh;
@@ -686,10 +689,12 @@ __global__ void __launch_bounds__(kThreads) llKernel(LLBatchArgs a) {
   const Red<T, OP> fn(opArg);
   uint64_t e64 = dc.counters[ctrIndex(c, CTR_LL, 0)];
   __syncthreads();
+  const int L = dc.llChannels;
   for (int k = 0; k < a.nOps; k++) {
-    if (c >= a.ops[k].nch) continue;
+    const int j = (c - a.ops[k].chOff + L) % L;  // op k runs on channels chOff, chOff+1, ... (mod L)
+    if (j >= a.ops[k].nch) continue;
     e64++;
-    if (!llChannelOp<T, OP>(dc, fn, a.ops[k], c, e64, abortSh)) break;
+    if (!llChannelOp<T, OP>(dc, fn, a.ops[k], c, j, e64, abortSh)) break;
   }
   if (threadIdx.x == 0) dc.counters[ctrIndex(c, CTR_LL, 0)] = e64;
 }

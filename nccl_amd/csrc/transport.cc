@@ -148,6 +148,13 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
   size_t cb = (size_t)comm->maxChannels * CTR_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
   HIPCHECK(hipMalloc((void**)&comm->counters, cb));
   HIPCHECK(hipMemset(comm->counters, 0, cb));
+  // Test knob (reference TEST_LL_CLEANUP, include/device.h:99-106, shrinks the LL flag space to exercise
+  // wraparound): start every channel's LL epoch at NCCL_AMD_LL_EPOCH_BASE, e.g. just below 2^32.
+  if (int64_t base = paramInt("NCCL_AMD_LL_EPOCH_BASE", 0)) {
+    std::vector<uint64_t> init(cb / sizeof(uint64_t), 0);
+    for (int c = 0; c < comm->maxChannels; c++) init[ctrIndex(c, CTR_LL, 0)] = (uint64_t)base;
+    HIPCHECK(hipMemcpy(comm->counters, init.data(), cb, hipMemcpyHostToDevice));
+  }
   HIPCHECK(hipHostMalloc((void**)&comm->hostAbort, 64, hipHostMallocMapped | hipHostMallocCoherent));
   HIPCHECK(hipHostMalloc((void**)&comm->hostError, 64, hipHostMallocMapped | hipHostMallocCoherent));
   memset(comm->hostAbort, 0, 64);

@@ -124,3 +124,84 @@ def test_multi_process(built, nranks, env):
         p.join(timeout=60)
     bad = [e for r in sorted(results) for e in results[r]]
     assert not bad, "\n".join(bad[:20])
+
+
+def test_reference_example_known_answer(built):
+    """docs/examples/03_collectives/01_allreduce/c/main.cc:99-168: 32 Mi floats per rank, sendbuff[i][0] = i
+    and zeros elsewhere, group of per-rank ncclAllReduce; element 0 must be n(n-1)/2 exactly (and the
+    rest zero) — here with 3 ranks on the one GPU, at the example's full size."""
+    torch = _torch()
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    n, size = 3, 32 * 1024 * 1024
+    comms = nccl_amd.Communicator.init_all([0] * n)
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    sends = [torch.zeros(size, device="cuda") for _ in range(n)]
+    recvs = [torch.full((size,), -1.0, device="cuda") for _ in range(n)]
+    for i in range(n):
+        sends[i][0] = i
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for c, s, x, y in zip(comms, streams, sends, recvs):
+            c.allreduce(x, y, nccl_amd.SUM, stream=s)
+    torch.cuda.synchronize()
+    for y in recvs:
+        assert float(y[0]) == n * (n - 1) / 2
+        assert int(torch.count_nonzero(y[1:])) == 0
+    for c in comms:
+        c.destroy()
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "float32"])
+def test_tolerance_vs_fp32_reference(built, dtype):
+    """contrib/nccl_ubx/tests/distributed/_workers/_run_ubx_op.py:65-128 convention: randn inputs
+    (seed 42+rank), reference = fp32 sum, bf16 atol 0.0625 / rtol 0.02, fp32 atol 1e-4 / rtol 1e-3."""
+    torch = _torch()
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    n, count = 4, 1 << 20
+    comms = nccl_amd.Communicator.init_all([0] * n)
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    dt = getattr(torch, dtype)
+    xs = []
+    for r in range(n):
+        g = torch.Generator(device="cuda")
+        g.manual_seed(42 + r)
+        xs.append(torch.randn(count, device="cuda", generator=g).to(dt))
+    ys = [torch.empty_like(x) for x in xs]
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for c, s, x, y in zip(comms, streams, xs, ys):
+            c.allreduce(x, y, nccl_amd.SUM, stream=s)
+    torch.cuda.synchronize()
+    ref = sum(x.float() for x in xs)
+    atol, rtol = (0.0625, 0.02) if dtype == "bfloat16" else (1e-4, 1e-3)
+    for y in ys:
+        torch.testing.assert_close(y.float(), ref, atol=atol, rtol=rtol)
+    for c in comms:
+        c.destroy()
+
+
+def test_ll_epoch_wraparound(built):
+    """LL flags are 32-bit epochs with parity double-buffering; start just below 2^32 (reference
+    TEST_LL_CLEANUP idea) and run many LL AllReduces across the wrap, checking each bit-exactly."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    os.environ["NCCL_AMD_LL_EPOCH_BASE"] = str(2**32 - 5)
+    try:
+        torch.cuda.set_device(0)
+        comms = nccl_amd.Communicator.init_all([0, 0])
+    finally:
+        os.environ.pop("NCCL_AMD_LL_EPOCH_BASE")
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    cs = list(zip(comms, streams))
+    errs = []
+    for i in range(12):
+        errs += G.run_case(cs, "allreduce", 7 if i % 2 else 9, 0, 1000 + 37 * i, 0, seed=500 + i)
+    for c in comms:
+        c.destroy()
+    assert not errs, errs
