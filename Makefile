@@ -14,13 +14,13 @@ SRCDIR   := nccl_amd/csrc
 COMMON   := -O3 -fPIC -std=c++17 -ffp-contract=off -fvisibility=hidden -Wall -Wno-unused-function \
             -Wno-unused-variable -Wno-unused-but-set-variable -Iinclude
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics
-HOSTSRC  := debug.cc bootstrap.cc transport.cc init.cc group.cc enqueue.cc register.cc
+HOSTSRC  := debug.cc bootstrap.cc transport.cc init.cc group.cc enqueue.cc register.cc tuner.cc
 HOSTOBJ  := $(HOSTSRC:%.cc=$(BUILD)/%.o)
 DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test
+all: lib oracle numerics-host bootstrap-test tuner-test
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -35,7 +35,7 @@ $(BUILD)/%.o: $(SRCDIR)/%.hip $(HDRS)
 $(LIBDIR)/libnccl.so: $(HOSTOBJ) $(DEVOBJ)
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-soname,libnccl.so.2 -Wl,-Bsymbolic \
-	  -o $@ $^ -lpthread
+	  -o $@ $^ -lpthread -ldl
 	ln -sf libnccl.so $(LIBDIR)/libnccl.so.2
 
 oracle: oracle/_build/liboracle.so
@@ -67,3 +67,11 @@ build/bootstrap_test: tests/native/bootstrap_test.cc $(SRCDIR)/bootstrap.cc $(SR
 	  $(SRCDIR)/bootstrap.cc $(SRCDIR)/debug.cc -lpthread
 
 .PHONY: bootstrap-test
+
+# test-only tuner plugin (reference ABI v6) loaded through NCCL_TUNER_PLUGIN by the GPU tests
+tuner-test: tests/native/libnccl-tuner-test.so
+
+tests/native/libnccl-tuner-test.so: tests/native/tuner_plugin.c include/nccl_tuner.h include/nccl.h
+	gcc -O2 -fPIC -shared -fvisibility=hidden -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ $<
+
+.PHONY: tuner-test

@@ -175,6 +175,8 @@ struct ncclComm {
   int nSlots = 0;
   int maxChannels = 0;
   ncclamd::CommTuning tune;
+  void* tunerCtx = nullptr;  // external tuner plugin context (tuner.cc)
+  bool tunerLoaded = false;
   int llChannels = 32;      // LL protocol: channels and line bytes per (channel, parity, sender)
   size_t llBytes = 32 << 10;
   int chanCap = 0;  // channels per launch that stay co-resident even with several ranks per GPU
@@ -247,6 +249,12 @@ ncclResult_t collFork(const CollInfo& info);
 bool llPlan(const CollInfo& info, LLOp* op);                  // LL eligibility + plan (enqueue.cc)
 bool llBatchable(const CollInfo& a, const CollInfo& b);
 ncclResult_t launchLLBatch(const std::vector<CollInfo>& ops);  // one LL launch for a group's small ARs
+
+// ---------------------------------------------------------------- tuner plugin (reference src/plugin/tuner.cc)
+enum TuneAlgo { TUNE_DEFAULT = 0, TUNE_LL = 1, TUNE_ONESHOT = 2, TUNE_DIRECT = 3 };
+ncclResult_t tunerLoad(ncclComm* comm);
+void tunerUnload(ncclComm* comm);
+void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, bool llOk, int* algo, int* nch);
 ncclResult_t collJoin(const CollInfo& info);
 ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
 

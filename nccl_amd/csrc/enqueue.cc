@@ -194,13 +194,20 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   const size_t bytes = info.count * (size_t)ts;
   const size_t npk = (bytes + 7) / 8;
   const CommTuning& t = comm->tune;
+  const bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
+  const bool fits = t.llOn && al8 && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
   // NCCL_PROTO leaves only LL enabled
-  bool useLL = t.llOn && (!t.simpleOn || (t.algo == 0 && bytes <= (size_t)t.llBytes));
-  const bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
-  if (!useLL || !al8 || npk > (size_t)comm->llChannels * (comm->llBytes / 16)) return false;
+  bool useLL = fits && (!t.simpleOn || (t.algo == 0 && bytes <= (size_t)t.llBytes));
+  int tuned = TUNE_DEFAULT, tunedNch = 0;
+  if (comm->tunerLoaded) {  // an external tuner plugin may overrule the size table (tuner.cc)
+    tunerPick(comm, FUNC_ALLREDUCE, bytes, 1, fits, &tuned, &tunedNch);
+    if (tuned != TUNE_DEFAULT) useLL = fits && tuned == TUNE_LL;
+  }
+  if (!useLL) return false;
   const uint64_t perCh = (uint64_t)t.llChannelBytes / 8;
   int nch = (int)((npk + perCh - 1) / perCh);
+  if (tunedNch > 0 && (uint64_t)tunedNch * (comm->llBytes / 16) >= npk) nch = tunedNch;
   if (nch < 1) nch = 1;
   if (nch > comm->llChannels) nch = comm->llChannels;
   if (nch > comm->chanCap) nch = comm->chanCap;
@@ -330,6 +337,14 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes : ((size_t)2 << 20) / n;
     oneShot = comm->tune.algo == 1 || (comm->tune.algo == 0 && bytes <= lim);
   }
+  int tunedNch = 0;
+  if (comm->tunerLoaded) {  // external tuner plugin: one-shot (TREE/SIMPLE) vs direct (RING/SIMPLE), channels
+    int tuned = TUNE_DEFAULT;
+    tunerPick(comm, info.func, count * (size_t)ts * (info.func == FUNC_ALLGATHER || info.func == FUNC_REDUCESCATTER ? n : 1),
+              1, false, &tuned, &tunedNch);
+    if (tuned == TUNE_ONESHOT && info.func == FUNC_ALLREDUCE) oneShot = true;
+    if (tuned == TUNE_DIRECT) oneShot = false;
+  }
   const bool oneShotAR = oneShot;
   // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce, one launch, no fences
   if (info.func == FUNC_ALLREDUCE && llPlan(info, &p.ll.ops[0])) {
@@ -413,10 +428,11 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   }
   if (oneShot) {
     p.algo = ALGO_ONESHOT;
-    planChannels(comm, count * ts, ts, p, (size_t)comm->tune.oneShotChannelBytes, 32);
+    size_t minPart = tunedNch > 0 ? (count * ts + tunedNch - 1) / tunedNch : (size_t)comm->tune.oneShotChannelBytes;
+    planChannels(comm, count * ts, ts, p, minPart, 32);
   } else {
-    planChannels(comm, blockElems * ts, ts, p, (size_t)comm->tune.minChannelBytes,
-                 comm->chanCap);
+    size_t minPart = tunedNch > 0 ? (blockElems * ts + tunedNch - 1) / tunedNch : (size_t)comm->tune.minChannelBytes;
+    planChannels(comm, blockElems * ts, ts, p, minPart, comm->chanCap);
   }
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,

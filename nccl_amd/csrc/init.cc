@@ -167,6 +167,7 @@ static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id,
   computeChannelCap(comm);
   if ((res = transportConnect(comm)) != ncclSuccess) goto fail;
   if ((res = commAllocDevState(comm)) != ncclSuccess) goto fail;
+  if ((res = tunerLoad(comm)) != ncclSuccess) goto fail;
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
   INFO("comm %p rank %d nRanks %d dev %d busId %s - Init COMPLETE", (void*)comm, rank, nranks, dev,
        comm->peers[rank].busId);
@@ -293,6 +294,7 @@ NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
     computeChannelCap(cs[i]);
     res = transportConnect(cs[i]);
     if (res == ncclSuccess) res = commAllocDevState(cs[i]);
+    if (res == ncclSuccess) res = tunerLoad(cs[i]);
   }
   (void)hipSetDevice(oldDev);
   if (res != ncclSuccess) {
@@ -336,6 +338,7 @@ NCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
 NCCL_ALIAS(ncclResult_t, ncclCommFinalize, ncclComm_t)
 
 static ncclResult_t commFree(ncclComm* comm) {
+  tunerUnload(comm);
   windowsFree(comm);
   if (comm->internalStream) (void)hipStreamDestroy(comm->internalStream);
   if (comm->evIn) (void)hipEventDestroy(comm->evIn);

@@ -249,3 +249,64 @@ def test_group_aggregates_small_allreduces(two_comms, dtype, op):
     want_rs = G.expected("reducescatter", rs_in, dtype, op)
     for r in range(n):
         assert G.same_bits(G.from_device(bufs[r][2], npdt), want_rs[r], dtype)
+
+
+def _tuner_worker(force, nch, q):
+    try:
+        os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "30000"
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        plugin = os.path.join(root, "tests", "native", "libnccl-tuner-test.so")
+        os.environ["NCCL_TUNER_PLUGIN"] = plugin
+        os.environ["TEST_TUNER_FORCE"] = force
+        os.environ["TEST_TUNER_NCH"] = str(nch)
+        logf = f"/tmp/nccl_amd_tuner_{force}_{os.getpid()}.log"
+        os.environ["NCCL_DEBUG"] = "TRACE"
+        os.environ["NCCL_DEBUG_FILE"] = logf
+        import torch
+        import nccl_amd
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comms = nccl_amd.Communicator.init_all([0, 0])
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        cs = list(zip(comms, streams))
+        errs = []
+        for i, (coll, count) in enumerate((("allreduce", 1024), ("allreduce", 16_384), ("allreduce", 300_001),
+                                           ("reducescatter", 2 * 50_000), ("allgather", 20_000), ("reduce", 77_777))):
+            errs += G.run_case(cs, coll, 7, 0, count, 0, seed=700 + i, root=1)
+        lib = ctypes.CDLL(plugin)
+        calls, inits, last = lib.testTunerCalls(), lib.testTunerInits(), lib.testTunerLastFunc()
+        for c in comms:
+            c.destroy()
+        log = open(logf).read() if os.path.exists(logf) else ""
+        q.put((errs, calls, inits, last, log))
+    except Exception as e:
+        q.put(([f"exception {e!r}"], 0, 0, -1, ""))
+
+
+@pytest.mark.parametrize("force,nch", [("ring_simple", 3), ("tree_simple", 0), ("ring_ll", 2), ("none", 0)])
+def test_tuner_plugin(built, force, nch):
+    """An external tuner plugin (reference ABI v6, tests/native/tuner_plugin.c) loaded through
+    NCCL_TUNER_PLUGIN steers algorithm/protocol/channels; every result stays bit-exact. Runs in a fresh
+    process: the plugin is loaded once per process, like the reference's (src/plugin/tuner.cc)."""
+    import multiprocessing as mp
+    import queue
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_tuner_worker, args=(force, nch, q))
+    p.start()
+    try:
+        errs, calls, inits, last, log = q.get(timeout=240)
+    except queue.Empty:
+        p.kill()
+        raise AssertionError("tuner worker timed out")
+    p.join(timeout=60)
+    assert not errs, errs
+    assert inits == 2, inits          # one init per communicator
+    assert calls >= 6, calls          # consulted for every collective
+    assert last == 1, last            # ncclFuncReduce was the last call
+    ar = [l for l in log.splitlines() if "AllReduce: " in l and ("->" in l or " LL " in l)]
+    if force == "ring_simple":   # every AllReduce on the direct path with the plugin's 3 channels
+        assert ar and all(" LL " not in l and "nch 3 " in l for l in ar), ar
+    elif force == "ring_ll":     # LL wherever it fits (1024 and 16384 elements); 2 channels where they suffice
+        assert sum(" LL count" in l for l in ar) >= 2 and any("nch 2 " in l for l in ar), ar

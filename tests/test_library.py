@@ -101,3 +101,40 @@ def test_registration_argument_checks_without_gpu(built):
     assert lib.ncclCommWindowDeregister(None, None) == 4
     out = P()
     assert lib.ncclWinGetUserPtr(None, None, ctypes.byref(out)) == 4
+
+
+def test_tuner_plugin_abi_mock(built):
+    """Drive the test tuner plugin through the v6 struct exactly as libnccl.so does (reference
+    plugins/tuner/example/test/test_plugin.c style: no GPU, synthetic sizes)."""
+    path = os.path.join(ROOT, "tests", "native", "libnccl-tuner-test.so")
+    if not os.path.exists(path):
+        subprocess.check_call(["make", "tuner-test"], cwd=ROOT)
+    lib = ctypes.CDLL(path)
+    P, I, S = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+    INIT = ctypes.CFUNCTYPE(I, ctypes.POINTER(P), ctypes.c_uint64, S, S, P, P, P)
+    GET = ctypes.CFUNCTYPE(I, P, I, S, I, P, I, I, I, ctypes.POINTER(I))
+    FIN = ctypes.CFUNCTYPE(I, P)
+
+    class V6(ctypes.Structure):
+        _fields_ = [("name", ctypes.c_char_p), ("init", INIT), ("getCollInfo", GET), ("finalize", FIN),
+                    ("getChunkSize", P)]
+
+    t = V6.in_dll(lib, "ncclTunerPlugin_v6")
+    assert t.name == b"mi355x-test"
+    ctx = P()
+    assert t.init(ctypes.byref(ctx), 1, 8, 1, None, None, None) == 0
+    table = (ctypes.c_float * 21)(*([-1.0] * 21))      # [7 algorithms][3 protocols]
+    table[1 * 3 + 2] = 12.5                             # RING/SIMPLE offered
+    table[0 * 3 + 2] = 9.0                              # TREE/SIMPLE offered
+    nch = I(0)
+    os.environ["TEST_TUNER_FORCE"] = "ring_simple"
+    os.environ["TEST_TUNER_NCH"] = "5"
+    try:
+        assert t.getCollInfo(ctx, 4, 1 << 20, 1, ctypes.cast(table, P), 7, 3, 0, ctypes.byref(nch)) == 0
+    finally:
+        os.environ.pop("TEST_TUNER_FORCE")
+        os.environ.pop("TEST_TUNER_NCH")
+    assert table[1 * 3 + 2] == 0.0 and table[0 * 3 + 2] == 9.0 and nch.value == 5
+    assert table[0] == -1.0                             # ignored entries stay ignored
+    assert lib.testTunerCalls() == 1 and lib.testTunerLastFunc() == 4
+    assert t.finalize(ctx) == 0
