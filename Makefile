@@ -20,7 +20,7 @@ DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test tuner-test
+all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -75,3 +75,11 @@ tests/native/libnccl-tuner-test.so: tests/native/tuner_plugin.c include/nccl_tun
 	gcc -O2 -fPIC -shared -fvisibility=hidden -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ $<
 
 .PHONY: tuner-test
+
+# nccl-tests-style native driver written against include/nccl.h only (C ABI check + Python-free timing)
+nccl-perf: tests/native/nccl_perf
+
+tests/native/nccl_perf: tests/native/nccl_perf.cc include/nccl.h $(LIBDIR)/libnccl.so
+	$(HIPCC) -O2 --offload-arch=$(ARCH) -Iinclude -o $@ $< -L$(LIBDIR) -lnccl -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+.PHONY: nccl-perf

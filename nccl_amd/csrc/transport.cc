@@ -188,6 +188,10 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
   for (int r = 0; r < comm->nRanks; r++)
     if (r != comm->rank && comm->peers[r].pid == me.pid && strcmp(comm->peers[r].busId, me.busId) == 0)
       comm->sharedDevInProcess = true;
+  // NCCL_AMD_FORK_JOIN=0: the caller guarantees every rank's stream has a hardware queue of its own
+  // (e.g. hipExtStreamCreateWithCUMask streams), so launch directly on it and skip the cross-queue
+  // event fork/join (tens of microseconds per collective)
+  if (!paramInt("NCCL_AMD_FORK_JOIN", 1)) comm->sharedDevInProcess = false;
   if (comm->sharedDevInProcess) {
     std::vector<uint32_t> mask((me.numCUs + 31) / 32, 0u);
     for (int cu = 0; cu < me.numCUs; cu++) mask[cu / 32] |= 1u << (cu % 32);
