@@ -1,0 +1,28 @@
+"""The C ABI driven from native code: tests/native/nccl_perf (nccl-tests style, built by `make nccl-perf`
+against include/nccl.h only) runs AllReduce sum/max over fp32/bf16 with 2 ranks on the one GPU, eager and
+hipGraph-replayed, and fails on any wrong element or async error."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "native", "nccl_perf")
+
+
+@pytest.mark.parametrize("args,forkjoin", [
+    (["-b", "8", "-e", "16777216", "-f", "16", "-i", "5"], "0"),
+    (["-b", "8", "-e", "1048576", "-f", "32", "-i", "5", "-g", "1"], "0"),
+    (["-b", "4", "-e", "4194304", "-f", "64", "-i", "3", "-t", "bf16", "-o", "max"], "0"),
+    (["-b", "1024", "-e", "1048576", "-f", "32", "-i", "3"], "1"),
+])
+def test_native_driver(built, args, forkjoin):
+    if not os.path.exists(EXE):
+        subprocess.check_call(["make", "nccl-perf"], cwd=ROOT)
+    env = dict(os.environ, NCCL_MULTI_RANK_GPU_ENABLE="1", NCCL_AMD_FORK_JOIN=forkjoin,
+               NCCL_AMD_SPIN_TIMEOUT_MS="20000")
+    out = subprocess.run([EXE, "-r", "2"] + args, env=env, capture_output=True, text=True, timeout=200)
+    assert out.returncode == 0, out.stdout + out.stderr
+    rows = [l.split() for l in out.stdout.splitlines() if l.strip() and not l.startswith("#")]
+    assert rows and all(r[-1] == "0" for r in rows), out.stdout
