@@ -297,9 +297,23 @@ class Communicator:
         if config is None:
             _check(lib.ncclCommInitRank(ctypes.byref(c), nranks, _uid(unique_id), rank), "ncclCommInitRank")
         else:
-            _check(lib.ncclCommInitRankConfig(ctypes.byref(c), nranks, _uid(unique_id), rank, ctypes.byref(config)),
-                   "ncclCommInitRankConfig")
+            rc = lib.ncclCommInitRankConfig(ctypes.byref(c), nranks, _uid(unique_id), rank, ctypes.byref(config))
+            if not (rc == Result.InProgress and config.blocking == 0):  # non-blocking: poll wait_ready()
+                _check(rc, "ncclCommInitRankConfig")
         return cls(c.value)
+
+    def wait_ready(self, timeout_s: float = 600.0) -> None:
+        """Non-blocking communicators: poll ncclCommGetAsyncError until it leaves ncclInProgress."""
+        import time
+        t0 = time.time()
+        while True:
+            e = self.async_error()
+            if e != Result.InProgress:
+                _check(e, "ncclCommInitRankConfig (non-blocking)")
+                return
+            if time.time() - t0 > timeout_s:
+                raise TimeoutError("communicator still initialising")
+            time.sleep(0.001)
 
     @classmethod
     def init_all(cls, devices: Sequence[int] | int) -> list["Communicator"]:

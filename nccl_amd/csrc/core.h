@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/nccl.h"
@@ -198,6 +199,7 @@ struct ncclComm {
   std::atomic<int> asyncResult{ncclSuccess};
   bool finalized = false;
   bool destroyed = false;
+  std::thread initThread;  // non-blocking ncclCommInitRankConfig (config.blocking = 0)
   uint64_t opCount = 0;
   uint64_t endMagic;
 };

@@ -137,10 +137,10 @@ struct ShapeInfo {
   CommTuning tune;
 };
 
-static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id, int rank, int dev,
-                                    const ncclConfig_t* cfg) {
-  ncclComm* comm = new ncclComm();
-  commDefaults(comm, rank, nranks, dev, cfg);
+// Initialise `comm` (commDefaults already applied) in place. On failure its device/bootstrap resources
+// are released but the object stays (the caller deletes it, or a non-blocking caller keeps it so the
+// user can read the error with ncclCommGetAsyncError and then destroy it).
+static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id, int rank, int dev) {
   ncclResult_t res = ncclSuccess;
   struct Blob {
     PeerInfo info;
@@ -148,7 +148,7 @@ static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id,
   };
   std::vector<Blob> blobs(nranks);
   if ((res = bootstrapInit(&id, rank, nranks, &comm->bootstrap)) != ncclSuccess) goto fail;
-  // Agree on the channel/slot shape: rank 0's parameters win (env may differ per process).
+  // Agree on the channel/slot shape and the tuning knobs: rank 0's parameters win (env may differ).
   {
     std::vector<ShapeInfo> shapes(nranks);
     shapes[rank] = {comm->maxChannels, comm->nSlots, comm->slotBytes, comm->tune};
@@ -171,15 +171,44 @@ static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id,
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
   INFO("comm %p rank %d nRanks %d dev %d busId %s - Init COMPLETE", (void*)comm, rank, nranks, dev,
        comm->peers[rank].busId);
-  *out = comm;
   return ncclSuccess;
 fail:
   transportFree(comm);
   bootstrapClose(comm->bootstrap);
-  comm->startMagic = comm->endMagic = 0;
-  delete comm;
-  *out = nullptr;
+  comm->bootstrap = nullptr;
   return res;
+}
+
+static ncclResult_t commInitRankDev(ncclComm** out, int nranks, ncclUniqueId id, int rank, int dev,
+                                    const ncclConfig_t* cfg) {
+  ncclComm* comm = new ncclComm();
+  commDefaults(comm, rank, nranks, dev, cfg);
+  ncclResult_t res = commInitRankInto(comm, nranks, id, rank, dev);
+  if (res != ncclSuccess) {
+    comm->startMagic = comm->endMagic = 0;
+    delete comm;
+    *out = nullptr;
+    return res;
+  }
+  *out = comm;
+  return ncclSuccess;
+}
+
+// Non-blocking communicator (config.blocking = 0; reference init.cc ncclCommInitRankConfig +
+// ncclCommGetAsyncError): the handle is returned at once with ncclInProgress and initialisation runs
+// on a thread; ncclCommGetAsyncError reports ncclInProgress until it finishes, then its result.
+static ncclResult_t commInitRankAsync(ncclComm** out, int nranks, ncclUniqueId id, int rank, int dev,
+                                      const ncclConfig_t* cfg) {
+  ncclComm* comm = new ncclComm();
+  commDefaults(comm, rank, nranks, dev, cfg);
+  comm->asyncResult.store(ncclInProgress);
+  comm->initThread = std::thread([comm, nranks, id, rank, dev]() {
+    ncclResult_t r = hipSetDevice(dev) == hipSuccess ? commInitRankInto(comm, nranks, id, rank, dev)
+                                                     : ncclUnhandledCudaError;
+    comm->asyncResult.store(r);
+  });
+  *out = comm;
+  return ncclInProgress;
 }
 
 }  // namespace ncclamd
@@ -234,6 +263,7 @@ static ncclResult_t initRankCommon(ncclComm_t* newcomm, int nranks, ncclUniqueId
       return commInitRankDev(newcomm, nranks, commId, myrank, dev, hasCfg ? &cfgCopy : nullptr);
     });
   }
+  if (hasCfg && cfgCopy.blocking == 0) return commInitRankAsync(newcomm, nranks, commId, myrank, dev, &cfgCopy);
   return commInitRankDev(newcomm, nranks, commId, myrank, dev, hasCfg ? &cfgCopy : nullptr);
 }
 
@@ -338,6 +368,7 @@ NCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
 NCCL_ALIAS(ncclResult_t, ncclCommFinalize, ncclComm_t)
 
 static ncclResult_t commFree(ncclComm* comm) {
+  if (comm->initThread.joinable()) comm->initThread.join();  // a non-blocking init still running
   tunerUnload(comm);
   windowsFree(comm);
   if (comm->internalStream) (void)hipStreamDestroy(comm->internalStream);
@@ -356,6 +387,7 @@ NCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   NCCLCHECK(commCheck(comm, "ncclCommDestroy", "comm"));
   int old = 0;
   (void)hipGetDevice(&old);
+  if (comm->initThread.joinable()) comm->initThread.join();
   (void)hipSetDevice(comm->device);
   // Local, like the reference (init.cc:2879-2911): wait for this rank's kernels, then for the credit
   // words peers still owe us (the only writes a peer can make after our kernels finished), so no
@@ -372,6 +404,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommDestroy, ncclComm_t)
 NCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;
   NCCLCHECK(commCheck(comm, "ncclCommAbort", "comm"));
+  if (comm->initThread.joinable()) comm->initThread.join();
   // Kernels poll the abort word inside every bounded spin (reference primitives.h:154-164).
   if (comm->hostAbort) __atomic_store_n(comm->hostAbort, 1u, __ATOMIC_RELEASE);
   (void)hipSetDevice(comm->device);

@@ -310,3 +310,26 @@ def test_tuner_plugin(built, force, nch):
         assert ar and all(" LL " not in l and "nch 3 " in l for l in ar), ar
     elif force == "ring_ll":     # LL wherever it fits (1024 and 16384 elements); 2 channels where they suffice
         assert sum(" LL count" in l for l in ar) >= 2 and any("nch 2 " in l for l in ar), ar
+
+
+def test_nonblocking_init_from_one_thread(built):
+    """config.blocking = 0 (reference init.cc, nccl.h.in:84-108): ncclCommInitRankConfig returns
+    ncclInProgress at once, so ONE thread can create both ranks without a group; ncclCommGetAsyncError
+    reports ncclInProgress until each is ready, then the comms work normally."""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    torch.cuda.set_device(0)
+    uid = nccl_amd.get_unique_id()
+    cfg = nccl_amd.Config.default(blocking=0)
+    comms = [nccl_amd.Communicator.init(2, r, uid, cfg) for r in range(2)]
+    states = [c.async_error() for c in comms]
+    assert all(s in (0, 7) for s in states), states
+    for c in comms:
+        c.wait_ready(120)
+    assert [c.async_error() for c in comms] == [0, 0]
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    errs = G.run_case(list(zip(comms, streams)), "allreduce", 7, 0, 77_777, 0, seed=11)
+    for c in comms:
+        c.destroy()
+    assert not errs, errs
