@@ -85,13 +85,13 @@ def test_group_of_mixed_collectives(two_comms):
     assert np.array_equal(mx[1].cpu().numpy(), oracle.reduce(ins, 7, 2, 1))
 
 
+@pytest.mark.parametrize("count", [1_000, 50_001])  # LL protocol / one-shot
 @pytest.mark.parametrize("device_scalar", [False, True])
-def test_premulsum_custom_op(two_comms, device_scalar):
+def test_premulsum_custom_op(two_comms, device_scalar, count):
     import torch
     import nccl_amd
     import oracle
     comms, streams = two_comms
-    count = 50_001
     ins = _inputs(2, count, seed=13)
     scal = np.float32(0.375)
     dev_scal = torch.tensor([scal], device="cuda")
