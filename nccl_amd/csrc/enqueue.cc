@@ -7,6 +7,8 @@
 // replaced by the small MI355X table in choosePlan()).
 #include <string.h>
 
+#include <algorithm>
+
 #include "core.h"
 
 namespace ncclamd {
@@ -108,7 +110,7 @@ void loadTuning(CommTuning* t) {
   t->symDisable = (int)paramInt("NCCL_AMD_SYM_DISABLE", 0);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
   t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks)
-  t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 128 << 10);
+  t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)
   t->llChannelBytes = paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096);
   if (t->llChannelBytes < 8) t->llChannelBytes = 8;
   t->minChannelBytes = paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
@@ -198,7 +200,10 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   const bool fits = t.llOn && al8 && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
   // NCCL_PROTO leaves only LL enabled
-  bool useLL = fits && (!t.simpleOn || (t.algo == 0 && bytes <= (size_t)t.llBytes));
+  // LL lines carry 2x the payload to each of the n-1 peers: its range shrinks with n like the one-shot's
+  // (default 256 KiB / n: 128 KiB at n=2, 32 KiB at n=8)
+  const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : std::max<size_t>(16 << 10, ((size_t)256 << 10) / comm->nRanks);
+  bool useLL = fits && (!t.simpleOn || (t.algo == 0 && bytes <= llLim));
   int tuned = TUNE_DEFAULT, tunedNch = 0;
   if (comm->tunerLoaded) {  // an external tuner plugin may overrule the size table (tuner.cc)
     tunerPick(comm, FUNC_ALLREDUCE, bytes, 1, fits, &tuned, &tunedNch);
