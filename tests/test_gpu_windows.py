@@ -28,7 +28,8 @@ def _cases(n, quick=False):
     """(collective, dtype, op, count, elem_offset, inplace)"""
     out = []
     counts = [1, 7, 4096 + 5, 200_003] if not quick else [7, 70_001]
-    for dtype, op in ((7, 0), (9, 0), (6, 0), (2, 3), (3, 2), (4, 1), (0, 0), (8, 4), (2, 4), (10, 0)):
+    for dtype, op in ((7, 0), (9, 0), (6, 0), (2, 3), (3, 2), (4, 1), (0, 0), (8, 4), (2, 4), (10, 0), (1, 4),
+                      (5, 2), (11, 1)):
         for count in counts:
             out.append(("allreduce", dtype, op, count, 0, False))
         out.append(("reducescatter", dtype, op, 50_001 * n, 0, False))
