@@ -173,6 +173,9 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
     d.flags[r] = comm->peerFlags[r];
   }
   d.counters = comm->counters;
+  // the LL channels of a launch must be co-resident like any channel: never more than chanCap (the line
+  // area was sized for the full count; host planning and the kernel's batch modulus use this value)
+  if (comm->llChannels > comm->chanCap && comm->chanCap > 0) comm->llChannels = comm->chanCap;
   d.llOffset = llOffset(comm);
   d.llBytes = comm->llBytes;
   d.llChannels = comm->llChannels;
