@@ -134,6 +134,8 @@ struct CommTuning {
   int64_t llChannelBytes;   // NCCL_AMD_LL_CHANNEL_BYTES
   int64_t minChannelBytes;  // NCCL_AMD_MIN_CHANNEL_BYTES
   int64_t oneShotChannelBytes;  // NCCL_AMD_ONESHOT_CHANNEL_BYTES
+  int copyVariant;          // NCCL_AMD_COPY_VARIANT (nRanks == 1 copy kernel, diagnostics)
+  int64_t copyGrid;         // NCCL_AMD_COPY_GRID (cap on its workgroups; default: one per 16 KiB tile)
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
 
@@ -242,6 +244,8 @@ struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src
   hipStream_t stream;
   CollArgs args;
   LLBatchArgs ll;  // ALGO_LL
+  int copyVariant;  // ALGO_COPY
+  int64_t copyGrid;
 };
 
 ncclResult_t enqueueCheck(CollInfo* info);
@@ -275,7 +279,7 @@ ncclWindow_vidmem* findSymWindow(ncclComm* comm, const void* p, size_t bytes);
 void windowsFree(ncclComm* comm);  // release every window and IPC mapping (destroy/abort)
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
 ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);
-ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream);
+ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int variant, int64_t gridCap);
 ncclResult_t warmKernels();  // load all kernel code objects on the current device (kernels.hip)
 int typeSize(ncclDataType_t t);
 

@@ -115,6 +115,8 @@ void loadTuning(CommTuning* t) {
   if (t->llChannelBytes < 8) t->llChannelBytes = 8;
   t->minChannelBytes = paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
   t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
+  t->copyVariant = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
+  t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);
 }
 
 // Pointer check (reference argcheck.cc:12-28), active with NCCL_CHECK_POINTERS=1.
@@ -303,6 +305,8 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     }
     p.algo = ALGO_COPY;
     p.bytes = bytes;
+    p.copyVariant = comm->tune.copyVariant;
+    p.copyGrid = comm->tune.copyGrid;
     return launchPlan(p);
   }
 

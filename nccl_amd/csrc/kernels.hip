@@ -73,18 +73,17 @@ __global__ void copyBytesKernel(char* dst, const char* src, uint64_t n) {
     dst[i] = src[i];
 }
 
-ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream) {
+ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int var, int64_t gridCap) {
   if (bytes == 0 || dst == src) return ncclSuccess;
   if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
     uint64_t npk = bytes >> 4;
     if (npk) {
       // variant (NCCL_AMD_COPY_VARIANT): 0 nt/nt U4 (default), 1 plain/plain U4, 2 plain/nt U4, 3 nt/nt U8
-      int var = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
       int U = var == 3 ? 8 : 4;
       uint64_t tiles = (npk + 256 * U - 1) / (256 * U);
       // one 16 KiB tile per workgroup by default: measured best on 256 MiB with buffers rotated past the
       // 256 MiB Infinity Cache (6.48 TB/s vs 6.26 for a 2048-block grid-stride; scripts/copy_variants.hip)
-      int grid = (int)std::min<uint64_t>(tiles, (uint64_t)paramInt("NCCL_AMD_COPY_GRID", 1 << 30));
+      int grid = (int)std::min<uint64_t>(tiles, (uint64_t)(gridCap > 0 ? gridCap : 1));
       u32x4* d = (u32x4*)dst;
       const u32x4* s = (const u32x4*)src;
       switch (var) {
@@ -110,7 +109,8 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
 }
 
 ncclResult_t launchPlan(const LaunchPlan& p) {
-  if (p.algo == ALGO_COPY) return launchCopy(p.args.recvbuff, p.args.sendbuff, p.bytes, p.stream);
+  if (p.algo == ALGO_COPY)
+    return launchCopy(p.args.recvbuff, p.args.sendbuff, p.bytes, p.stream, p.copyVariant, p.copyGrid);
   if (p.func == FUNC_ALLGATHER) return launchKernGather(p);
   switch (p.datatype) {
     case ncclInt8: case ncclUint8: return launchKernU8(p);
