@@ -460,3 +460,19 @@ class Communicator:
         if self._comm:
             _check(load().ncclCommAbort(self._comm), "ncclCommAbort")
             self._comm = 0
+
+
+def ddp_comm_hook(comm: "Communicator"):
+    """A torch DDP communication hook that reduces every gradient bucket with this engine (ncclAvg, in
+    place, on the current stream) instead of the process group's backend:
+    ``ddp_model.register_comm_hook(None, nccl_amd.ddp_comm_hook(comm))``."""
+    import torch
+
+    def hook(state, bucket):
+        t = bucket.buffer()
+        comm.allreduce(t, t, RedOp.AVG)
+        fut = torch.futures.Future()
+        fut.set_result(t)
+        return fut
+
+    return hook
