@@ -316,11 +316,14 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   uint64_t blockElems;
   switch (info.func) {
     case FUNC_ALLREDUCE:
-    case FUNC_REDUCE:
-      // rank block = alignUp(divUp(count, n), 16/sizeof(T)) (reference all_reduce.h:38)
-      blockElems = (count + n - 1) / n;
+    case FUNC_REDUCE: {
+      // rank block = alignUp(divUp(count, n), 16/sizeof(T)) (reference all_reduce.h:38); a Reduce over
+      // n >= 3 ranks cuts n-1 blocks, none owned by the root (kernels.h Channel::rootless)
+      const int nb = (info.func == FUNC_REDUCE && n >= 3) ? n - 1 : n;
+      blockElems = (count + nb - 1) / nb;
       blockElems = (blockElems + epp - 1) / epp * epp;
       break;
+    }
     default:  // RS: recvcount, AG: sendcount
       blockElems = count;
       break;

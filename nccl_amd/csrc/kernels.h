@@ -314,39 +314,49 @@ struct Channel {
     if (COLL == COLL_AR || COLL == COLL_AG) return true;
     return COLL == COLL_REDUCE && !isRoot && p == a.root;
   }
+  // Reduce over n >= 3 ranks: the root owns no block — the buffer is cut into n-1 blocks owned by the other
+  // ranks — so the root's links carry only the n-1 reduced blocks in (S in total) instead of its own
+  // block's n-1 contributions plus the n-1 reduced blocks (2(n-1)/n * S). Fold order is unchanged
+  // (root+1, ..., root, reduce.h:34-52): it never depended on who folds.
+  __device__ bool rootless() const { return COLL == COLL_REDUCE && n >= 3; }
+  __device__ bool owns(int r) const { return !rootless() || r != a.root; }
+  __device__ int blockOf(int r) const { return rootless() && r > a.root ? r - 1 : r; }
 
   // A: scatter input block p to owner p's RS staging (AR, RS, REDUCE)
   __device__ bool phaseA(int step) {
     int tid = threadIdx.x;
     if (tid < NCCL_AMD_MAX_RANKS) {
       uint64_t s = ctr(CTR_SEND_RS, tid);
-      sh.want[tid] = (tid < n && tid != me && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
+      sh.want[tid] = (tid < n && tid != me && owns(tid) && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
     }
     __syncthreads();
     if (!waitAll(dc, sh.st, myFlags(FLG_RS_ACK), sh.want, forceAcq)) return false;
     for (int k = 1; k < n; k++) {
       int p = peerAt(k);
+      if (!owns(p)) continue;
+      const int b = blockOf(p);
       uint64_t lo, hi;
-      sliceRange(a, c, step, blockLen(p), lo, hi);
+      sliceRange(a, c, step, blockLen(b), lo, hi);
       int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
       char* dst = dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me);
-      const char* src = (const char*)a.sendbuff + ((uint64_t)p * a.chunk + lo) * ts;
+      const char* src = (const char*)a.sendbuff + ((uint64_t)b * a.chunk + lo) * ts;
       copyRange<T, true>(dst, src, (hi - lo) * ts, aligned);
     }
     if (tid < NCCL_AMD_MAX_RANKS) {
-      bool act = tid < n && tid != me;
+      bool act = tid < n && tid != me && owns(tid);
       sh.sigVal[tid] = act ? ctr(CTR_SEND_RS, tid) + 1 : 0;
       sh.sigPtr[tid] = act ? dc.flags[tid] + flagIndex(c, FLG_RS_READY, me) : nullptr;
     }
     __syncthreads();
     signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, !noRel);
-    if (tid < n && tid != me) ctr(CTR_SEND_RS, tid)++;
+    if (tid < n && tid != me && owns(tid)) ctr(CTR_SEND_RS, tid)++;
     __syncthreads();
     return true;
   }
 
   // B: fold my block (AR, RS, REDUCE) or publish my input block (AG); push to AG staging
   __device__ bool phaseB(int step) {
+    if (rootless() && isRoot) return true;  // the root owns no block
     int tid = threadIdx.x;
     const bool push = (COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && !isRoot));
     if (COLL != COLL_AG) {
@@ -363,8 +373,9 @@ struct Channel {
       __syncthreads();
       if (!waitAll(dc, sh.st, myFlags(FLG_AG_ACK), sh.want, forceAcq)) return false;
     }
+    const int myB = blockOf(me);
     uint64_t lo, hi;
-    sliceRange(a, c, step, blockLen(me), lo, hi);
+    sliceRange(a, c, step, blockLen(myB), lo, hi);
     const uint64_t nelem = hi - lo;
     if (tid == 0) {
       int np = 0;
@@ -378,7 +389,7 @@ struct Channel {
       int first = (COLL == COLL_REDUCE ? a.root + 1 : me + 1) % n;
       for (int k = 0; k < n; k++) {
         int q = (first + k) % n;
-        sh.srcPtr[k] = q == me ? (const char*)a.sendbuff + ((uint64_t)me * a.chunk + lo) * ts
+        sh.srcPtr[k] = q == me ? (const char*)a.sendbuff + ((uint64_t)myB * a.chunk + lo) * ts
                                : dc.staging[me] + stagingOffset(dc, c, STG_RS, (int)(ctr(CTR_RECV_RS, q) % nSlots), q);
       }
     }
@@ -391,7 +402,7 @@ struct Channel {
     } else {
       char* dstLocal = nullptr;
       if (COLL == COLL_RS) dstLocal = (char*)a.recvbuff + lo * ts;
-      else if (COLL == COLL_AR || isRoot) dstLocal = (char*)a.recvbuff + ((uint64_t)me * a.chunk + lo) * ts;
+      else if (COLL == COLL_AR || isRoot) dstLocal = (char*)a.recvbuff + ((uint64_t)myB * a.chunk + lo) * ts;
       foldRange<T, OP>(fn, n, sh.srcPtr, nelem, dstLocal, sh.pushPtr, sh.nPush, aligned);
     }
     // one release covers both: AG data ready at each destination; RS slots consumed (ack to senders)
@@ -490,10 +501,11 @@ struct Channel {
     if (!waitAll(dc, sh.st, myFlags(FLG_AG_READY), sh.want, true)) return false;
     for (int k = 1; k < n; k++) {
       int q = (me + n - k) % n;
+      const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
       uint64_t lo, hi;
-      sliceRange(a, c, step, blockLen(q), lo, hi);
+      sliceRange(a, c, step, blockLen(b), lo, hi);
       const char* src = dc.staging[me] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_RECV_AG, q) % nSlots), q);
-      char* dst = (char*)a.recvbuff + ((uint64_t)q * a.chunk + lo) * ts;
+      char* dst = (char*)a.recvbuff + ((uint64_t)b * a.chunk + lo) * ts;
       copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
     }
     if (tid < NCCL_AMD_MAX_RANKS) {
