@@ -262,6 +262,34 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dic
     comm.deregister_window(win)
     del win_t, sendw, recvw, base, hbuf, hres
 
+    # --- staged-path tuning matrix at the headline size (data for the next tuning round: knobs are read
+    #     at communicator init, so each setting gets its own communicator) ---
+    S = (16 if quick else 256) * MIB
+    c = S // 4
+    xs = torch.empty(c, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+    ys = torch.empty_like(xs)
+    tuning = []
+    knobs = ("NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_MIN_CHANNEL_BYTES")
+    saved = {k: os.environ.get(k) for k in knobs}
+    for env in ({}, {"NCCL_AMD_SLOT_BYTES": "65536"}, {"NCCL_AMD_SLOT_BYTES": "262144"},
+                {"NCCL_AMD_SLOT_BYTES": "524288"}, {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_MAX_CTAS": "128"},
+                {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}):
+        for k in knobs:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+        ms = tmax(_time_ms(lambda: cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, sp), stream, 10))
+        tuning.append({"env": env or "default", "ms": round(ms, 4),
+                       "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)})
+        torch.cuda.synchronize()
+        cm.destroy()
+    for k, v in saved.items():
+        os.environ.pop(k, None)
+        if v is not None:
+            os.environ[k] = v
+    out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}", "runs": tuning}
+    del xs, ys
+
     # --- xGMI probes (rank 0, peer copies via hipMemcpyPeerAsync) ---
     ndev = torch.cuda.device_count()
     if rank == 0 and ndev > 1:
