@@ -1,0 +1,45 @@
+"""One rank of a 2-process AllReduce on the one-GPU box, rendezvous through a file (no launcher, so one
+of the two processes can run under rocprofv3 without any process being spawned from a profiled one).
+usage: mp_rank.py RANK UIDFILE [ITERS]  — rank 1 creates the ncclUniqueId and writes it to UIDFILE."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import nccl_amd  # noqa: E402
+
+
+def main():
+    rank, path = int(sys.argv[1]), sys.argv[2]
+    iters = int(sys.argv[3]) if len(sys.argv) > 3 else 5
+    if rank == 1:
+        uid = nccl_amd.get_unique_id()
+        with open(path + ".tmp", "wb") as f:
+            f.write(uid)
+        os.rename(path + ".tmp", path)
+    else:
+        t0 = time.time()
+        while not os.path.exists(path):
+            if time.time() - t0 > 60:
+                raise TimeoutError("no unique id")
+            time.sleep(0.05)
+        uid = open(path, "rb").read()
+    torch.cuda.set_device(0)
+    comm = nccl_amd.Communicator.init(2, rank, uid)
+    S = 256 << 20
+    x = torch.full((S // 4,), float(rank + 1), device="cuda")
+    y = torch.empty_like(x)
+    s = torch.cuda.current_stream()
+    for _ in range(2 + iters):
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), S // 4, 7, 0, s.cuda_stream)
+    torch.cuda.synchronize()
+    ok = bool((y == 3.0).all())
+    print(f"rank {rank}: ok={ok} async={comm.async_error()}", flush=True)
+    comm.destroy()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
