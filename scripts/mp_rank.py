@@ -1,6 +1,7 @@
 """One rank of a 2-process AllReduce on the one-GPU box, rendezvous through a file (no launcher, so one
 of the two processes can run under rocprofv3 without any process being spawned from a profiled one).
-usage: mp_rank.py RANK UIDFILE [ITERS]  — rank 1 creates the ncclUniqueId and writes it to UIDFILE."""
+usage: mp_rank.py RANK UIDFILE [ITERS] [staged|sym] — rank 1 creates the ncclUniqueId and writes it to
+UIDFILE; `sym` puts both buffers in a symmetric window (zero-copy kernels)."""
 import os
 import sys
 import time
@@ -29,14 +30,24 @@ def main():
     torch.cuda.set_device(0)
     comm = nccl_amd.Communicator.init(2, rank, uid)
     S = 256 << 20
-    x = torch.full((S // 4,), float(rank + 1), device="cuda")
-    y = torch.empty_like(x)
+    mode = sys.argv[4] if len(sys.argv) > 4 else "staged"
+    if mode == "sym":
+        win_t = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
+        win = comm.register_window(win_t.data_ptr(), 2 * S)
+        x = win_t[:S].view(torch.float32)
+        y = win_t[S:].view(torch.float32)
+        x.fill_(float(rank + 1))
+    else:
+        x = torch.full((S // 4,), float(rank + 1), device="cuda")
+        y = torch.empty_like(x)
     s = torch.cuda.current_stream()
     for _ in range(2 + iters):
         comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), S // 4, 7, 0, s.cuda_stream)
     torch.cuda.synchronize()
     ok = bool((y == 3.0).all())
     print(f"rank {rank}: ok={ok} async={comm.async_error()}", flush=True)
+    if mode == "sym":
+        comm.deregister_window(win)
     comm.destroy()
     return 0 if ok else 1
 

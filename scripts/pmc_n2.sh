@@ -6,12 +6,13 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp NCCL_AMD_SPIN_TIMEOUT_MS=20000
 mkdir -p gpurun_out/pmc2
+M=${MODE:-staged}
 for C in FETCH_SIZE WRITE_SIZE; do
   U=/tmp/uid_$C.bin; rm -f $U
-  timeout -k 5 100 python3 scripts/mp_rank.py 1 $U > gpurun_out/pmc2/rank1_$C.log 2>&1 &
+  timeout -k 5 100 python3 scripts/mp_rank.py 1 $U 5 $M > gpurun_out/pmc2/rank1_${M}_$C.log 2>&1 &
   P1=$!
-  timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc2/$C -o run -- python3 scripts/mp_rank.py 0 $U \
-    > gpurun_out/pmc2/rank0_$C.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $C --output-format csv -d gpurun_out/pmc2/${M}_$C -o run -- python3 scripts/mp_rank.py 0 $U 5 $M \
+    > gpurun_out/pmc2/rank0_${M}_$C.log 2>&1
   R0=$?
   wait $P1; R1=$?
   echo "$C rank0=$R0 rank1=$R1"
