@@ -20,7 +20,7 @@ DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf
+all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf plan-test
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -83,3 +83,12 @@ tests/native/nccl_perf: tests/native/nccl_perf.cc include/nccl.h $(LIBDIR)/libnc
 	$(HIPCC) -O2 --offload-arch=$(ARCH) -Iinclude -o $@ $< -L$(LIBDIR) -lnccl -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 .PHONY: nccl-perf
+
+# CPU test driver of enqueue.cc's planning (no GPU: launches and the few HIP calls are stubbed)
+plan-test: tests/native/plan_test
+
+tests/native/plan_test: tests/native/plan_test.cc $(SRCDIR)/enqueue.cc $(SRCDIR)/debug.cc $(HDRS)
+	$(CXX) -O1 -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ tests/native/plan_test.cc \
+	  $(SRCDIR)/enqueue.cc $(SRCDIR)/debug.cc -lpthread
+
+.PHONY: plan-test

@@ -1,0 +1,105 @@
+// plan_test.cc — CPU test driver for the host-side planning of enqueue.cc (size table, protocol and
+// algorithm choice, channel/slice plan, NCCL_ALGO / NCCL_PROTO handling). It is compiled together with
+// enqueue.cc and debug.cc (no GPU, no HIP runtime): the launch entry points and the few HIP runtime calls
+// enqueue.cc makes are stubbed so every plan is recorded and printed instead of launched.
+//
+//   plan_test NRANKS FUNC(ar|rs|ag|reduce) DTYPE COUNT [ALIGN_OFFSET_BYTES] [CHANCAP]
+// prints one line: algo=<copy|onerank|direct|oneshot|ll> nch=<channels> part=<elements|payloads>
+//                  slice=<elements> steps=<n> chunk=<elements>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../nccl_amd/csrc/core.h"
+
+// ---- HIP runtime stubs (enqueue.cc only sets the device, queries attributes and records events) ----
+extern "C" {
+hipError_t hipSetDevice(int) { return hipSuccess; }
+hipError_t hipGetLastError(void) { return hipSuccess; }
+const char* hipGetErrorString(hipError_t) { return "stub"; }
+hipError_t hipPointerGetAttributes(hipPointerAttribute_t*, const void*) { return hipErrorInvalidValue; }
+hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
+}
+
+namespace ncclamd {
+static LaunchPlan gPlan;
+static SymPlan gSym;
+static int gKind = -1;  // 0 LaunchPlan, 1 SymPlan
+ncclResult_t launchPlan(const LaunchPlan& p) {
+  gPlan = p;
+  gKind = 0;
+  return ncclSuccess;
+}
+ncclResult_t launchSymPlan(const SymPlan& p) {
+  gSym = p;
+  gKind = 1;
+  return ncclSuccess;
+}
+ncclWindow_vidmem* findSymWindow(ncclComm*, const void*, size_t) { return nullptr; }
+bool groupActive() { return false; }
+ncclResult_t groupDeferColl(const CollInfo&) { return ncclSuccess; }
+void groupRecordError(ncclResult_t) {}
+void tunerPick(ncclComm*, CollFunc, size_t, int, bool, int*, int* nch) { *nch = 0; }
+ncclResult_t commCheck(const ncclComm*, const char*, const char*) { return ncclSuccess; }
+}  // namespace ncclamd
+
+using namespace ncclamd;
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: plan_test NRANKS FUNC DTYPE COUNT [ALIGN_OFFSET] [CHANCAP]\n");
+    return 2;
+  }
+  const int n = atoi(argv[1]);
+  const char* f = argv[2];
+  const int dt = atoi(argv[3]);
+  const size_t count = strtoull(argv[4], nullptr, 0);
+  const size_t off = argc > 5 ? strtoull(argv[5], nullptr, 0) : 0;
+  ncclComm comm;
+  comm.startMagic = comm.endMagic = kCommMagic;
+  comm.rank = 0;
+  comm.nRanks = n;
+  comm.device = 0;
+  comm.minCTAs = 1;
+  comm.maxCTAs = comm.maxChannels = 256;
+  comm.nSlots = 2;
+  // commDefaults' slot size: 1 GiB staging budget / (channels x 2 kinds x 2 slots x n), in [16 KiB, 1 MiB]
+  comm.slotBytes = ((size_t)1 << 30) / (256 * 2 * 2 * (n > 1 ? n : 2));
+  if (comm.slotBytes > ((size_t)1 << 20)) comm.slotBytes = (size_t)1 << 20;
+  if (comm.slotBytes < ((size_t)16 << 10)) comm.slotBytes = (size_t)16 << 10;
+  comm.chanCap = argc > 6 ? atoi(argv[6]) : 256;
+  comm.devComm = (DevComm*)0x1000;
+  loadTuning(&comm.tune);
+  CollInfo info;
+  memset(&info, 0, sizeof(info));
+  info.func = !strcmp(f, "rs") ? FUNC_REDUCESCATTER : !strcmp(f, "ag") ? FUNC_ALLGATHER
+            : !strcmp(f, "reduce") ? FUNC_REDUCE : FUNC_ALLREDUCE;
+  info.opName = f;
+  info.sendbuff = (const void*)(0x10000000ull + off);
+  info.recvbuff = (void*)(0x20000000ull + off);
+  info.count = count;
+  info.datatype = (ncclDataType_t)dt;
+  info.op = ncclSum;
+  info.comm = &comm;
+  info.stream = nullptr;
+  ncclResult_t r = launchColl(info);
+  if (r != ncclSuccess) {
+    printf("error=%d\n", (int)r);
+    return 1;
+  }
+  if (gKind == 1) {
+    printf("algo=sym nch=%d part=%lu slice=0 steps=1 chunk=%lu\n", gSym.nChannels, (unsigned long)gSym.args.part,
+           (unsigned long)gSym.args.chunk);
+    return 0;
+  }
+  const char* names[] = {"copy", "onerank", "direct", "oneshot", "ll"};
+  const LaunchPlan& p = gPlan;
+  if (p.algo == ALGO_LL)
+    printf("algo=ll nch=%d part=%lu slice=0 steps=1 chunk=%lu\n", p.nChannels, (unsigned long)p.ll.ops[0].part,
+           (unsigned long)p.ll.ops[0].chunk);
+  else
+    printf("algo=%s nch=%d part=%lu slice=%lu steps=%d chunk=%lu\n", names[p.algo], p.nChannels,
+           (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps, (unsigned long)p.args.chunk);
+  return 0;
+}

@@ -1,0 +1,107 @@
+"""CPU tests of the host-side planning in enqueue.cc (no GPU): tests/native/plan_test compiles enqueue.cc
+with the launches and the few HIP calls stubbed and prints the plan of one collective. Checks the size
+table (LL / one-shot / direct crossovers and how they scale with n), NCCL_ALGO / NCCL_PROTO (reference
+syntax), the LL alignment and capacity rules, the co-residency channel cap, the rootless Reduce block
+split, and the invariants every plan must satisfy for the kernels' indexing to be in bounds."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "native", "plan_test")
+SIZES = {0: 1, 1: 1, 2: 4, 3: 4, 4: 8, 5: 8, 6: 2, 7: 4, 8: 8, 9: 2, 10: 1, 11: 1}
+
+
+@pytest.fixture(scope="module")
+def exe():
+    src = os.path.join(ROOT, "tests", "native", "plan_test.cc")
+    if not os.path.exists(EXE) or os.path.getmtime(EXE) < os.path.getmtime(src):
+        subprocess.check_call(["make", "plan-test"], cwd=ROOT, stdout=subprocess.DEVNULL)
+    return EXE
+
+
+def plan(exe, n, func, dtype, count, offset=0, chancap=256, **env):
+    e = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_")}
+    e.update({k: str(v) for k, v in env.items()})
+    out = subprocess.run([exe, str(n), func, str(dtype), str(count), str(offset), str(chancap)], env=e,
+                         capture_output=True, text=True, timeout=30)
+    assert out.returncode == 0, out.stdout + out.stderr
+    return {k: (v if k == "algo" else int(v)) for k, v in (t.split("=") for t in out.stdout.split())}
+
+
+@pytest.mark.parametrize("n,nbytes,algo", [
+    (1, 4096, "copy"), (1, 256 << 20, "copy"),
+    (2, 8, "ll"), (2, 64 << 10, "ll"), (2, 128 << 10, "ll"), (2, 256 << 10, "oneshot"), (2, 1 << 20, "oneshot"),
+    (2, 4 << 20, "direct"), (2, 256 << 20, "direct"),
+    (4, 64 << 10, "ll"), (4, 128 << 10, "oneshot"), (4, 512 << 10, "oneshot"), (4, 1 << 20, "direct"),
+    (8, 16 << 10, "ll"), (8, 32 << 10, "ll"), (8, 64 << 10, "oneshot"), (8, 256 << 10, "oneshot"),
+    (8, 512 << 10, "direct"), (8, 256 << 20, "direct"),
+])
+def test_allreduce_size_table(exe, n, nbytes, algo):
+    assert plan(exe, n, "ar", 7, nbytes // 4)["algo"] == algo
+
+
+def test_proto_and_algo_overrides(exe):
+    assert plan(exe, 8, "ar", 7, (256 << 10) // 4, NCCL_PROTO="LL")["algo"] == "ll"        # LL to capacity
+    assert plan(exe, 2, "ar", 7, 1024, NCCL_PROTO="^LL")["algo"] == "oneshot"
+    assert plan(exe, 2, "ar", 7, 1024, NCCL_PROTO="Simple")["algo"] == "oneshot"
+    assert plan(exe, 2, "ar", 7, 1024, NCCL_PROTO="LL,Simple")["algo"] == "ll"
+    assert plan(exe, 2, "ar", 7, 1024, NCCL_ALGO="DIRECT")["algo"] == "direct"
+    assert plan(exe, 2, "ar", 7, 1024, NCCL_ALGO="RING")["algo"] == "direct"
+    assert plan(exe, 8, "ar", 7, 64 << 20, NCCL_ALGO="ONESHOT")["algo"] == "oneshot"
+    assert plan(exe, 2, "ar", 7, 1024, NCCL_ALGO="DIRECT", NCCL_PROTO="LL")["algo"] == "ll"  # only LL left
+    assert plan(exe, 2, "ar", 7, 100_000, NCCL_AMD_LL_BYTES=1 << 20)["algo"] == "ll"
+    assert plan(exe, 2, "ar", 7, 4_000_000, NCCL_AMD_ONESHOT_BYTES=64 << 20)["algo"] == "oneshot"
+
+
+def test_ll_needs_8_byte_alignment_and_room(exe):
+    assert plan(exe, 2, "ar", 7, 1001, offset=4)["algo"] == "oneshot"     # 4-byte aligned only
+    assert plan(exe, 2, "ar", 7, 1001, offset=8)["algo"] == "ll"
+    big = plan(exe, 2, "ar", 7, (512 << 10) // 4, NCCL_PROTO="LL")        # exactly the line area
+    assert big["algo"] == "ll" and big["part"] * 16 <= 32 << 10
+    assert plan(exe, 2, "ar", 7, (1 << 20) // 4, NCCL_PROTO="LL,Simple", NCCL_AMD_LL_BYTES=4 << 20)["algo"] == "oneshot"
+
+
+@pytest.mark.parametrize("func", ["rs", "ag", "reduce"])
+def test_non_allreduce_always_direct(exe, func):
+    for count in (1, 1000, 1 << 20):
+        assert plan(exe, 8, func, 9, count)["algo"] == "direct"
+
+
+def test_rootless_reduce_blocks(exe):
+    # n >= 3: n-1 blocks (root owns none), each alignUp(divUp(count, n-1), 16/sizeof(T)) elements
+    for n, count in ((3, 1), (4, 999_999), (8, 33_554_432)):
+        p = plan(exe, n, "reduce", 2, count)
+        epp = 16 // 4
+        want = -(-count // (n - 1))
+        want = -(-want // epp) * epp
+        assert p["chunk"] == want, (n, count, p)
+    p = plan(exe, 2, "reduce", 2, 1000)  # n = 2 keeps one block per rank
+    assert p["chunk"] == 500
+
+
+@pytest.mark.parametrize("n,func,dtype,count", [
+    (2, "ar", 7, 67_108_864), (8, "ar", 7, 67_108_864), (8, "ar", 6, 12_345_679), (3, "ar", 8, 7_777_777),
+    (8, "rs", 9, 67_108_864), (8, "ag", 9, 67_108_864), (8, "reduce", 2, 33_554_432), (5, "ar", 0, 3_000_001),
+])
+def test_plan_invariants(exe, n, func, dtype, count):
+    p = plan(exe, n, func, dtype, count)
+    ts = SIZES[dtype]
+    epp = 16 // ts
+    assert p["algo"] == "direct"
+    assert 1 <= p["nch"] <= 256
+    assert p["part"] % epp == 0 and p["slice"] % epp == 0 and 0 < p["slice"] <= p["part"]
+    assert p["steps"] == -(-p["part"] // p["slice"])
+    assert p["part"] * p["nch"] >= p["chunk"]          # the channels cover a whole rank block
+    if func == "ar":
+        assert p["chunk"] * n >= count and p["chunk"] % epp == 0
+    if func in ("rs", "ag"):
+        assert p["chunk"] == count
+
+
+def test_channel_cap(exe):
+    # several ranks per GPU: every channel of a launch must be co-resident, so plans respect chanCap
+    for cap in (1, 7, 64):
+        assert plan(exe, 4, "ar", 7, 64 << 20, chancap=cap)["nch"] <= cap
+        assert plan(exe, 4, "ar", 7, 1000, chancap=cap, NCCL_PROTO="LL")["nch"] <= cap
