@@ -429,8 +429,8 @@ def main(argv=None):
         step()
     e1.record(stream)
     torch.cuda.synchronize()
+    t1 = time.perf_counter()  # this rank's K steps are done; the MAX over ranks below covers the slowest
     barrier()
-    t1 = time.perf_counter()
     wall = t1 - t0
     gpu_ms = e0.elapsed_time(e1) / args.steps
     wall, gpu_ms = max_over_ranks(dist, [wall, gpu_ms])
