@@ -15,6 +15,11 @@
 // counters exactly like the reference's head/tail protocol (prims_simple.h:100-173), but
 // bidirectional over all 7 links at once instead of one ring neighbour.
 //
+// Besides this staged kernel (collKernel, with its one-shot variant COLL_AR1) the file holds
+//   llKernel   the LL protocol for small AllReduces and group batches (flag-in-data lines, no fences),
+//   symKernel  the zero-copy kernels for buffers in symmetric windows (peers' buffers pulled directly),
+//   oneRankKernel (PreMulSum at nRanks == 1; the nRanks == 1 copy lives in kernels.hip).
+//
 // Memory model: remote payload = `global_store_dwordx4 ... sc0 sc1` (system-scope
 // write-through) into the peer's UNCACHED staging; every storing wave drains (s_waitcnt vmcnt(0)),
 // the workgroup barriers, one lane issues a system release fence and then a system-scope flag
