@@ -83,14 +83,17 @@ struct CollArgs {
 // LL AllReduce batch: up to kMaxLLBatch small AllReduce ops of one group (same comm, stream, type and
 // op) run by ONE launch (reference: ops of a group aggregated into one kernel plan, enqueue.cc:405-470).
 constexpr int kMaxLLBatch = 32;
+enum LLColl { LL_AR = 0, LL_RS = 1, LL_AG = 2 };
 struct LLOp {
   const void* send;
   void* recv;
-  uint64_t count;  // elements
+  uint64_t count;  // elements (AllReduce: of the buffer; ReduceScatter / AllGather: of one rank block)
   uint64_t chunk;  // elements per rank block (fold order of each element's owner)
   uint64_t part;   // 8-byte payloads per channel
   int nch;         // channels this op uses
   int chOff;       // first channel (batches spread their ops over the LL channels)
+  int coll;        // LLColl
+  int pad;
 };
 struct LLBatchArgs {
   const DevComm* comm;

@@ -189,26 +189,31 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
   p.args.nSteps = (int)((part + slice - 1) / slice);
 }
 
-// LL eligibility and channel plan of one AllReduce (reference tuning: LL for the smallest sizes, or as
-// NCCL_PROTO dictates). Needs 8-byte aligned buffers and room in the comm's line area.
+// LL eligibility and channel plan of one AllReduce, ReduceScatter or AllGather (reference tuning: LL for
+// the smallest sizes, or as NCCL_PROTO dictates). Needs 8-byte aligned buffers (and, for the blocked
+// collectives, 8-byte aligned rank blocks) and room in the comm's line area. The payload space is the
+// AllReduce buffer or one ReduceScatter / AllGather rank block; the size limit applies to it.
 bool llPlan(const CollInfo& info, LLOp* op) {
   ncclComm* comm = info.comm;
-  if (info.func != FUNC_ALLREDUCE || comm->nRanks == 1) return false;
+  if (info.func == FUNC_REDUCE || comm->nRanks == 1) return false;
+  const int n = comm->nRanks;
   const int ts = typeSize(info.datatype);
-  const size_t bytes = info.count * (size_t)ts;
+  const size_t bytes = info.count * (size_t)ts;  // payload space
   const size_t npk = (bytes + 7) / 8;
   const CommTuning& t = comm->tune;
-  const bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
+  bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
+  if (info.func != FUNC_ALLREDUCE) al8 = al8 && (bytes & 7) == 0;
   const bool fits = t.llOn && al8 && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
-  // NCCL_PROTO leaves only LL enabled
+  // NCCL_PROTO leaves only LL enabled.
   // LL lines carry 2x the payload to each of the n-1 peers: its range shrinks with n like the one-shot's
-  // (default 256 KiB / n: 128 KiB at n=2, 32 KiB at n=8)
-  const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : std::max<size_t>(16 << 10, ((size_t)256 << 10) / comm->nRanks);
+  // (default 256 KiB / n: 128 KiB at n=2, 32 KiB at n=8; for ReduceScatter / AllGather that is per rank
+  // block, i.e. 256 KiB of total data at any n, the same per-rank link bytes)
+  const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : std::max<size_t>(16 << 10, ((size_t)256 << 10) / n);
   bool useLL = fits && (!t.simpleOn || (t.algo == 0 && bytes <= llLim));
   int tuned = TUNE_DEFAULT, tunedNch = 0;
   if (comm->tunerLoaded) {  // an external tuner plugin may overrule the size table (tuner.cc)
-    tunerPick(comm, FUNC_ALLREDUCE, bytes, 1, fits, &tuned, &tunedNch);
+    tunerPick(comm, info.func, info.func == FUNC_ALLREDUCE ? bytes : bytes * n, 1, fits, &tuned, &tunedNch);
     if (tuned != TUNE_DEFAULT) useLL = fits && tuned == TUNE_LL;
   }
   if (!useLL) return false;
@@ -220,10 +225,12 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   if (nch > comm->chanCap) nch = comm->chanCap;
   uint64_t part = (npk + nch - 1) / nch;
   if (part * 16 > comm->llBytes) return false;
-  const int n = comm->nRanks;
   const uint64_t epp = 16 / ts;
-  uint64_t blockElems = (info.count + n - 1) / n;
-  blockElems = (blockElems + epp - 1) / epp * epp;
+  uint64_t blockElems = info.count;
+  if (info.func == FUNC_ALLREDUCE) {
+    blockElems = (info.count + n - 1) / n;
+    blockElems = (blockElems + epp - 1) / epp * epp;
+  }
   op->send = info.sendbuff;
   op->recv = info.recvbuff;
   op->count = info.count;
@@ -231,6 +238,8 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   op->part = part;
   op->nch = nch;
   op->chOff = 0;
+  op->coll = info.func == FUNC_ALLREDUCE ? LL_AR : info.func == FUNC_REDUCESCATTER ? LL_RS : LL_AG;
+  op->pad = 0;
   return true;
 }
 
@@ -358,8 +367,9 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     if (tuned == TUNE_DIRECT) oneShot = false;
   }
   const bool oneShotAR = oneShot;
-  // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce, one launch, no fences
-  if (info.func == FUNC_ALLREDUCE && llPlan(info, &p.ll.ops[0])) {
+  // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce / ReduceScatter / AllGather,
+  // one launch, no fences
+  if (llPlan(info, &p.ll.ops[0])) {
     p.algo = ALGO_LL;
     p.ll.comm = comm->devComm;
     p.ll.redArg = p.args.redArg;

@@ -594,7 +594,9 @@ __device__ __forceinline__ uint64_t loadLL(const uint64_t* p) {
 template <typename T, int OP>
 __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>& fn, const LLOp& op, int c, int j,
                                             uint64_t e64, int& abortSh) {
-  // c: physical channel (line area + epoch); j: this op's part index on it
+  // c: physical channel (line area + epoch); j: this op's part index on it. Payload space: AllReduce the
+  // whole buffer; ReduceScatter / AllGather one rank block (rank p's line for payload pk carries block p's
+  // payload pk for ReduceScatter, its own input's payload pk for AllGather).
   const int tid = threadIdx.x, me = dc.rank, n = dc.nRanks;
   constexpr int EPP = 8 / sizeof(T);  // elements per 8-byte payload
   const uint32_t flag = (uint32_t)e64 ? (uint32_t)e64 : 1u;  // never 0 (the area starts zeroed)
@@ -604,39 +606,47 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
   const uint64_t lo = min((uint64_t)j * op.part, npk), hi = min(lo + op.part, npk);
   const char* send = (const char*)op.send;
   char* recv = (char*)op.recv;
+  auto payload = [&](const char* base, uint64_t pk) -> uint64_t {
+    uint64_t v = 0;
+    if (pk * 8 + 8 <= nbytes) v = *(const uint64_t*)(base + pk * 8);
+    else for (uint64_t b = pk * 8; b < nbytes; b++) v |= (uint64_t)(unsigned char)base[b] << (8 * (b - pk * 8));
+    return v;
+  };
+  auto storePayload = [&](char* base, uint64_t pk, uint64_t v) {
+    if (pk * 8 + 8 <= nbytes) *(uint64_t*)(base + pk * 8) = v;
+    else for (uint64_t b = pk * 8; b < nbytes; b++) base[b] = (char)(v >> (8 * (b - pk * 8)));
+  };
 
-  // send: my payload of [lo,hi) to every peer, 16-byte lines (two 8-byte payloads per line)
+  // send: payloads [lo,hi) to every peer, 16-byte lines (two 8-byte payloads per thread step)
   for (uint64_t i = lo + 2 * tid; i < hi; i += 2 * kThreads) {
-    uint64_t v[2] = {0, 0};
-    for (int h = 0; h < 2; h++) {
-      uint64_t pk = i + h;
-      if (pk >= hi) break;
-      if (pk * 8 + 8 <= nbytes) v[h] = *(const uint64_t*)(send + pk * 8);
-      else for (uint64_t b = pk * 8; b < nbytes; b++) v[h] |= (uint64_t)(unsigned char)send[b] << (8 * (b - pk * 8));
-    }
-    u32x4 line = {(uint32_t)v[0], flag, (uint32_t)(v[0] >> 32), flag};
-    u32x4 line2 = {(uint32_t)v[1], flag, (uint32_t)(v[1] >> 32), flag};
     const uint64_t off = (i - lo) * 16;  // payload pk's line sits at (pk - lo) * 16
+    uint64_t v0 = 0, v1 = 0;
+    if (op.coll != LL_RS) {
+      v0 = payload(send, i);
+      if (i + 1 < hi) v1 = payload(send, i + 1);
+    }
     for (int k = 1; k < n; k++) {
       int p = (me + k) % n;
+      if (op.coll == LL_RS) {  // block p goes to its owner
+        v0 = payload(send + (uint64_t)p * nbytes, i);
+        if (i + 1 < hi) v1 = payload(send + (uint64_t)p * nbytes, i + 1);
+      }
       char* base = (char*)dc.flags[p] + llLineOffset(dc, c, par, me) + off;
-      storeRemote(base, line);
-      if (i + 1 < hi) storeRemote(base + 16, line2);
+      storeRemote(base, u32x4{(uint32_t)v0, flag, (uint32_t)(v0 >> 32), flag});
+      if (i + 1 < hi) storeRemote(base + 16, u32x4{(uint32_t)v1, flag, (uint32_t)(v1 >> 32), flag});
     }
   }
-  // receive + fold: one 8-byte payload per thread step (after the barrier every input byte has been
-  // sent, so an in-place output cannot overwrite a payload another thread still has to send)
+  // receive: one 8-byte payload per thread step (after the barrier every input byte has been sent, so an
+  // in-place output cannot overwrite a payload another thread still has to send)
   __syncthreads();
   const uint64_t t0 = clockTicks();
   bool ok = true;
+  const char* myLL = (const char*)dc.flags[me];
   for (uint64_t pk = lo + tid; pk < hi; pk += kThreads) {
-    const uint64_t firstElt = pk * 8 / sizeof(T);
-    const int owner = (int)(firstElt / op.chunk);  // 8-byte payloads never straddle rank blocks
     // pass 1: wait until every peer's line for this payload carries this epoch's flag
     uint32_t pending = 0;
     for (int q = 0; q < n; q++)
       if (q != me) pending |= 1u << q;
-    const char* myLL = (const char*)dc.flags[me];
     uint32_t spins = 0;
     while (pending) {
       for (int q = 0; q < n; q++) {
@@ -661,34 +671,45 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
       ok = false;
       break;
     }
+    if (op.coll == LL_AG) {  // place every peer's payload in its block, and my own
+      for (int q = 0; q < n; q++) {
+        char* dst = recv + (uint64_t)q * nbytes;
+        if (q == me) {
+          if (dst != send) storePayload(dst, pk, payload(send, pk));
+        } else {
+          const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
+          storePayload(dst, pk, (loadLL(ln) & 0xffffffffull) | (loadLL(ln + 1) << 32));
+        }
+      }
+      continue;
+    }
     // pass 2: fold in the owner block's ring order (the lines stay valid until epoch + 2)
+    const int owner = op.coll == LL_RS ? me : (int)((pk * 8 / sizeof(T)) / op.chunk);  // never straddles
+    const char* mine = op.coll == LL_RS ? send + (uint64_t)me * nbytes : send;
     union { uint64_t u; T e[EPP]; } acc, x;
     for (int k = 0; k < n; k++) {
       int q = (owner + 1 + k) % n;
       if (q == me) {
-        x.u = 0;
-        if (pk * 8 + 8 <= nbytes) x.u = *(const uint64_t*)(send + pk * 8);
-        else for (uint64_t b = pk * 8; b < nbytes; b++) x.u |= (uint64_t)(unsigned char)send[b] << (8 * (b - pk * 8));
+        x.u = payload(mine, pk);
       } else {
         const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
         x.u = (loadLL(ln) & 0xffffffffull) | (loadLL(ln + 1) << 32);
       }
 #pragma unroll
-      for (int j = 0; j < EPP; j++) {
-        T y = fn.pre(x.e[j]);
-        acc.e[j] = k == 0 ? y : fn.red(y, acc.e[j]);
+      for (int e = 0; e < EPP; e++) {
+        T y = fn.pre(x.e[e]);
+        acc.e[e] = k == 0 ? y : fn.red(y, acc.e[e]);
       }
     }
 #pragma unroll
-    for (int j = 0; j < EPP; j++) acc.e[j] = fn.post(acc.e[j]);
-    if (pk * 8 + 8 <= nbytes) *(uint64_t*)(recv + pk * 8) = acc.u;
-    else for (uint64_t b = pk * 8; b < nbytes; b++) recv[b] = (char)(acc.u >> (8 * (b - pk * 8)));
+    for (int e = 0; e < EPP; e++) acc.e[e] = fn.post(acc.e[e]);
+    storePayload(recv, pk, acc.u);
   }
   __syncthreads();  // every payload of this op is folded before the next op's lines go out
   return ok && !abortSh;
 }
 
-// One launch runs a batch of LL AllReduce ops; op k occupies channels [chOff_k, chOff_k + nch_k) mod
+// One launch runs a batch of LL ops (a single ReduceScatter / AllGather, or up to 32 AllReduces); op k occupies channels [chOff_k, chOff_k + nch_k) mod
 // llChannels, so the small ops of a batch land on different channels and run in parallel (one
 // round trip for the batch). A channel runs its ops in batch order and its epoch advances once per op
 // it takes part in; all ranks build the same batch, so epochs agree.
@@ -913,13 +934,19 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
         hipLaunchKernelGGL((collKernel<T, OP, COLL_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
     case FUNC_REDUCESCATTER:
-      hipLaunchKernelGGL((collKernel<T, OP, COLL_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_LL)
+        hipLaunchKernelGGL((llKernel<T, OP>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.ll);
+      else
+        hipLaunchKernelGGL((collKernel<T, OP, COLL_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
     case FUNC_REDUCE:
       hipLaunchKernelGGL((collKernel<T, OP, COLL_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
     case FUNC_ALLGATHER:
-      hipLaunchKernelGGL((collKernel<T, 0, COLL_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_LL)
+        hipLaunchKernelGGL((llKernel<T, 0>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.ll);
+      else
+        hipLaunchKernelGGL((collKernel<T, 0, COLL_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
   }
   HIPCHECK(hipGetLastError());

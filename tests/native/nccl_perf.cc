@@ -4,11 +4,14 @@
 //
 //   nccl_perf [-d ndev] [-r ranks_per_dev] [-b min_bytes] [-e max_bytes] [-f factor] [-i iters] [-w warmup]
 //             [-o op: sum|max] [-t type: float|half|bf16|int] [-g 0|1 (replay a captured hipGraph)]
+//             [-c coll: ar|rs|ag]
 //
 // All ranks live in this process (ncclCommInitAll over ndev devices x ranks_per_dev; several ranks per
 // device need NCCL_MULTI_RANK_GPU_ENABLE=1). Each rank r fills its input with (r+1), so every element of
-// an AllReduce sum must be n(n+1)/2 (max: n); the "#wrong" column counts mismatching elements.
-// busBW = algBW * 2(n-1)/n (reference plugins/profiler/inspector/inspector.cc:1450-1492).
+// an AllReduce / ReduceScatter sum must be n(n+1)/2 (max: n) and AllGather block q must be q+1; the
+// "#wrong" column counts mismatching elements. bytes = the AllReduce buffer, the ReduceScatter input or
+// the AllGather output (nccl-tests convention). busBW = algBW * 2(n-1)/n for AllReduce, (n-1)/n for the
+// others (reference plugins/profiler/inspector/inspector.cc:1450-1492).
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
@@ -47,7 +50,7 @@ __global__ void fillKernel(void* p, size_t n, int type, float v) {
     else ((int*)p)[i] = (int)v;
   }
 }
-__global__ void checkKernel(const void* p, size_t n, int type, float want, unsigned long long* bad) {
+__global__ void checkKernel(const void* p, size_t n, int type, float want, size_t blk, unsigned long long* bad) {
   unsigned long long local = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float v;
@@ -55,7 +58,7 @@ __global__ void checkKernel(const void* p, size_t n, int type, float want, unsig
     else if (type == ncclFloat16) v = __half2float(((const __half*)p)[i]);
     else if (type == ncclBfloat16) v = __bfloat162float(((const __hip_bfloat16*)p)[i]);
     else v = (float)((const int*)p)[i];
-    local += v != want;
+    local += v != (blk ? (float)(i / blk + 1) : want);
   }
   if (local) atomicAdd(bad, local);
 }
@@ -66,8 +69,9 @@ int main(int argc, char** argv) {
   double factor = 2;
   ncclRedOp_t op = ncclSum;
   ncclDataType_t type = ncclFloat32;
+  char coll = 'a';  // a: AllReduce, r: ReduceScatter, g: AllGather
   int c;
-  while ((c = getopt(argc, argv, "d:r:b:e:f:i:w:o:t:g:")) != -1) {
+  while ((c = getopt(argc, argv, "d:r:b:e:f:i:w:o:t:g:c:")) != -1) {
     switch (c) {
       case 'd': ndevArg = atoi(optarg); break;
       case 'r': perDev = atoi(optarg); break;
@@ -77,6 +81,7 @@ int main(int argc, char** argv) {
       case 'i': iters = atoi(optarg); break;
       case 'w': warmup = atoi(optarg); break;
       case 'g': graph = atoi(optarg); break;
+      case 'c': coll = !strcmp(optarg, "rs") ? 'r' : !strcmp(optarg, "ag") ? 'g' : 'a'; break;
       case 'o': op = !strcmp(optarg, "max") ? ncclMax : ncclSum; break;
       case 't':
         type = !strcmp(optarg, "half") ? ncclFloat16 : !strcmp(optarg, "bf16") ? ncclBfloat16
@@ -118,15 +123,23 @@ int main(int argc, char** argv) {
   HIPCK(hipMallocManaged(&bad, sizeof(*bad)));
   for (int r = 0; r < n; r++) HIPCK(hipStreamSynchronize(streams[r]));
   const float want = op == ncclSum ? n * (n + 1) / 2.0f : (float)n;
-  printf("# nccl_perf: libnccl %d, %d ranks (%d devices x %d), type %d, op %s, %s\n", version, n, ndev, perDev,
-         (int)type, op == ncclSum ? "sum" : "max", graph ? "hipGraph replay" : "eager launches");
+  printf("# nccl_perf: libnccl %d, %s, %d ranks (%d devices x %d), type %d, op %s, %s\n", version,
+         coll == 'r' ? "ReduceScatter" : coll == 'g' ? "AllGather" : "AllReduce", n, ndev, perDev, (int)type,
+         op == ncclSum ? "sum" : "max", graph ? "hipGraph replay" : "eager launches");
+  auto issue = [&](int r, size_t count) {
+    if (coll == 'r') return ncclReduceScatter(send[r], recv[r], count / n, type, op, comms[r], streams[r]);
+    if (coll == 'g') return ncclAllGather(send[r], recv[r], count / n, type, comms[r], streams[r]);
+    return ncclAllReduce(send[r], recv[r], count, type, op, comms[r], streams[r]);
+  };
   printf("# %12s %12s %10s %10s %10s %8s\n", "bytes", "count", "time(us)", "algbw", "busbw", "#wrong");
-  for (size_t bytes = minB; bytes <= maxB; bytes = std::max(bytes + es, (size_t)(bytes * factor))) {
-    const size_t count = bytes / es;
+  const size_t step = coll == 'a' ? es : es * n;
+  for (size_t bytes = minB; bytes <= maxB; bytes = std::max(bytes + step, (size_t)(bytes * factor))) {
+    if (coll != 'a' && bytes % step) continue;
+    const size_t count = bytes / es;  // elements of the AllReduce buffer / RS input / AG output
     auto enqueue = [&](int iters_) {
       for (int k = 0; k < iters_; k++) {
         NCK(ncclGroupStart());
-        for (int r = 0; r < n; r++) NCK(ncclAllReduce(send[r], recv[r], count, type, op, comms[r], streams[r]));
+        for (int r = 0; r < n; r++) NCK(issue(r, count));
         NCK(ncclGroupEnd());
       }
     };
@@ -139,7 +152,7 @@ int main(int argc, char** argv) {
         HIPCK(hipSetDevice(devs[r]));
         hipGraph_t g;
         HIPCK(hipStreamBeginCapture(streams[r], hipStreamCaptureModeRelaxed));
-        for (int k = 0; k < iters; k++) NCK(ncclAllReduce(send[r], recv[r], count, type, op, comms[r], streams[r]));
+        for (int k = 0; k < iters; k++) NCK(issue(r, count));
         HIPCK(hipStreamEndCapture(streams[r], &g));
         hipGraphExec_t ex;
         HIPCK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
@@ -165,7 +178,9 @@ int main(int argc, char** argv) {
     *bad = 0;
     for (int r = 0; r < n; r++) {
       HIPCK(hipSetDevice(devs[r]));
-      hipLaunchKernelGGL(checkKernel, dim3(256), dim3(256), 0, streams[r], recv[r], count, (int)type, want, bad);
+      const size_t outCount = coll == 'r' ? count / n : count;
+      hipLaunchKernelGGL(checkKernel, dim3(256), dim3(256), 0, streams[r], recv[r], outCount, (int)type, want,
+                         coll == 'g' ? count / n : (size_t)0, bad);
       HIPCK(hipStreamSynchronize(streams[r]));
     }
     for (int r = 0; r < n; r++) {
@@ -178,7 +193,8 @@ int main(int argc, char** argv) {
     }
     const double us = ms * 1e3 / iters;
     const double algbw = bytes / (us * 1e-6) / 1e9;
-    printf("  %12zu %12zu %10.2f %10.2f %10.2f %8llu\n", bytes, count, us, algbw, algbw * 2.0 * (n - 1) / n,
+    printf("  %12zu %12zu %10.2f %10.2f %10.2f %8llu\n", bytes, count, us, algbw,
+           algbw * (coll == 'a' ? 2.0 : 1.0) * (n - 1) / n,
            (unsigned long long)*bad);
     if (*bad) return 5;
   }

@@ -7,6 +7,8 @@ with a repeated device, NCCL_MULTI_RANK_GPU_ENABLE=1, reference init.cc:68) and 
 import multiprocessing as mp
 import os
 
+import numpy as np
+
 import pytest
 
 os.environ.setdefault("NCCL_AMD_SPIN_TIMEOUT_MS", "30000")
@@ -205,3 +207,36 @@ def test_ll_epoch_wraparound(built):
     for c in comms:
         c.destroy()
     assert not errs, errs
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_ll_reducescatter_allgather(built, nranks):
+    """LL protocol for the blocked collectives (8-byte aligned rank blocks within the LL range): every
+    type and op, ragged payload tails (blocks of 8k+2 / 8k+4 bytes are excluded by the alignment rule,
+    so the tails are whole 8-byte payloads across channel parts), in place and out of place."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0] * nranks)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    cs = list(zip(comms, streams))
+    errs = []
+    i = 0
+    for dtype in (7, 9, 6, 2, 3, 4, 0, 1, 5, 8, 10, 11):
+        es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+        for block_bytes in (8, 1024, 24_008):
+            block = max(1, block_bytes // es)
+            for coll, ops in (("reducescatter", (0, 1, 2, 3, 4)), ("allgather", (0,))):
+                for op in ops:
+                    count = block * nranks if coll == "reducescatter" else block
+                    errs += G.run_case(cs, coll, dtype, op, count, 0, seed=900 + i)
+                    if op == 0:
+                        errs += G.run_case(cs, coll, dtype, op, count, 0, seed=901 + i, inplace=True)
+                    i += 1
+        if errs:
+            break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])

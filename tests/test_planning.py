@@ -1,8 +1,8 @@
 """CPU tests of the host-side planning in enqueue.cc (no GPU): tests/native/plan_test compiles enqueue.cc
 with the launches and the few HIP calls stubbed and prints the plan of one collective. Checks the size
 table (LL / one-shot / direct crossovers and how they scale with n), NCCL_ALGO / NCCL_PROTO (reference
-syntax), the LL alignment and capacity rules, the co-residency channel cap, the rootless Reduce block
-split, and the invariants every plan must satisfy for the kernels' indexing to be in bounds."""
+syntax), the LL alignment and capacity rules, the co-residency channel cap, the ReduceScatter / AllGather LL
+range, the rootless Reduce block split, and the invariants every plan must satisfy for the kernels' indexing to be in bounds."""
 import os
 import subprocess
 
@@ -63,10 +63,26 @@ def test_ll_needs_8_byte_alignment_and_room(exe):
     assert plan(exe, 2, "ar", 7, (1 << 20) // 4, NCCL_PROTO="LL,Simple", NCCL_AMD_LL_BYTES=4 << 20)["algo"] == "oneshot"
 
 
-@pytest.mark.parametrize("func", ["rs", "ag", "reduce"])
-def test_non_allreduce_always_direct(exe, func):
+def test_reduce_always_direct(exe):
     for count in (1, 1000, 1 << 20):
-        assert plan(exe, 8, func, 9, count)["algo"] == "direct"
+        assert plan(exe, 8, "reduce", 9, count)["algo"] == "direct"
+
+
+@pytest.mark.parametrize("func", ["rs", "ag"])
+def test_blocked_collectives_size_table(exe, func):
+    # LL while a rank block is within 256 KiB / n (256 KiB of total data), direct above; the blocks
+    # must be 8-byte aligned (count * sizeof(T) % 8 == 0) for the line payloads
+    for n in (2, 4, 8):
+        limit = (256 << 10) // n // 4          # fp32 elements per block at the limit
+        assert plan(exe, n, func, 7, 2)["algo"] == "ll"
+        assert plan(exe, n, func, 7, limit)["algo"] == "ll"
+        assert plan(exe, n, func, 7, limit + 2)["algo"] == "direct"
+        assert plan(exe, n, func, 7, 1)["algo"] == "direct"   # 4-byte blocks: no LL
+        assert plan(exe, n, func, 8, 1)["algo"] == "ll"       # one fp64 per block
+    assert plan(exe, 2, func, 7, 1000, NCCL_PROTO="^LL")["algo"] == "direct"
+    assert plan(exe, 2, func, 7, 1000, offset=4)["algo"] == "direct"
+    p = plan(exe, 8, func, 7, 1000)
+    assert p["chunk"] == 1000 and p["part"] * p["nch"] * 8 >= 4000
 
 
 def test_rootless_reduce_blocks(exe):
