@@ -95,13 +95,18 @@ struct LLOp {
   int coll;        // LLColl
   int pad;
 };
-struct LLBatchArgs {
+// The kernel arguments hold room for K ops: a lone op launches with K = 1 (88 bytes of kernel arguments
+// instead of 1.8 KiB; the host issue cost of a launch grows with its argument bytes, about 3 us at 64 B
+// vs 6.5 us at 2 KiB on the MI355X box, scripts/launch_probe.hip).
+template <int K>
+struct LLArgs {
   const DevComm* comm;
   uint64_t redArg;
   const void* redArgPtr;
   int nOps;
-  LLOp ops[kMaxLLBatch];
+  LLOp ops[K];
 };
+using LLBatchArgs = LLArgs<kMaxLLBatch>;
 
 // Symmetric (window) collective arguments: every rank's buffers as mapped in this process (reference
 // ncclSymPtr::peerPtr, src/device/symmetric/kernel.cuh), so peers are read and written directly.

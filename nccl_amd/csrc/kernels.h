@@ -713,8 +713,8 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
 // llChannels, so the small ops of a batch land on different channels and run in parallel (one
 // round trip for the batch). A channel runs its ops in batch order and its epoch advances once per op
 // it takes part in; all ranks build the same batch, so epochs agree.
-template <typename T, int OP>
-__global__ void __launch_bounds__(kThreads) llKernel(LLBatchArgs a) {
+template <typename T, int OP, int K>
+__global__ void __launch_bounds__(kThreads) llKernel(LLArgs<K> a) {
   __shared__ int abortSh;
   const DevComm& dc = *a.comm;
   const int c = blockIdx.x;
@@ -728,7 +728,7 @@ __global__ void __launch_bounds__(kThreads) llKernel(LLBatchArgs a) {
   uint64_t e64 = dc.counters[ctrIndex(c, CTR_LL, 0)];
   __syncthreads();
   const int L = dc.llChannels;
-  for (int k = 0; k < a.nOps; k++) {
+  for (int k = 0; k < (K == 1 ? 1 : a.nOps); k++) {
     const int j = (c - a.ops[k].chOff + L) % L;  // op k runs on channels chOff, chOff+1, ... (mod L)
     if (j >= a.ops[k].nch) continue;
     e64++;
@@ -914,6 +914,24 @@ __global__ void __launch_bounds__(256) oneRankKernel(T* dst, const T* src, uint6
 
 // ------------------------------------------------------------------------------------ host launcher
 
+// LL launch with the smallest argument block that holds the batch (1, 8 or 32 ops)
+template <typename T, int OP, int K>
+inline void launchLLK(const LaunchPlan& p) {
+  LLArgs<K> a;
+  a.comm = p.ll.comm;
+  a.redArg = p.ll.redArg;
+  a.redArgPtr = p.ll.redArgPtr;
+  a.nOps = p.ll.nOps;
+  for (int k = 0; k < p.ll.nOps && k < K; k++) a.ops[k] = p.ll.ops[k];
+  hipLaunchKernelGGL((llKernel<T, OP, K>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
+}
+template <typename T, int OP>
+inline void launchLL(const LaunchPlan& p) {
+  if (p.ll.nOps <= 1) launchLLK<T, OP, 1>(p);
+  else if (p.ll.nOps <= 8) launchLLK<T, OP, 8>(p);
+  else launchLLK<T, OP, kMaxLLBatch>(p);
+}
+
 template <typename T, int OP>
 inline ncclResult_t launchTyped(const LaunchPlan& p) {
   if (p.algo == ALGO_ONERANK) {
@@ -927,7 +945,7 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
   switch (p.func) {
     case FUNC_ALLREDUCE:
       if (p.algo == ALGO_LL)
-        hipLaunchKernelGGL((llKernel<T, OP>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.ll);
+        launchLL<T, OP>(p);
       else if (p.algo == ALGO_ONESHOT)
         hipLaunchKernelGGL((collKernel<T, OP, COLL_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       else
@@ -935,7 +953,7 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
       break;
     case FUNC_REDUCESCATTER:
       if (p.algo == ALGO_LL)
-        hipLaunchKernelGGL((llKernel<T, OP>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.ll);
+        launchLL<T, OP>(p);
       else
         hipLaunchKernelGGL((collKernel<T, OP, COLL_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
@@ -944,7 +962,7 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
       break;
     case FUNC_ALLGATHER:
       if (p.algo == ALGO_LL)
-        hipLaunchKernelGGL((llKernel<T, 0>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.ll);
+        launchLL<T, 0>(p);
       else
         hipLaunchKernelGGL((collKernel<T, 0, COLL_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;

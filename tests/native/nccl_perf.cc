@@ -4,7 +4,8 @@
 //
 //   nccl_perf [-d ndev] [-r ranks_per_dev] [-b min_bytes] [-e max_bytes] [-f factor] [-i iters] [-w warmup]
 //             [-o op: sum|max] [-t type: float|half|bf16|int] [-g 0|1 (replay a captured hipGraph)]
-//             [-c coll: ar|rs|ag]
+//             [-c coll: ar|rs|ag] [-H 0|1 (hold: a spin kernel occupies each stream while the timed
+//             collectives are issued, so host(us) is the pure issue cost; keep -i small, e.g. 100)]
 //
 // All ranks live in this process (ncclCommInitAll over ndev devices x ranks_per_dev; several ranks per
 // device need NCCL_MULTI_RANK_GPU_ENABLE=1). Each rank r fills its input with (r+1), so every element of
@@ -21,6 +22,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "nccl.h"
@@ -50,6 +52,10 @@ __global__ void fillKernel(void* p, size_t n, int type, float v) {
     else ((int*)p)[i] = (int)v;
   }
 }
+__global__ void spinKernel(long long cycles) {
+  long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < cycles) __builtin_amdgcn_s_sleep(10);
+}
 __global__ void checkKernel(const void* p, size_t n, int type, float want, size_t blk, unsigned long long* bad) {
   unsigned long long local = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
@@ -64,14 +70,14 @@ __global__ void checkKernel(const void* p, size_t n, int type, float want, size_
 }
 
 int main(int argc, char** argv) {
-  int ndevArg = 0, perDev = 1, iters = 20, warmup = 5, graph = 0;
+  int ndevArg = 0, perDev = 1, iters = 20, warmup = 5, graph = 0, hold = 0;
   size_t minB = 8, maxB = 64 << 20;
   double factor = 2;
   ncclRedOp_t op = ncclSum;
   ncclDataType_t type = ncclFloat32;
   char coll = 'a';  // a: AllReduce, r: ReduceScatter, g: AllGather
   int c;
-  while ((c = getopt(argc, argv, "d:r:b:e:f:i:w:o:t:g:c:")) != -1) {
+  while ((c = getopt(argc, argv, "d:r:b:e:f:i:w:o:t:g:c:H:")) != -1) {
     switch (c) {
       case 'd': ndevArg = atoi(optarg); break;
       case 'r': perDev = atoi(optarg); break;
@@ -81,6 +87,7 @@ int main(int argc, char** argv) {
       case 'i': iters = atoi(optarg); break;
       case 'w': warmup = atoi(optarg); break;
       case 'g': graph = atoi(optarg); break;
+      case 'H': hold = atoi(optarg); break;
       case 'c': coll = !strcmp(optarg, "rs") ? 'r' : !strcmp(optarg, "ag") ? 'g' : 'a'; break;
       case 'o': op = !strcmp(optarg, "max") ? ncclMax : ncclSum; break;
       case 't':
@@ -131,7 +138,7 @@ int main(int argc, char** argv) {
     if (coll == 'g') return ncclAllGather(send[r], recv[r], count / n, type, comms[r], streams[r]);
     return ncclAllReduce(send[r], recv[r], count, type, op, comms[r], streams[r]);
   };
-  printf("# %12s %12s %10s %10s %10s %8s\n", "bytes", "count", "time(us)", "algbw", "busbw", "#wrong");
+  printf("# %12s %12s %10s %10s %10s %8s %9s\n", "bytes", "count", "time(us)", "algbw", "busbw", "#wrong", "host(us)");
   const size_t step = coll == 'a' ? es : es * n;
   for (size_t bytes = minB; bytes <= maxB; bytes = std::max(bytes + step, (size_t)(bytes * factor))) {
     if (coll != 'a' && bytes % step) continue;
@@ -160,11 +167,16 @@ int main(int argc, char** argv) {
         execs.push_back(ex);
       }
     }
+    if (hold)  // ~20 ms on the 100 MHz wall clock: longer than issuing the timed loop
+      for (int r = 0; r < n; r++) hipLaunchKernelGGL(spinKernel, dim3(1), dim3(64), 0, streams[r], 2000000LL);
     for (int r = 0; r < n; r++) HIPCK(hipEventRecord(ev0[r], streams[r]));
+    double hostUs = 0;  // host time to issue one group of n collectives (eager only)
     if (graph) {
       for (int r = 0; r < n; r++) HIPCK(hipGraphLaunch(execs[r], streams[r]));
     } else {
+      auto h0 = std::chrono::steady_clock::now();
       enqueue(iters);
+      hostUs = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count() / iters;
     }
     for (int r = 0; r < n; r++) HIPCK(hipEventRecord(ev1[r], streams[r]));
     float ms = 0;
@@ -193,9 +205,8 @@ int main(int argc, char** argv) {
     }
     const double us = ms * 1e3 / iters;
     const double algbw = bytes / (us * 1e-6) / 1e9;
-    printf("  %12zu %12zu %10.2f %10.2f %10.2f %8llu\n", bytes, count, us, algbw,
-           algbw * (coll == 'a' ? 2.0 : 1.0) * (n - 1) / n,
-           (unsigned long long)*bad);
+    printf("  %12zu %12zu %10.2f %10.2f %10.2f %8llu %9.2f\n", bytes, count, us, algbw,
+           algbw * (coll == 'a' ? 2.0 : 1.0) * (n - 1) / n, (unsigned long long)*bad, hostUs);
     if (*bad) return 5;
   }
   for (int r = 0; r < n; r++) NCK(ncclCommDestroy(comms[r]));
