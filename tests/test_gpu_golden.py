@@ -1,0 +1,107 @@
+"""GPU parity against the committed golden fixtures (tests/golden/*.npz, made by make_golden.py from an
+independent numpy restatement of the reference's fold order and arithmetic): every fixture runs through
+the C ABI with its own rank count — one process per rank, all on the box's one GPU, HIP IPC between
+them — under the default size table and with each protocol forced (LL, one-shot, direct), and every
+rank's output must match the fixture bit for bit."""
+import glob
+import multiprocessing as mp
+import os
+import queue
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
+# protocol settings, each its own communicator (tuning knobs are read at init)
+SETTINGS = [{}, {"NCCL_PROTO": "LL"}, {"NCCL_PROTO": "^LL", "NCCL_ALGO": "ONESHOT"},
+            {"NCCL_PROTO": "^LL", "NCCL_ALGO": "DIRECT"}]
+KNOBS = ("NCCL_PROTO", "NCCL_ALGO")
+
+
+def _fixtures(n):
+    out = []
+    for f in FIXTURES:
+        z = np.load(f)  # plain arrays only (allow_pickle stays False)
+        if int(z["n"]) == n:
+            out.append((os.path.basename(f), {k: z[k] for k in z.files}))
+    return out
+
+
+def _worker(rank, n, uids, q):
+    try:
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "30000"
+        import torch
+        import nccl_amd
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        errs = []
+        for setting, uid in zip(SETTINGS, uids):
+            for k in KNOBS:
+                os.environ.pop(k, None)
+            os.environ.update(setting)
+            comm = nccl_amd.Communicator.init(n, rank, uid)
+            s = torch.cuda.Stream()
+            for name, z in _fixtures(n):
+                coll, dtype, op = str(z["coll"]), int(z["dtype"]), int(z["op"])
+                root = int(z["root"]) if "root" in z else 0
+                x = z[f"in{rank}"]
+                want = z[f"out{rank}"] if coll == "reducescatter" else z["out"]
+                keep_in, sv = G.to_device(x, dev)
+                rv = None
+                if coll != "reduce" or rank == root:
+                    keep_out, rv = G.to_device(np.zeros_like(want), dev)
+                torch.cuda.synchronize()
+                G.launch(comm, coll, sv, rv, x.size, dtype, op, root, s.cuda_stream)
+                s.synchronize()
+                ae = comm.async_error()
+                if ae:
+                    errs.append(f"rank {rank} {setting} {name}: async error {ae}")
+                    break
+                if rv is None:
+                    continue
+                got = G.from_device(rv, want.dtype)
+                if not G.same_bits(got, want, dtype):
+                    bad = np.nonzero(got != want)[0]
+                    errs.append(f"rank {rank} {setting} {name}: {bad.size} mismatches, first at {bad[:5].tolist()}")
+            comm.destroy()
+            if errs:
+                break
+        q.put((rank, errs))
+    except Exception as e:  # report instead of hanging the parent
+        q.put((rank, [f"rank {rank} exception: {e!r}"]))
+
+
+@pytest.mark.parametrize("n", sorted({int(np.load(f)["n"]) for f in FIXTURES}))
+def test_golden_fixtures(built, n):
+    import torch
+    assert torch.cuda.is_available(), "GPU test on a box without a GPU"
+    import nccl_amd
+    uids = [nccl_amd.get_unique_id() for _ in SETTINGS]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, n, uids, q)) for r in range(n)]
+    for p in ps:
+        p.start()
+    results, t0 = {}, time.time()
+    while len(results) < n and time.time() - t0 < 600:
+        try:
+            r, errs = q.get(timeout=30)
+            results[r] = errs
+        except queue.Empty:
+            alive = sum(p.is_alive() for p in ps)
+            print(f"[golden n={n}] waiting: {len(results)} done, {alive} alive, {time.time() - t0:.0f}s", flush=True)
+            if alive == 0:
+                break
+    for p in ps:
+        if p.is_alive() and len(results) < n:
+            p.kill()
+    for p in ps:
+        p.join(timeout=60)
+    assert len(results) == n, f"only {len(results)} of {n} ranks reported"
+    bad = [e for r in sorted(results) for e in results[r]]
+    assert not bad, "\n".join(bad[:20])
