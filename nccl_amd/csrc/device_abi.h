@@ -83,7 +83,7 @@ struct CollArgs {
 // LL AllReduce batch: up to kMaxLLBatch small AllReduce ops of one group (same comm, stream, type and
 // op) run by ONE launch (reference: ops of a group aggregated into one kernel plan, enqueue.cc:405-470).
 constexpr int kMaxLLBatch = 32;
-enum LLColl { LL_AR = 0, LL_RS = 1, LL_AG = 2 };
+enum LLColl { LL_AR = 0, LL_RS = 1, LL_AG = 2, LL_REDUCE = 3 };
 struct LLOp {
   const void* send;
   void* recv;
@@ -93,7 +93,7 @@ struct LLOp {
   int nch;         // channels this op uses
   int chOff;       // first channel (batches spread their ops over the LL channels)
   int coll;        // LLColl
-  int pad;
+  int root;        // LL_REDUCE: the rank that folds and stores (the others send and poll only)
 };
 // The kernel arguments hold room for K ops: a lone op launches with K = 1 (88 bytes of kernel arguments
 // instead of 1.8 KiB; the host issue cost of a launch grows with its argument bytes, about 3 us at 64 B

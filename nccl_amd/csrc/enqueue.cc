@@ -189,20 +189,21 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
   p.args.nSteps = (int)((part + slice - 1) / slice);
 }
 
-// LL eligibility and channel plan of one AllReduce, ReduceScatter or AllGather (reference tuning: LL for
+// LL eligibility and channel plan of one AllReduce, ReduceScatter, AllGather or Reduce (reference tuning: LL for
 // the smallest sizes, or as NCCL_PROTO dictates). Needs 8-byte aligned buffers (and, for the blocked
 // collectives, 8-byte aligned rank blocks) and room in the comm's line area. The payload space is the
-// AllReduce buffer or one ReduceScatter / AllGather rank block; the size limit applies to it.
+// AllReduce / Reduce buffer or one ReduceScatter / AllGather rank block; the size limit applies to it.
 bool llPlan(const CollInfo& info, LLOp* op) {
   ncclComm* comm = info.comm;
-  if (info.func == FUNC_REDUCE || comm->nRanks == 1) return false;
+  if (comm->nRanks == 1) return false;
   const int n = comm->nRanks;
   const int ts = typeSize(info.datatype);
   const size_t bytes = info.count * (size_t)ts;  // payload space
   const size_t npk = (bytes + 7) / 8;
   const CommTuning& t = comm->tune;
   bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
-  if (info.func != FUNC_ALLREDUCE) al8 = al8 && (bytes & 7) == 0;
+  const bool blocked = info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER;
+  if (blocked) al8 = al8 && (bytes & 7) == 0;
   const bool fits = t.llOn && al8 && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
   // NCCL_PROTO leaves only LL enabled.
@@ -213,7 +214,7 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   bool useLL = fits && (!t.simpleOn || (t.algo == 0 && bytes <= llLim));
   int tuned = TUNE_DEFAULT, tunedNch = 0;
   if (comm->tunerLoaded) {  // an external tuner plugin may overrule the size table (tuner.cc)
-    tunerPick(comm, info.func, info.func == FUNC_ALLREDUCE ? bytes : bytes * n, 1, fits, &tuned, &tunedNch);
+    tunerPick(comm, info.func, blocked ? bytes * n : bytes, 1, fits, &tuned, &tunedNch);
     if (tuned != TUNE_DEFAULT) useLL = fits && tuned == TUNE_LL;
   }
   if (!useLL) return false;
@@ -238,8 +239,9 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   op->part = part;
   op->nch = nch;
   op->chOff = 0;
-  op->coll = info.func == FUNC_ALLREDUCE ? LL_AR : info.func == FUNC_REDUCESCATTER ? LL_RS : LL_AG;
-  op->pad = 0;
+  op->coll = info.func == FUNC_ALLREDUCE ? LL_AR : info.func == FUNC_REDUCESCATTER ? LL_RS
+           : info.func == FUNC_ALLGATHER ? LL_AG : LL_REDUCE;
+  op->root = info.root;
   return true;
 }
 
@@ -367,8 +369,8 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     if (tuned == TUNE_DIRECT) oneShot = false;
   }
   const bool oneShotAR = oneShot;
-  // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce / ReduceScatter / AllGather,
-  // one launch, no fences
+  // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce / ReduceScatter / AllGather /
+  // Reduce, one launch, no fences
   if (llPlan(info, &p.ll.ops[0])) {
     p.algo = ALGO_LL;
     p.ll.comm = comm->devComm;

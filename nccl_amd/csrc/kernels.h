@@ -683,8 +683,13 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
       }
       continue;
     }
+    // Reduce: every rank sends to and polls every peer (that keeps the parity double-buffering safe, as
+    // for AllReduce), only the root folds, in its ring order root+1, ..., root (reference reduce.h)
+    if (op.coll == LL_REDUCE && me != op.root) continue;
     // pass 2: fold in the owner block's ring order (the lines stay valid until epoch + 2)
-    const int owner = op.coll == LL_RS ? me : (int)((pk * 8 / sizeof(T)) / op.chunk);  // never straddles
+    const int owner = op.coll == LL_RS ? me
+                    : op.coll == LL_REDUCE ? op.root
+                    : (int)((pk * 8 / sizeof(T)) / op.chunk);  // an AllReduce payload never straddles blocks
     const char* mine = op.coll == LL_RS ? send + (uint64_t)me * nbytes : send;
     union { uint64_t u; T e[EPP]; } acc, x;
     for (int k = 0; k < n; k++) {
@@ -958,7 +963,10 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
         hipLaunchKernelGGL((collKernel<T, OP, COLL_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
     case FUNC_REDUCE:
-      hipLaunchKernelGGL((collKernel<T, OP, COLL_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_LL)
+        launchLL<T, OP>(p);
+      else
+        hipLaunchKernelGGL((collKernel<T, OP, COLL_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
       break;
     case FUNC_ALLGATHER:
       if (p.algo == ALGO_LL)

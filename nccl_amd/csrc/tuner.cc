@@ -151,7 +151,9 @@ void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, bool
   } else {
     f = func == FUNC_REDUCESCATTER ? ncclFuncReduceScatter : func == FUNC_ALLGATHER ? ncclFuncAllGather : ncclFuncReduce;
     table[NCCL_ALGO_RING][NCCL_PROTO_SIMPLE] = (float)(10.0 + (n - 1.0) / n * bytes * usPerByte);
-    if (llOk && func != FUNC_REDUCE) table[NCCL_ALGO_RING][NCCL_PROTO_LL] = (float)(4.0 + 2.0 * (n - 1.0) / n * bytes * usPerByte);
+    if (llOk)  // Reduce's LL lines go to every peer, like AllReduce's
+      table[NCCL_ALGO_RING][NCCL_PROTO_LL] =
+          (float)(4.0 + (func == FUNC_REDUCE ? 2.0 * (n - 1) : 2.0 * (n - 1.0) / n) * bytes * usPerByte);
   }
   float before[NCCL_NUM_ALGORITHMS][NCCL_NUM_PROTOCOLS];
   memcpy(before, table, sizeof(table));

@@ -12,3 +12,7 @@ for c in rs ag; do
   exit 1
 done
 for f in gpurun_out/native_{rs,ag}_*.txt; do echo "== $f"; cat $f; done
+# Reduce (root 0): LL vs SIMPLE direct
+timeout -k 10 120 ./tests/native/nccl_perf -r 2 -c reduce -b 64 -e 1048576 -f 4 -i 200 -w 20 > gpurun_out/native_reduce_ll.txt 2>&1 &&
+NCCL_PROTO=^LL timeout -k 10 120 ./tests/native/nccl_perf -r 2 -c reduce -b 64 -e 1048576 -f 4 -i 200 -w 20 > gpurun_out/native_reduce_simple.txt 2>&1 &&
+cat gpurun_out/native_reduce_ll.txt gpurun_out/native_reduce_simple.txt

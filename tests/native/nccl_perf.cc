@@ -4,14 +4,14 @@
 //
 //   nccl_perf [-d ndev] [-r ranks_per_dev] [-b min_bytes] [-e max_bytes] [-f factor] [-i iters] [-w warmup]
 //             [-o op: sum|max] [-t type: float|half|bf16|int] [-g 0|1 (replay a captured hipGraph)]
-//             [-c coll: ar|rs|ag] [-H 0|1 (hold: a spin kernel occupies each stream while the timed
+//             [-c coll: ar|rs|ag|reduce (root 0)] [-H 0|1 (hold: a spin kernel occupies each stream while the timed
 //             collectives are issued, so host(us) is the pure issue cost; keep -i small, e.g. 100)]
 //
 // All ranks live in this process (ncclCommInitAll over ndev devices x ranks_per_dev; several ranks per
 // device need NCCL_MULTI_RANK_GPU_ENABLE=1). Each rank r fills its input with (r+1), so every element of
 // an AllReduce / ReduceScatter sum must be n(n+1)/2 (max: n) and AllGather block q must be q+1; the
 // "#wrong" column counts mismatching elements. bytes = the AllReduce buffer, the ReduceScatter input or
-// the AllGather output (nccl-tests convention). busBW = algBW * 2(n-1)/n for AllReduce, (n-1)/n for the
+// the AllGather output (nccl-tests convention). busBW = algBW * 2(n-1)/n for AllReduce, 1 for Reduce, (n-1)/n for the
 // others (reference plugins/profiler/inspector/inspector.cc:1450-1492).
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
@@ -88,7 +88,7 @@ int main(int argc, char** argv) {
       case 'w': warmup = atoi(optarg); break;
       case 'g': graph = atoi(optarg); break;
       case 'H': hold = atoi(optarg); break;
-      case 'c': coll = !strcmp(optarg, "rs") ? 'r' : !strcmp(optarg, "ag") ? 'g' : 'a'; break;
+      case 'c': coll = !strcmp(optarg, "rs") ? 'r' : !strcmp(optarg, "ag") ? 'g' : !strcmp(optarg, "reduce") ? 'd' : 'a'; break;
       case 'o': op = !strcmp(optarg, "max") ? ncclMax : ncclSum; break;
       case 't':
         type = !strcmp(optarg, "half") ? ncclFloat16 : !strcmp(optarg, "bf16") ? ncclBfloat16
@@ -131,17 +131,19 @@ int main(int argc, char** argv) {
   for (int r = 0; r < n; r++) HIPCK(hipStreamSynchronize(streams[r]));
   const float want = op == ncclSum ? n * (n + 1) / 2.0f : (float)n;
   printf("# nccl_perf: libnccl %d, %s, %d ranks (%d devices x %d), type %d, op %s, %s\n", version,
-         coll == 'r' ? "ReduceScatter" : coll == 'g' ? "AllGather" : "AllReduce", n, ndev, perDev, (int)type,
+         coll == 'r' ? "ReduceScatter" : coll == 'g' ? "AllGather" : coll == 'd' ? "Reduce (root 0)" : "AllReduce", n, ndev,
+         perDev, (int)type,
          op == ncclSum ? "sum" : "max", graph ? "hipGraph replay" : "eager launches");
   auto issue = [&](int r, size_t count) {
     if (coll == 'r') return ncclReduceScatter(send[r], recv[r], count / n, type, op, comms[r], streams[r]);
     if (coll == 'g') return ncclAllGather(send[r], recv[r], count / n, type, comms[r], streams[r]);
+    if (coll == 'd') return ncclReduce(send[r], recv[r], count, type, op, 0, comms[r], streams[r]);
     return ncclAllReduce(send[r], recv[r], count, type, op, comms[r], streams[r]);
   };
   printf("# %12s %12s %10s %10s %10s %8s %9s\n", "bytes", "count", "time(us)", "algbw", "busbw", "#wrong", "host(us)");
-  const size_t step = coll == 'a' ? es : es * n;
+  const size_t step = coll == 'a' || coll == 'd' ? es : es * n;
   for (size_t bytes = minB; bytes <= maxB; bytes = std::max(bytes + step, (size_t)(bytes * factor))) {
-    if (coll != 'a' && bytes % step) continue;
+    if (bytes % step) continue;
     const size_t count = bytes / es;  // elements of the AllReduce buffer / RS input / AG output
     auto enqueue = [&](int iters_) {
       for (int k = 0; k < iters_; k++) {
@@ -188,7 +190,7 @@ int main(int argc, char** argv) {
     }
     for (hipGraphExec_t ex : execs) HIPCK(hipGraphExecDestroy(ex));
     *bad = 0;
-    for (int r = 0; r < n; r++) {
+    for (int r = 0; r < (coll == 'd' ? 1 : n); r++) {  // Reduce: only the root's output is defined
       HIPCK(hipSetDevice(devs[r]));
       const size_t outCount = coll == 'r' ? count / n : count;
       hipLaunchKernelGGL(checkKernel, dim3(256), dim3(256), 0, streams[r], recv[r], outCount, (int)type, want,
@@ -206,7 +208,7 @@ int main(int argc, char** argv) {
     const double us = ms * 1e3 / iters;
     const double algbw = bytes / (us * 1e-6) / 1e9;
     printf("  %12zu %12zu %10.2f %10.2f %10.2f %8llu %9.2f\n", bytes, count, us, algbw,
-           algbw * (coll == 'a' ? 2.0 : 1.0) * (n - 1) / n, (unsigned long long)*bad, hostUs);
+           coll == 'd' ? algbw : algbw * (coll == 'a' ? 2.0 : 1.0) * (n - 1) / n, (unsigned long long)*bad, hostUs);
     if (*bad) return 5;
   }
   for (int r = 0; r < n; r++) NCK(ncclCommDestroy(comms[r]));

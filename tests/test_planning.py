@@ -63,9 +63,15 @@ def test_ll_needs_8_byte_alignment_and_room(exe):
     assert plan(exe, 2, "ar", 7, (1 << 20) // 4, NCCL_PROTO="LL,Simple", NCCL_AMD_LL_BYTES=4 << 20)["algo"] == "oneshot"
 
 
-def test_reduce_always_direct(exe):
-    for count in (1, 1000, 1 << 20):
-        assert plan(exe, 8, "reduce", 9, count)["algo"] == "direct"
+def test_reduce_size_table(exe):
+    # LL (lines to every peer, the root folds) up to the AllReduce LL limit, direct above; no one-shot
+    assert plan(exe, 8, "reduce", 9, 1)["algo"] == "ll"
+    assert plan(exe, 8, "reduce", 9, 1000)["algo"] == "ll"
+    assert plan(exe, 2, "reduce", 7, (128 << 10) // 4)["algo"] == "ll"
+    assert plan(exe, 2, "reduce", 7, (128 << 10) // 4 + 1)["algo"] == "direct"
+    assert plan(exe, 8, "reduce", 9, 1 << 20)["algo"] == "direct"
+    assert plan(exe, 8, "reduce", 9, 1000, NCCL_PROTO="^LL")["algo"] == "direct"
+    assert plan(exe, 8, "reduce", 7, 1001, offset=4)["algo"] == "direct"
 
 
 @pytest.mark.parametrize("func", ["rs", "ag"])
@@ -88,12 +94,12 @@ def test_blocked_collectives_size_table(exe, func):
 def test_rootless_reduce_blocks(exe):
     # n >= 3: n-1 blocks (root owns none), each alignUp(divUp(count, n-1), 16/sizeof(T)) elements
     for n, count in ((3, 1), (4, 999_999), (8, 33_554_432)):
-        p = plan(exe, n, "reduce", 2, count)
+        p = plan(exe, n, "reduce", 2, count, NCCL_PROTO="^LL")
         epp = 16 // 4
         want = -(-count // (n - 1))
         want = -(-want // epp) * epp
         assert p["chunk"] == want, (n, count, p)
-    p = plan(exe, 2, "reduce", 2, 1000)  # n = 2 keeps one block per rank
+    p = plan(exe, 2, "reduce", 2, 1000, NCCL_PROTO="^LL")  # n = 2 keeps one block per rank
     assert p["chunk"] == 500
 
 
