@@ -1,6 +1,6 @@
 """The C ABI driven from native code: tests/native/nccl_perf (nccl-tests style, built by `make nccl-perf`
-against include/nccl.h only) runs AllReduce sum/max over fp32/bf16 with 2 ranks on the one GPU, eager and
-hipGraph-replayed, and fails on any wrong element or async error."""
+against include/nccl.h only) runs AllReduce sum/max over fp32/bf16 (plus ReduceScatter, AllGather and Reduce) with 2 ranks on the one
+GPU, eager, hipGraph-replayed and in hold mode, and fails on any wrong element or async error."""
 import os
 import subprocess
 
@@ -16,6 +16,10 @@ EXE = os.path.join(ROOT, "tests", "native", "nccl_perf")
     (["-b", "8", "-e", "1048576", "-f", "32", "-i", "5", "-g", "1"], "0"),
     (["-b", "4", "-e", "4194304", "-f", "64", "-i", "3", "-t", "bf16", "-o", "max"], "0"),
     (["-b", "1024", "-e", "1048576", "-f", "32", "-i", "3"], "1"),
+    (["-c", "rs", "-b", "64", "-e", "4194304", "-f", "16", "-i", "5"], "0"),
+    (["-c", "ag", "-b", "64", "-e", "4194304", "-f", "16", "-i", "5", "-t", "half"], "0"),
+    (["-c", "reduce", "-b", "8", "-e", "4194304", "-f", "16", "-i", "5", "-t", "int", "-o", "max"], "0"),
+    (["-b", "8", "-e", "262144", "-f", "8", "-i", "20", "-H", "1"], "0"),
 ])
 def test_native_driver(built, args, forkjoin):
     if not os.path.exists(EXE):
@@ -25,4 +29,4 @@ def test_native_driver(built, args, forkjoin):
     out = subprocess.run([EXE, "-r", "2"] + args, env=env, capture_output=True, text=True, timeout=200)
     assert out.returncode == 0, out.stdout + out.stderr
     rows = [l.split() for l in out.stdout.splitlines() if l.strip() and not l.startswith("#")]
-    assert rows and all(r[-1] == "0" for r in rows), out.stdout
+    assert rows and all(r[5] == "0" for r in rows), out.stdout  # columns: bytes count time algbw busbw #wrong host
