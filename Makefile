@@ -28,9 +28,12 @@ $(BUILD)/%.o: $(SRCDIR)/%.cc $(HDRS)
 	@mkdir -p $(BUILD)
 	$(CXX) $(COMMON) -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -c $< -o $@
 
+# The kernels' register / scratch / occupancy report goes to build/<name>.usage
+# (tests/test_occupancy.py checks that every channel kernel fits two workgroups per CU).
 $(BUILD)/%.o: $(SRCDIR)/%.hip $(HDRS)
 	@mkdir -p $(BUILD)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $(BUILD)/$*.usage; \
+	  st=$$?; grep -E "warning|error" $(BUILD)/$*.usage >&2; exit $$st
 
 $(LIBDIR)/libnccl.so: $(HOSTOBJ) $(DEVOBJ)
 	@mkdir -p $(LIBDIR)

@@ -38,6 +38,11 @@ namespace ncclamd {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kThreads = 512;  // 8 waves of 64 per channel workgroup
+// Several ranks on one GPU (NCCL_MULTI_RANK_GPU_ENABLE) need every channel of every rank resident at
+// once: the host caps channels at 2 workgroups per CU (chanCap), so each channel kernel must fit two
+// 512-thread workgroups per CU = 4 waves per SIMD, i.e. at most 128 VGPRs. The attribute makes the
+// compiler hold that budget (tests/test_occupancy.py checks the build's resource report).
+#define kCoResident __attribute__((amdgpu_waves_per_eu(4)))
 
 // ------------------------------------------------------------------------------------ primitives
 
@@ -207,7 +212,9 @@ template <typename T, int OP>
 __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const char* const* src, uint64_t nelem,
                                           char* dstLocal, char* const* dstPush, int nPush, bool aligned) {
   constexpr int EPP = 16 / sizeof(T);
-  constexpr int U = 4;
+  // 1-byte types unpack 16 elements per pack into separate registers: one pack per batch keeps the kernel
+  // within its register budget (kWavesPerEU)
+  constexpr int U = sizeof(T) == 1 ? 1 : 4;
   if (aligned) {
     const uint64_t npk = nelem / EPP;
     for (uint64_t base = threadIdx.x; base < npk; base += (uint64_t)U * kThreads) {
@@ -527,7 +534,7 @@ struct Channel {
 };
 
 template <typename T, int OP, int COLL>
-__global__ void __launch_bounds__(kThreads) collKernel(CollArgs a) {
+__global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
   __shared__ Shared sh;
   const DevComm& dc = *a.comm;
   const int tid = threadIdx.x;
@@ -719,7 +726,7 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
 // round trip for the batch). A channel runs its ops in batch order and its epoch advances once per op
 // it takes part in; all ranks build the same batch, so epochs agree.
 template <typename T, int OP, int K>
-__global__ void __launch_bounds__(kThreads) llKernel(LLArgs<K> a) {
+__global__ void __launch_bounds__(kThreads) kCoResident llKernel(LLArgs<K> a) {
   __shared__ int abortSh;
   const DevComm& dc = *a.comm;
   const int c = blockIdx.x;
@@ -790,7 +797,7 @@ __device__ __forceinline__ bool symWait(const DevComm& dc, SymShared& sh, int c,
 }
 
 template <typename T, int OP, int COLL>
-__global__ void __launch_bounds__(kThreads) symKernel(SymArgs a) {
+__global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
   __shared__ SymShared sh;
   const DevComm& dc = *a.comm;
   const int tid = threadIdx.x, c = blockIdx.x, me = dc.rank, n = dc.nRanks;

@@ -240,3 +240,83 @@ def test_ll_reducescatter_allgather(built, nranks):
     for c in comms:
         c.destroy()
     assert not errs, "\n".join(errs[:20])
+
+
+def test_counts_above_int32(built):
+    """Maximum-size edge: element counts past 2^31 (uint8, so 2 GiB+ buffers) through the one-rank copy and
+    the two-rank staged AllReduce, ReduceScatter and AllGather, checked elementwise on the device against
+    the modular sums of two closed-form inputs (size-independent property: (a + b) mod 256)."""
+    torch = _torch()
+    import nccl_amd
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    big = (1 << 31) + 4099
+    idx = torch.arange(big, device="cuda", dtype=torch.int64)
+    xs = [(idx % 251).to(torch.uint8), ((idx * 7 + 3) % 253).to(torch.uint8)]
+    want = ((xs[0].to(torch.int16) + xs[1].to(torch.int16)) % 256).to(torch.uint8)
+    del idx
+    # one rank: the copy kernel
+    c1 = nccl_amd.Communicator.init_all([0])[0]
+    y = torch.empty_like(xs[0])
+    s = torch.cuda.Stream()
+    c1.all_reduce_raw(xs[0].data_ptr(), y.data_ptr(), big, 1, 0, s.cuda_stream)
+    s.synchronize()
+    assert c1.async_error() == 0 and torch.equal(y, xs[0])
+    c1.destroy()
+    del y
+    comms = nccl_amd.Communicator.init_all([0, 0])
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    # AllReduce
+    ys = [torch.empty_like(x) for x in xs]
+    with nccl_amd.group():
+        for c, st, x, yy in zip(comms, streams, xs, ys):
+            c.all_reduce_raw(x.data_ptr(), yy.data_ptr(), big, 1, 0, st.cuda_stream)
+    torch.cuda.synchronize()
+    for c, yy in zip(comms, ys):
+        assert c.async_error() == 0 and torch.equal(yy, want)
+    del ys
+    # ReduceScatter: recvcount = big // 2 per rank (input big - big % 2 elements)
+    rc = big // 2
+    outs = [torch.empty(rc, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    with nccl_amd.group():
+        for c, st, x, o in zip(comms, streams, xs, outs):
+            c.reduce_scatter_raw(x.data_ptr(), o.data_ptr(), rc, 1, 0, st.cuda_stream)
+    torch.cuda.synchronize()
+    for r, o in enumerate(outs):
+        assert comms[r].async_error() == 0 and torch.equal(o, want[r * rc:(r + 1) * rc])
+    del outs
+    # AllGather: sendcount = big // 2 + 1 per rank, output past 2^31
+    sc = big // 2 + 1
+    full = [torch.empty(2 * sc, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    with nccl_amd.group():
+        for c, st, x, f in zip(comms, streams, xs, full):
+            c.all_gather_raw(x.data_ptr(), f.data_ptr(), sc, 1, st.cuda_stream)
+    torch.cuda.synchronize()
+    for r, f in enumerate(full):
+        assert comms[r].async_error() == 0
+        assert torch.equal(f[:sc], xs[0][:sc]) and torch.equal(f[sc:], xs[1][:sc])
+    for c in comms:
+        c.destroy()
+
+
+def test_one_byte_types_full_channel_plans(built):
+    """1-byte types at sizes that plan the full 256 channels, 2 ranks in one process: every channel of
+    both ranks must be resident at once (kernel register budget, tests/test_occupancy.py) — before that
+    budget the uint8 / fp8 kernels fit one workgroup per CU and these cases waited forever."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0])
+    streams = [torch.cuda.Stream() for _ in range(2)]
+    cs = list(zip(comms, streams))
+    errs = []
+    for i, (coll, dt, op) in enumerate([("allreduce", 1, 0), ("allreduce", 0, 3), ("allreduce", 10, 0),
+                                        ("allreduce", 11, 2), ("reducescatter", 1, 0), ("reduce", 10, 0)]):
+        errs += G.run_case(cs, coll, dt, op, (64 << 20) + 6, 0, seed=700 + i)
+        if errs:
+            break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
