@@ -141,6 +141,62 @@ def test_hipgraph_capture_and_replay(two_comms):
             assert np.array_equal(y[r].cpu().numpy(), want), f"replay {it} rank {r}"
 
 
+def test_hipgraph_mixed_sequence(two_comms):
+    """One captured graph per rank holding a sequence that crosses every protocol — LL AllReduce,
+    ReduceScatter, AllGather and Reduce, a one-shot and a direct AllReduce, a direct ReduceScatter —
+    replayed with fresh inputs: every epoch, credit and LL flag lives in device memory, so each replay must
+    continue the counters where the previous one left them (fp32 sums, bit-exact vs the oracle)."""
+    import torch
+    import nccl_amd
+    import oracle
+    comms, _ = two_comms
+    streams = [nccl_amd.dedicated_stream(0), nccl_amd.dedicated_stream(0)]
+    # (collective, input count per rank)
+    seq = [("allreduce", 1000), ("reducescatter", 2 * 1024), ("allgather", 1536), ("reduce", 3000),
+           ("allreduce", 100_000), ("allreduce", 1 << 20), ("reducescatter", 2 * (1 << 19))]
+    outc = {"allreduce": lambda c: c, "reducescatter": lambda c: c // 2, "allgather": lambda c: 2 * c,
+            "reduce": lambda c: c}
+    xs = [[torch.empty(c, device="cuda") for _, c in seq] for _ in range(2)]
+    ys = [[torch.empty(outc[k](c), device="cuda") for k, c in seq] for _ in range(2)]
+    graphs = [torch.cuda.CUDAGraph() for _ in range(2)]
+    torch.cuda.synchronize()
+    for r in range(2):
+        with torch.cuda.graph(graphs[r], stream=streams[r]):
+            sp = streams[r].cuda_stream
+            for (k, c), x, y in zip(seq, xs[r], ys[r]):
+                if k == "allreduce":
+                    comms[r].all_reduce_raw(x.data_ptr(), y.data_ptr(), c, 7, 0, sp)
+                elif k == "reducescatter":
+                    comms[r].reduce_scatter_raw(x.data_ptr(), y.data_ptr(), c // 2, 7, 0, sp)
+                elif k == "allgather":
+                    comms[r].all_gather_raw(x.data_ptr(), y.data_ptr(), c, 7, sp)
+                else:
+                    comms[r].reduce_raw(x.data_ptr(), y.data_ptr(), c, 7, 0, 1, sp)
+    for it in range(4):
+        ins = [_inputs(2, c, seed=300 + 10 * it + j) for j, (_, c) in enumerate(seq)]
+        for r in range(2):
+            for j in range(len(seq)):
+                xs[r][j].copy_(torch.from_numpy(ins[j][r]))
+        torch.cuda.synchronize()
+        for r in range(2):
+            with torch.cuda.stream(streams[r]):
+                graphs[r].replay()
+        torch.cuda.synchronize()
+        assert all(c.async_error() == 0 for c in comms)
+        for j, (k, c) in enumerate(seq):
+            if k == "allreduce":
+                want = [oracle.all_reduce(ins[j], 7, 0)] * 2
+            elif k == "reducescatter":
+                want = oracle.reduce_scatter(ins[j], 7, 0)
+            elif k == "allgather":
+                want = [oracle.all_gather(ins[j])] * 2
+            else:
+                want = [None, oracle.reduce(ins[j], 7, 0, 1)]
+            for r in range(2):
+                if want[r] is not None:
+                    assert np.array_equal(ys[r][j].cpu().numpy(), want[r]), f"replay {it} op {j} ({k}) rank {r}"
+
+
 def test_init_rank_in_group_single_thread(built):
     import torch
     import nccl_amd
