@@ -106,14 +106,14 @@ def _time_ms(fn, stream, iters: int, warmup: int = 3) -> float:
     return a.elapsed_time(b) / iters
 
 
-def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dict:
+def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: dict | None = None) -> dict:
     """The other BASELINE.json configs at this N (the driver runs bench.py on the 8-GPU node, so this is
     where they get measured): RS+AG bf16 1 GiB bucket (configs[2]), AllReduce fp16 8 B..256 MiB sweep,
     one-shot vs direct (configs[3]), Reduce int32 min/max 128 MiB root 0 (configs[4]); each with a
     size-independent exactness check, plus xGMI peer-copy probes for the roofline denominator."""
     import torch
     import nccl_amd
-    out = {}
+    out = {} if out is None else out  # filled as it goes: a watchdog can report the finished parts
     sp = stream.cuda_stream
 
     def agree(ok: bool) -> bool:
@@ -271,9 +271,11 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False) -> dic
     tuning = []
     knobs = ("NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_MIN_CHANNEL_BYTES")
     saved = {k: os.environ.get(k) for k in knobs}
-    for env in ({}, {"NCCL_AMD_SLOT_BYTES": "65536"}, {"NCCL_AMD_SLOT_BYTES": "262144"},
-                {"NCCL_AMD_SLOT_BYTES": "524288"}, {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_MAX_CTAS": "128"},
-                {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}):
+    # (the staging slab is capped at 1 GiB per rank, so slot sizes scale with channels x slots x n:
+    #  default 128 KiB slots at n = 8, 256 KiB with 128 channels)
+    for env in ({}, {"NCCL_AMD_SLOT_BYTES": "32768"}, {"NCCL_AMD_SLOT_BYTES": "65536"},
+                {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_AMD_NSLOTS": "4"}, {"NCCL_MAX_CTAS": "128"},
+                {"NCCL_MAX_CTAS": "64"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}):
         for k in knobs:
             os.environ.pop(k, None)
         os.environ.update(env)
@@ -383,6 +385,9 @@ def load_pmc(workload_key: str):
 
 def main(argv=None):
     args = parse(argv)
+    if os.environ.get("BENCH_STACKS_AFTER_S"):  # diagnostics: dump every thread's stack if the run stalls
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["BENCH_STACKS_AFTER_S"]), repeat=True)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -495,14 +500,6 @@ def main(argv=None):
         except Exception as e:  # secondary measurement
             extra["host_staged"] = {"error": repr(e)}
 
-    if n > 1 and not args.no_suite:
-        try:
-            extra["suite"] = run_suite(comm, n, rank, dist, stream, quick=args.quick_suite)
-        except Exception as e:  # secondary measurements never fail the headline line
-            extra["suite"] = {"error": repr(e)}
-        torch.cuda.synchronize()
-        barrier()
-
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         try:
@@ -511,8 +508,8 @@ def main(argv=None):
             cpu = {"value": None, "error": repr(e)}
     barrier()
 
-    if rank == 0:
-        line = {
+    def headline():
+        return {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": n, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -523,7 +520,42 @@ def main(argv=None):
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             "roofline": roof, "cpu_baseline": cpu, "check": "pass" if ok else "FAIL", **extra,
         }
-        print(json.dumps(line), flush=True)
+
+    if n > 1 and not args.no_suite:
+        # The suite (secondary measurements) runs under a watchdog: if any part of it stalls, every rank
+        # still ends and rank 0 still prints the headline line, with the parts that finished.
+        import threading
+        suite = {}
+        extra["suite"] = suite
+        done = threading.Event()
+        limit = float(os.environ.get("BENCH_SUITE_TIMEOUT_S", "300"))
+        t_suite = time.perf_counter()
+
+        def watchdog():
+            if done.wait(limit):
+                return
+            if rank == 0:
+                extra["suite"] = dict(suite, error=f"suite stopped by the {limit:.0f} s watchdog; finished parts kept")
+                try:
+                    text = json.dumps(headline())
+                except Exception:  # a part was being written at that instant: report the headline alone
+                    extra["suite"] = {"error": f"suite stopped by the {limit:.0f} s watchdog"}
+                    text = json.dumps(headline())
+                print(text, flush=True)
+            os._exit(0 if ok else 1)
+
+        threading.Thread(target=watchdog, daemon=True).start()
+        try:
+            run_suite(comm, n, rank, dist, stream, quick=args.quick_suite, out=suite)
+        except Exception as e:  # secondary measurements never fail the headline line
+            suite["error"] = repr(e)
+        torch.cuda.synchronize()
+        barrier()
+        done.set()
+        suite["seconds"] = round(time.perf_counter() - t_suite, 1)
+
+    if rank == 0:
+        print(json.dumps(headline()), flush=True)
     comm.destroy()
     if dist is not None:
         dist.destroy_process_group()

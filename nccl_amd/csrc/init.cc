@@ -44,6 +44,22 @@ static uint64_t hostHash() {
   return h;
 }
 
+// Hard cap on one rank's staging slab (one IPC-exported allocation): on this platform (ROCm 7.2, dmabuf
+// IPC) importing a peer's 2 GiB uncached slab blocked hipIpcOpenMemHandle forever in multi-process runs
+// (4 ranks, 512 KiB slots; 1 GiB slabs never did), so slot-size overrides that would exceed 1 GiB are
+// scaled down instead.
+// Every rank adopts rank 0's (already capped) shape.
+static void clampStaging(ncclComm* c, int nranks) {
+  const int64_t cap = (int64_t)1 << 30;
+  const int64_t per = (int64_t)c->maxChannels * 2 * c->nSlots * (nranks > 1 ? nranks : 2);
+  if ((int64_t)c->slotBytes * per <= cap) return;
+  int64_t sb = cap / per / 4096 * 4096;
+  if (sb < 4096) sb = 4096;
+  WARN("staging slab %lld MiB exceeds the 1 GiB cap: slot size %zu -> %lld bytes",
+       (long long)(((int64_t)c->slotBytes * per) >> 20), c->slotBytes, (long long)sb);
+  c->slotBytes = (size_t)sb;
+}
+
 static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclConfig_t* cfg) {
   c->startMagic = c->endMagic = kCommMagic;
   c->rank = rank;
@@ -77,6 +93,7 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   sb = (sb + 4095) / 4096 * 4096;
   if (sb < 4096) sb = 4096;
   c->slotBytes = (size_t)sb;
+  clampStaging(c, nranks);
 }
 
 static ncclResult_t checkConfig(const ncclConfig_t* cfg) {
@@ -161,12 +178,16 @@ static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id
   }
   if ((res = transportSetup(comm)) != ncclSuccess) goto fail;
   if ((res = fillPeerInfo(comm, &blobs[rank].info)) != ncclSuccess) goto fail;
+  TRACE("rank %d: handles exported", rank);
   if ((res = bootstrapAllGather(comm->bootstrap, blobs.data(), sizeof(Blob))) != ncclSuccess) goto fail;
+  TRACE("rank %d: peer table gathered", rank);
   comm->peers.resize(nranks);
   for (int r = 0; r < nranks; r++) comm->peers[r] = blobs[r].info;
   computeChannelCap(comm);
   if ((res = transportConnect(comm)) != ncclSuccess) goto fail;
+  TRACE("rank %d: peers mapped", rank);
   if ((res = commAllocDevState(comm)) != ncclSuccess) goto fail;
+  TRACE("rank %d: device state ready", rank);
   if ((res = tunerLoad(comm)) != ncclSuccess) goto fail;
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
   INFO("comm %p rank %d nRanks %d dev %d busId %s - Init COMPLETE", (void*)comm, rank, nranks, dev,

@@ -78,7 +78,9 @@ ncclResult_t transportConnect(ncclComm* comm) {
     } else {
       void* s = nullptr;
       void* f = nullptr;
+      TRACE("rank %d: importing rank %d's staging", comm->rank, r);
       HIPCHECK(hipIpcOpenMemHandle(&s, p.stagingHandle, hipIpcMemLazyEnablePeerAccess));
+      TRACE("rank %d: importing rank %d's flags", comm->rank, r);
       HIPCHECK(hipIpcOpenMemHandle(&f, p.flagsHandle, hipIpcMemLazyEnablePeerAccess));
       comm->peerStaging[r] = s;
       comm->peerFlags[r] = (uint64_t*)f;
