@@ -389,3 +389,36 @@ def test_nonblocking_init_from_one_thread(built):
     for c in comms:
         c.destroy()
     assert not errs, errs
+
+
+def test_communicator_churn_releases_resources(built):
+    """Create, use and destroy communicators many times (2 ranks in one process, then windows too):
+    device memory must return to where it started — staging, flags, counters, LL areas, IPC maps,
+    internal streams and events are all released by ncclCommDestroy."""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    torch.cuda.synchronize()
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+
+    def cycle(i):
+        comms = nccl_amd.Communicator.init_all([0, 0])
+        errs = G.run_case(list(zip(comms, streams)), "allreduce", 7, 0, 70_001 if i % 2 else 1000, 0, seed=i)
+        for c in comms:
+            c.destroy()
+        return errs
+
+    assert not cycle(0)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free0, _ = torch.cuda.mem_get_info()
+    for i in range(1, 25):
+        errs = cycle(i)
+        assert not errs, errs
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    free1, _ = torch.cuda.mem_get_info()
+    # each communicator holds > 1 GiB of staging: a leak of even one would show
+    assert free0 - free1 < (256 << 20), f"device memory not released: {(free0 - free1) >> 20} MiB lost"
