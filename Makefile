@@ -20,7 +20,7 @@ DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf plan-test
+all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf plan-test xgmi-probe
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -86,6 +86,14 @@ tests/native/nccl_perf: tests/native/nccl_perf.cc include/nccl.h $(LIBDIR)/libnc
 	$(HIPCC) -O2 --offload-arch=$(ARCH) -Iinclude -o $@ $< -L$(LIBDIR) -lnccl -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 .PHONY: nccl-perf
+
+# CU-driven peer bandwidth probe (run by bench.py's suite on multi-GPU nodes)
+xgmi-probe: tests/native/xgmi_probe
+
+tests/native/xgmi_probe: tests/native/xgmi_probe.hip
+	$(HIPCC) -O2 --offload-arch=$(ARCH) -o $@ $<
+
+.PHONY: xgmi-probe
 
 # CPU test driver of enqueue.cc's planning (no GPU: launches and the few HIP calls are stubbed)
 plan-test: tests/native/plan_test

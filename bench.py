@@ -312,6 +312,17 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         dt = (time.perf_counter() - t0) / 3
         probe["fanout_0toall_GBps"] = round(len(dsts) * nbytes / dt / 1e9, 1)
         probe["method"] = "torch copy_ (hipMemcpyPeerAsync); fan-out = concurrent copies on separate streams"
+        # the CU-driven probe (tests/native/xgmi_probe): 16-byte vector loads/stores from GPU 0's CUs, the
+        # access pattern of the collective kernels, one link and all links, write and read
+        exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "xgmi_probe")
+        if os.path.exists(exe):
+            try:
+                import subprocess
+                r = subprocess.run([exe, "256", "10"], capture_output=True, text=True, timeout=120)
+                probe["cu_kernel"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                    {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
+            except Exception as e:
+                probe["cu_kernel"] = {"error": repr(e)}
         out["xgmi_probe"] = probe
         del src, dsts
     return out

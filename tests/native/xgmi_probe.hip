@@ -1,0 +1,100 @@
+// xgmi_probe.hip — CU-driven peer-to-peer bandwidth over xGMI (the roofline denominators of DESIGN §7):
+// GPU 0 writes to (or reads from) 1 peer and all peers at once with 16-byte vector accesses, the way the
+// collective kernels move data, instead of the SDMA engines behind hipMemcpyPeer. Prints one JSON line.
+//   xgmi_probe [MiB per peer (default 256)] [iterations (default 10)]
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+#define CK(x)                                                                                   \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));                 \
+      exit(2);                                                                                  \
+    }                                                                                           \
+  } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct Targets {
+  u32x4* dst[8];
+  const u32x4* src[8];
+  int n;
+};
+
+// workgroup b moves its share of pair (b % n): a grid-stride copy of `vecs` 16-byte vectors per pair
+__global__ void __launch_bounds__(512) copyPairs(Targets t, size_t vecs) {
+  const int pair = blockIdx.x % t.n;
+  const size_t wgPerPair = gridDim.x / t.n;
+  const size_t w = blockIdx.x / t.n;
+  u32x4* d = t.dst[pair];
+  const u32x4* s = t.src[pair];
+  for (size_t i = w * blockDim.x + threadIdx.x; i < vecs; i += wgPerPair * blockDim.x)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
+int main(int argc, char** argv) {
+  const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 0) : 256;
+  const int iters = argc > 2 ? atoi(argv[2]) : 10;
+  int ndev = 0;
+  CK(hipGetDeviceCount(&ndev));
+  if (ndev < 2) {
+    printf("{\"error\": \"needs 2+ GPUs, found %d\"}\n", ndev);
+    return 0;
+  }
+  if (ndev > 8) ndev = 8;
+  const size_t bytes = mib << 20;
+  std::vector<void*> buf(ndev);
+  for (int d = 0; d < ndev; d++) {
+    CK(hipSetDevice(d));
+    CK(hipMalloc(&buf[d], bytes));
+    CK(hipMemset(buf[d], d, bytes));
+  }
+  CK(hipSetDevice(0));
+  void* local2 = nullptr;
+  CK(hipMalloc(&local2, bytes * (ndev - 1)));
+  for (int d = 1; d < ndev; d++) {
+    hipError_t e = hipDeviceEnablePeerAccess(d, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) CK(e);
+  }
+  (void)hipGetLastError();
+  hipStream_t s;
+  CK(hipStreamCreate(&s));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  auto run = [&](bool write, int npeers) -> double {
+    Targets t = {};
+    t.n = npeers;
+    for (int k = 0; k < npeers; k++) {
+      char* mine = (char*)local2 + (size_t)k * bytes;
+      if (write) {
+        t.src[k] = (const u32x4*)mine;
+        t.dst[k] = (u32x4*)buf[1 + k];
+      } else {
+        t.src[k] = (const u32x4*)buf[1 + k];
+        t.dst[k] = (u32x4*)mine;
+      }
+    }
+    const int grid = (2 * cus / npeers) * npeers;
+    hipLaunchKernelGGL(copyPairs, dim3(grid), dim3(512), 0, s, t, bytes / 16);
+    CK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; i++) hipLaunchKernelGGL(copyPairs, dim3(grid), dim3(512), 0, s, t, bytes / 16);
+    CK(hipEventRecord(e1, s));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return (double)bytes * npeers * iters / (ms * 1e-3) / 1e9;
+  };
+  const int all = ndev - 1;
+  double w1 = run(true, 1), r1 = run(false, 1), wa = run(true, all), ra = run(false, all);
+  printf("{\"method\": \"CU copy kernel on GPU 0, 16-byte nontemporal vectors, %zu MiB per peer, %d iters\", "
+         "\"peers\": %d, \"write_1link_GBps\": %.1f, \"read_1link_GBps\": %.1f, \"write_fanout_GBps\": %.1f, "
+         "\"read_fanin_GBps\": %.1f}\n", mib, iters, all, w1, r1, wa, ra);
+  return 0;
+}
