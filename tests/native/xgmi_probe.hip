@@ -39,8 +39,12 @@ __global__ void __launch_bounds__(512) copyPairs(Targets t, size_t vecs) {
 int main(int argc, char** argv) {
   const size_t mib = argc > 1 ? strtoull(argv[1], nullptr, 0) : 256;
   const int iters = argc > 2 ? atoi(argv[2]) : 10;
+  // loopback (argv[3] == "loopback"): the "peers" are 3 more buffers on GPU 0 — a one-GPU self-test of
+  // the kernel's indexing and of the data check, not a link measurement
+  const bool loop = argc > 3 && argv[3][0] == 'l';
   int ndev = 0;
   CK(hipGetDeviceCount(&ndev));
+  if (loop) ndev = 4;
   if (ndev < 2) {
     printf("{\"error\": \"needs 2+ GPUs, found %d\"}\n", ndev);
     return 0;
@@ -49,14 +53,15 @@ int main(int argc, char** argv) {
   const size_t bytes = mib << 20;
   std::vector<void*> buf(ndev);
   for (int d = 0; d < ndev; d++) {
-    CK(hipSetDevice(d));
+    CK(hipSetDevice(loop ? 0 : d));
     CK(hipMalloc(&buf[d], bytes));
     CK(hipMemset(buf[d], d, bytes));
   }
   CK(hipSetDevice(0));
   void* local2 = nullptr;
   CK(hipMalloc(&local2, bytes * (ndev - 1)));
-  for (int d = 1; d < ndev; d++) {
+  CK(hipMemset(local2, 0xA5, bytes * (ndev - 1)));
+  for (int d = 1; d < ndev && !loop; d++) {
     hipError_t e = hipDeviceEnablePeerAccess(d, 0);
     if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) CK(e);
   }
@@ -92,9 +97,18 @@ int main(int argc, char** argv) {
     return (double)bytes * npeers * iters / (ms * 1e-3) / 1e9;
   };
   const int all = ndev - 1;
-  double w1 = run(true, 1), r1 = run(false, 1), wa = run(true, all), ra = run(false, all);
-  printf("{\"method\": \"CU copy kernel on GPU 0, 16-byte nontemporal vectors, %zu MiB per peer, %d iters\", "
+  double w1 = run(true, 1), wa = run(true, all);
+  // every byte of every written peer buffer must now hold local2's pattern (0xA5)
+  size_t wrong = 0;
+  std::vector<unsigned char> host(bytes);
+  for (int k = 0; k < all; k++) {
+    CK(hipMemcpy(host.data(), buf[1 + k], bytes, hipMemcpyDefault));
+    for (size_t i = 0; i < bytes; i++) wrong += host[i] != 0xA5;
+  }
+  double r1 = run(false, 1), ra = run(false, all);
+  printf("{\"method\": \"CU copy kernel on GPU 0, 16-byte nontemporal vectors, %zu MiB per peer, %d iters%s\", "
          "\"peers\": %d, \"write_1link_GBps\": %.1f, \"read_1link_GBps\": %.1f, \"write_fanout_GBps\": %.1f, "
-         "\"read_fanin_GBps\": %.1f}\n", mib, iters, all, w1, r1, wa, ra);
-  return 0;
+         "\"read_fanin_GBps\": %.1f, \"wrong_bytes\": %zu}\n", mib, iters, loop ? ", LOOPBACK on one GPU" : "",
+         all, w1, r1, wa, ra, wrong);
+  return wrong ? 1 : 0;
 }

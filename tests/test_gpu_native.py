@@ -30,3 +30,16 @@ def test_native_driver(built, args, forkjoin):
     assert out.returncode == 0, out.stdout + out.stderr
     rows = [l.split() for l in out.stdout.splitlines() if l.strip() and not l.startswith("#")]
     assert rows and all(r[5] == "0" for r in rows), out.stdout  # columns: bytes count time algbw busbw #wrong host
+
+
+def test_xgmi_probe_loopback(built):
+    """The CU-driven peer-bandwidth probe that bench.py's suite runs on multi-GPU nodes, in its one-GPU
+    loopback mode: indexing covers every byte of every target (wrong_bytes == 0)."""
+    import json
+    exe = os.path.join(ROOT, "tests", "native", "xgmi_probe")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "xgmi-probe"], cwd=ROOT)
+    out = subprocess.run([exe, "64", "2", "loopback"], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stdout + out.stderr
+    rep = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rep["wrong_bytes"] == 0 and rep["write_fanout_GBps"] > 0
