@@ -93,13 +93,15 @@ def case_list(n: int, quick: bool = False):
     return cases
 
 
-def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=False, root=0, sync=True):
+def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=False, root=0, sync=True,
+             inputs=None):
     """Run one collective on every (comm, stream) of this process; returns list of error strings.
     `comms_and_streams` holds the ranks owned by this process: [(comm, torch stream), ...]; the
     inputs of ALL ranks are regenerated deterministically so each process can check its own ranks."""
     import torch
     n = comms_and_streams[0][0].nranks
-    inputs = make_inputs(n, dtype, count, seed)
+    if inputs is None:
+        inputs = make_inputs(n, dtype, count, seed)
     exp = expected(coll, inputs, dtype, op, root)
     npdt = oracle.NP_STORAGE[dtype]
     es = np.dtype(npdt).itemsize

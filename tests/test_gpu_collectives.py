@@ -320,3 +320,59 @@ def test_one_byte_types_full_channel_plans(built):
     for c in comms:
         c.destroy()
     assert not errs, "\n".join(errs[:20])
+
+
+# special values per dtype, in storage bits: NaNs (both signs), infinities, signed zeros, the smallest and a
+# large subnormal, the largest finite values (fp8 e4m3 has no infinity)
+SPECIALS = {
+    7: np.array([np.nan, -np.nan, np.inf, -np.inf, 0.0, -0.0, 1e-45, -1.1754942e-38, 3.4028235e38, -3.4028235e38,
+                 1.0], dtype=np.float32),
+    8: np.array([np.nan, -np.nan, np.inf, -np.inf, 0.0, -0.0, 5e-324, -2.2250738585072e-308, 1.7976931348623157e308,
+                 -1.7976931348623157e308, 1.0], dtype=np.float64),
+    6: np.array([0x7E00, 0xFE00, 0x7C00, 0xFC00, 0, 0x8000, 0x0001, 0x83FF, 0x7BFF, 0xFBFF, 0x3C00], dtype=np.uint16),
+    9: np.array([0x7FC0, 0xFFC0, 0x7F80, 0xFF80, 0, 0x8000, 0x0001, 0x807F, 0x7F7F, 0xFF7F, 0x3F80], dtype=np.uint16),
+    10: np.array([0x7F, 0xFF, 0x00, 0x80, 0x01, 0x87, 0x7E, 0xFE, 0x38], dtype=np.uint8),
+    11: np.array([0x7C, 0xFC, 0x7E, 0xFE, 0x00, 0x80, 0x01, 0x83, 0x7B, 0xFB, 0x3C], dtype=np.uint8),
+}
+
+
+def _with_specials(inputs, dtype):
+    sp = SPECIALS[dtype]
+    L = len(sp)
+    out = []
+    for r, x in enumerate(inputs):
+        y = x.copy()
+        raw = y.view(sp.dtype) if sp.dtype.kind in "ui" else y
+        for off, shift in ((0, 3), (1, 1), (2, 7)):  # different pairings of specials across the ranks
+            idx = np.arange(off, y.size, 37)
+            raw[idx] = sp[(np.arange(idx.size) + r * shift) % L]
+        out.append(y)
+    return out
+
+
+@pytest.mark.parametrize("dtype", [7, 8, 6, 9, 10, 11])
+def test_special_float_values(built, dtype):
+    """NaN / ±Inf / ±0 / subnormal / max-finite inputs, combined across 3 ranks, through every path (LL,
+    one-shot, direct) and operator: bit-exact vs the oracle (any NaN matches any NaN). Subnormals must
+    survive (no flush to zero, reference common.mk:103), min/max must ignore NaN like fminf/fmaxf."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0, 0])
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    cs = list(zip(comms, streams))
+    errs = []
+    es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+    for count in (4096 // es * 3 + 3, 600_000 // es, 4_000_000 // es):   # LL, one-shot, direct at n = 3
+        for op in (0, 1, 2, 3, 4):
+            ins = _with_specials(G.make_inputs(3, dtype, count, seed=11 + op), dtype)
+            errs += G.run_case(cs, "allreduce", dtype, op, count, 0, seed=0, inputs=ins)
+        ins = _with_specials(G.make_inputs(3, dtype, count - count % 3, seed=5), dtype)
+        errs += G.run_case(cs, "reducescatter", dtype, 0, count - count % 3, 0, seed=0, inputs=ins)
+        if errs:
+            break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
