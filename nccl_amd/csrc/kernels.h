@@ -307,6 +307,10 @@ struct Channel {
   const Red<T, OP>& fn;
   int c, me, n, nSlots;
   bool aligned, isRoot, forceAcq, forceRel, noRel;
+  // AG pull (NCCL_AMD_AG_PULL=1, AllReduce / AllGather): phase B leaves ONE copy of the owner's block in
+  // its own AG staging and phase C reads it from there over xGMI, instead of B pushing n-1 copies into
+  // the peers' staging. Same link bytes, reads instead of writes; slots, credits and flags unchanged.
+  bool agPull;
   static constexpr uint64_t ts = sizeof(T);
 
   __device__ uint64_t blockLen(int q) const {
@@ -391,10 +395,15 @@ struct Channel {
     const uint64_t nelem = hi - lo;
     if (tid == 0) {
       int np = 0;
-      for (int k = 1; k < n; k++) {
-        int p = (me + k) % n;
-        if (pushesTo(p))
-          sh.pushPtr[np++] = dc.staging[p] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_SEND_AG, p) % nSlots), me);
+      if (agPull) {  // every peer's AG counter is equal here (all are pushed to), so any one names the slot
+        sh.pushPtr[np++] =
+            dc.staging[me] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_SEND_AG, (me + 1) % n) % nSlots), me);
+      } else {
+        for (int k = 1; k < n; k++) {
+          int p = (me + k) % n;
+          if (pushesTo(p))
+            sh.pushPtr[np++] = dc.staging[p] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_SEND_AG, p) % nSlots), me);
+        }
       }
       sh.nPush = np;
       // fold order: owner+1, ..., owner (AR/RS, all_reduce.h:43-66) or root+1, ..., root (reduce.h:34-52)
@@ -516,7 +525,9 @@ struct Channel {
       const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
       uint64_t lo, hi;
       sliceRange(a, c, step, blockLen(b), lo, hi);
-      const char* src = dc.staging[me] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_RECV_AG, q) % nSlots), q);
+      const int slot = (int)(ctr(CTR_RECV_AG, q) % nSlots);
+      const char* src = agPull ? dc.staging[q] + stagingOffset(dc, c, STG_AG, slot, q)  // q's own copy, remote
+                               : dc.staging[me] + stagingOffset(dc, c, STG_AG, slot, q);
       char* dst = (char*)a.recvbuff + ((uint64_t)b * a.chunk + lo) * ts;
       copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
     }
@@ -554,10 +565,11 @@ __global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
   const Red<T, OP> fn(opArg);
   // protoFlags (NCCL_AMD_PROTO_FLAGS, diagnostics): 1 = acquire on credit waits too, 2 = release on
   // credit signals too, 4 = C(s) before A(s+1), 8 = NO release fence before data flags (unsafe, measures
-  // the fence cost only)
+  // the fence cost only), 16 = AG pull (NCCL_AMD_AG_PULL=1)
   Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
                           (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
-                          (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0};
+                          (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0,
+                          (COLL == COLL_AR || COLL == COLL_AG) && (a.protoFlags & 16) != 0};
   if (COLL == COLL_AR1) {
     bool ok1 = true;
     for (int s = 0; ok1 && s < a.nSteps; s++) ok1 = ch.oneShotA(s) && ch.oneShotB(s);

@@ -91,7 +91,9 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (3, {"NCCL_ALGO": "ONESHOT", "NCCL_AMD_SLOT_BYTES": "16384"}),
             (3, {"NCCL_PROTO": "LL"}),
             (2, {"NCCL_PROTO": "^LL"}),
-            (2, {"NCCL_ALGO": "DIRECT"})]
+            (2, {"NCCL_ALGO": "DIRECT"}),
+            (3, {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
+            (4, {"NCCL_AMD_AG_PULL": "1"})]
 
 
 @pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
