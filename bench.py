@@ -269,13 +269,15 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     xs = torch.empty(c, dtype=torch.float32, device="cuda").uniform_(-1, 1)
     ys = torch.empty_like(xs)
     tuning = []
-    knobs = ("NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_AG_PULL")
+    knobs = ("NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_AG_PULL",
+             "NCCL_AMD_RS_PULL")
     saved = {k: os.environ.get(k) for k in knobs}
     # (the staging slab is capped at 1 GiB per rank, so slot sizes scale with channels x slots x n:
     #  default 128 KiB slots at n = 8, 256 KiB with 128 channels)
     for env in ({}, {"NCCL_AMD_SLOT_BYTES": "32768"}, {"NCCL_AMD_SLOT_BYTES": "65536"},
                 {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_AMD_NSLOTS": "4"}, {"NCCL_MAX_CTAS": "128"},
-                {"NCCL_MAX_CTAS": "64"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}, {"NCCL_AMD_AG_PULL": "1"}):
+                {"NCCL_MAX_CTAS": "64"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}, {"NCCL_AMD_AG_PULL": "1"},
+                {"NCCL_AMD_RS_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}):
         for k in knobs:
             os.environ.pop(k, None)
         os.environ.update(env)

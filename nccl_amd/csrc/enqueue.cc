@@ -81,7 +81,7 @@ void loadTuning(CommTuning* t) {
   t->checkPointers = (int)paramInt("NCCL_CHECK_POINTERS", 0);
   t->forceElementwise = (int)paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0);
   t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 1) ? 0 : 8) |
-                  (paramInt("NCCL_AMD_AG_PULL", 0) ? 16 : 0);
+                  (paramInt("NCCL_AMD_AG_PULL", 0) ? 16 : 0) | (paramInt("NCCL_AMD_RS_PULL", 0) ? 32 : 0);
   if (const char* algo = paramStr("NCCL_ALGO")) {
     if (!strcasecmp(algo, "ONESHOT")) t->algo = 1;
     else if (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE")) t->algo = 2;

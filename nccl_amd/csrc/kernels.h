@@ -311,6 +311,10 @@ struct Channel {
   // its own AG staging and phase C reads it from there over xGMI, instead of B pushing n-1 copies into
   // the peers' staging. Same link bytes, reads instead of writes; slots, credits and flags unchanged.
   bool agPull;
+  // RS pull (NCCL_AMD_RS_PULL=1, AllReduce / ReduceScatter): phase A copies my input's block-p slice into
+  // MY OWN RS staging (area "for p", a local copy) and owner p's fold reads it from there over xGMI,
+  // instead of A writing it into p's staging. Same link bytes as reads; slots, credits and flags unchanged.
+  bool rsPull;
   static constexpr uint64_t ts = sizeof(T);
 
   __device__ uint64_t blockLen(int q) const {
@@ -354,7 +358,8 @@ struct Channel {
       uint64_t lo, hi;
       sliceRange(a, c, step, blockLen(b), lo, hi);
       int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
-      char* dst = dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me);
+      char* dst = rsPull ? dc.staging[me] + stagingOffset(dc, c, STG_RS, slot, p)   // my slab, area for p
+                         : dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me);
       const char* src = (const char*)a.sendbuff + ((uint64_t)b * a.chunk + lo) * ts;
       copyRange<T, true>(dst, src, (hi - lo) * ts, aligned);
     }
@@ -410,8 +415,10 @@ struct Channel {
       int first = (COLL == COLL_REDUCE ? a.root + 1 : me + 1) % n;
       for (int k = 0; k < n; k++) {
         int q = (first + k) % n;
+        const int rslot = (int)(ctr(CTR_RECV_RS, q) % nSlots);
         sh.srcPtr[k] = q == me ? (const char*)a.sendbuff + ((uint64_t)myB * a.chunk + lo) * ts
-                               : dc.staging[me] + stagingOffset(dc, c, STG_RS, (int)(ctr(CTR_RECV_RS, q) % nSlots), q);
+                     : rsPull  ? dc.staging[q] + stagingOffset(dc, c, STG_RS, rslot, me)  // q's slab, remote
+                               : dc.staging[me] + stagingOffset(dc, c, STG_RS, rslot, q);
       }
     }
     __syncthreads();
@@ -565,11 +572,12 @@ __global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
   const Red<T, OP> fn(opArg);
   // protoFlags (NCCL_AMD_PROTO_FLAGS, diagnostics): 1 = acquire on credit waits too, 2 = release on
   // credit signals too, 4 = C(s) before A(s+1), 8 = NO release fence before data flags (unsafe, measures
-  // the fence cost only), 16 = AG pull (NCCL_AMD_AG_PULL=1)
+  // the fence cost only), 16 = AG pull (NCCL_AMD_AG_PULL=1), 32 = RS pull (NCCL_AMD_RS_PULL=1)
   Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
                           (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
                           (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0,
-                          (COLL == COLL_AR || COLL == COLL_AG) && (a.protoFlags & 16) != 0};
+                          (COLL == COLL_AR || COLL == COLL_AG) && (a.protoFlags & 16) != 0,
+                          (COLL == COLL_AR || COLL == COLL_RS) && (a.protoFlags & 32) != 0};
   if (COLL == COLL_AR1) {
     bool ok1 = true;
     for (int s = 0; ok1 && s < a.nSteps; s++) ok1 = ch.oneShotA(s) && ch.oneShotB(s);

@@ -93,7 +93,9 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (2, {"NCCL_PROTO": "^LL"}),
             (2, {"NCCL_ALGO": "DIRECT"}),
             (3, {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
-            (4, {"NCCL_AMD_AG_PULL": "1"})]
+            (4, {"NCCL_AMD_AG_PULL": "1"}),
+            (3, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
+            (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"})]
 
 
 @pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
