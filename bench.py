@@ -145,6 +145,26 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     out["rs_ag_bf16"] = {"config": f"ncclReduceScatter + ncclAllGather bf16, {bucket // MIB} MiB bucket, n={n}",
                          "rs_ms": round(ms_rs, 4), "rs_busbw_GBps": bw(ms_rs), "ag_ms": round(ms_ag, 4),
                          "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(ok) else "FAIL"}
+    # the same with the pull variants of both phases (xGMI reads instead of writes), its own communicator
+    pulls = ("NCCL_AMD_RS_PULL", "NCCL_AMD_AG_PULL")
+    saved_p = {k: os.environ.get(k) for k in pulls}
+    os.environ.update({k: "1" for k in pulls})
+    cp = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+    for k, v in saved_p.items():
+        os.environ.pop(k, None)
+        if v is not None:
+            os.environ[k] = v
+    ms_rs = tmax(_time_ms(lambda: cp.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp), stream, 10))
+    ms_ag = tmax(_time_ms(lambda: cp.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp), stream, 10))
+    full.zero_()
+    cp.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp)
+    cp.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp)
+    torch.cuda.synchronize()
+    okp = bool(torch.equal(full, base * (n * (n + 1) // 2)))
+    cp.destroy()
+    out["rs_ag_bf16"]["pull"] = {"rs_ms": round(ms_rs, 4), "rs_busbw_GBps": bw(ms_rs), "ag_ms": round(ms_ag, 4),
+                                 "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(okp) else "FAIL",
+                                 "env": "NCCL_AMD_RS_PULL=1 NCCL_AMD_AG_PULL=1"}
     del send, shard, full, base
 
     # --- configs[3]: fp16 AllReduce sweep: LL vs one-shot vs direct. Protocol/algorithm knobs are read at
