@@ -533,8 +533,8 @@ def main(argv=None):
         except Exception as e:  # secondary measurement
             extra["host_staged"] = {"error": repr(e)}
 
-    cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    cpu = None  # the contract's CPU baseline is an N=1 figure (rank 0 only)
+    if n == 1 and rank == 0 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(n, count, args.cpu_seconds)
         except Exception as e:  # the baseline is reported, never required
