@@ -669,7 +669,11 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
   const uint64_t t0 = clockTicks();
   bool ok = true;
   const char* myLL = (const char*)dc.flags[me];
+  const bool folds = op.coll != LL_AG && !(op.coll == LL_REDUCE && me != op.root);
+  const char* mine = op.coll == LL_RS ? send + (uint64_t)me * nbytes : send;
   for (uint64_t pk = lo + tid; pk < hi; pk += kThreads) {
+    // my own contribution, loaded before the wait so its latency hides behind the peers' lines
+    const uint64_t myV = folds ? payload(mine, pk) : 0;
     // pass 1: wait until every peer's line for this payload carries this epoch's flag
     uint32_t pending = 0;
     for (int q = 0; q < n; q++)
@@ -712,17 +716,16 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
     }
     // Reduce: every rank sends to and polls every peer (that keeps the parity double-buffering safe, as
     // for AllReduce), only the root folds, in its ring order root+1, ..., root (reference reduce.h)
-    if (op.coll == LL_REDUCE && me != op.root) continue;
+    if (!folds) continue;
     // pass 2: fold in the owner block's ring order (the lines stay valid until epoch + 2)
     const int owner = op.coll == LL_RS ? me
                     : op.coll == LL_REDUCE ? op.root
                     : (int)((pk * 8 / sizeof(T)) / op.chunk);  // an AllReduce payload never straddles blocks
-    const char* mine = op.coll == LL_RS ? send + (uint64_t)me * nbytes : send;
     union { uint64_t u; T e[EPP]; } acc, x;
     for (int k = 0; k < n; k++) {
       int q = (owner + 1 + k) % n;
       if (q == me) {
-        x.u = payload(mine, pk);
+        x.u = myV;
       } else {
         const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
         x.u = (loadLL(ln) & 0xffffffffull) | (loadLL(ln + 1) << 32);
