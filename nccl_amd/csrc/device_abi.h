@@ -33,11 +33,17 @@
 namespace ncclamd {
 
 enum StagingKind { STG_RS = 0, STG_AG = 1, STG_KINDS = 2 };
+// FLG_PULL_READY / FLG_PULL_ACK and CTR_PULL_PUB / CTR_PULL_GOT: the AG-pull gather (kernels.h
+// Channel::agPull) publishes ONE copy per step that every peer reads, so it keeps its own sequence (the
+// per-pair AG counters diverge once a Reduce has pushed to its root only).
 enum FlagKind {
   FLG_RS_READY = 0, FLG_RS_ACK = 1, FLG_AG_READY = 2, FLG_AG_ACK = 3,
-  FLG_SYM_ENTER = 4, FLG_SYM_MID = 5, FLG_SYM_DONE = 6, FLG_KINDS = 7
+  FLG_SYM_ENTER = 4, FLG_SYM_MID = 5, FLG_SYM_DONE = 6, FLG_PULL_READY = 7, FLG_PULL_ACK = 8, FLG_KINDS = 9
 };
-enum CtrKind { CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_SYM = 4, CTR_LL = 5, CTR_KINDS = 6 };
+enum CtrKind {
+  CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_SYM = 4, CTR_LL = 5,
+  CTR_PULL_PUB = 6, CTR_PULL_GOT = 7, CTR_KINDS = 8
+};
 
 // Device reduction kinds (reference ncclDevRedOp_t subset, src/include/device.h)
 enum DevRedOp { DEV_SUM = 0, DEV_PROD = 1, DEV_MINMAX = 2, DEV_PREMULSUM = 3, DEV_SUMPOSTDIV = 4, DEV_NUMOPS = 5 };

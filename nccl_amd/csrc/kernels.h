@@ -309,7 +309,10 @@ struct Channel {
   bool aligned, isRoot, forceAcq, forceRel, noRel;
   // AG pull (NCCL_AMD_AG_PULL=1, AllReduce / AllGather): phase B leaves ONE copy of the owner's block in
   // its own AG staging and phase C reads it from there over xGMI, instead of B pushing n-1 copies into
-  // the peers' staging. Same link bytes, reads instead of writes; slots, credits and flags unchanged.
+  // the peers' staging. Same link bytes, reads instead of writes. The copy is shared by all readers, so
+  // it runs on its own per-channel sequence (CTR_PULL_PUB / CTR_PULL_GOT, FLG_PULL_READY / FLG_PULL_ACK):
+  // the slot is reused only after EVERY peer acked, and the per-pair AG counters (which a Reduce, pushing
+  // to its root only, advances unevenly) are left alone.
   bool agPull;
   // RS pull (NCCL_AMD_RS_PULL=1, AllReduce / ReduceScatter): phase A copies my input's block-p slice into
   // MY OWN RS staging (area "for p", a local copy) and owner p's fold reads it from there over xGMI,
@@ -387,12 +390,13 @@ struct Channel {
     }
     if (push) {
       if (tid < NCCL_AMD_MAX_RANKS) {
-        uint64_t s = ctr(CTR_SEND_AG, tid);
+        // pull: slot pub % nSlots is free once EVERY peer acked publication pub - nSlots
+        uint64_t s = agPull ? ctr(CTR_PULL_PUB, 0) : ctr(CTR_SEND_AG, tid);
         bool dstPeer = tid < n && tid != me && pushesTo(tid);
         sh.want[tid] = (dstPeer && s + 1 > (uint64_t)nSlots) ? s + 1 - nSlots : 0;
       }
       __syncthreads();
-      if (!waitAll(dc, sh.st, myFlags(FLG_AG_ACK), sh.want, forceAcq)) return false;
+      if (!waitAll(dc, sh.st, myFlags(agPull ? FLG_PULL_ACK : FLG_AG_ACK), sh.want, forceAcq)) return false;
     }
     const int myB = blockOf(me);
     uint64_t lo, hi;
@@ -400,9 +404,8 @@ struct Channel {
     const uint64_t nelem = hi - lo;
     if (tid == 0) {
       int np = 0;
-      if (agPull) {  // every peer's AG counter is equal here (all are pushed to), so any one names the slot
-        sh.pushPtr[np++] =
-            dc.staging[me] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_SEND_AG, (me + 1) % n) % nSlots), me);
+      if (agPull) {  // one copy in my own AG staging, at this channel's publication sequence
+        sh.pushPtr[np++] = dc.staging[me] + stagingOffset(dc, c, STG_AG, (int)(ctr(CTR_PULL_PUB, 0) % nSlots), me);
       } else {
         for (int k = 1; k < n; k++) {
           int p = (me + k) % n;
@@ -437,8 +440,8 @@ struct Channel {
     if (tid < NCCL_AMD_MAX_RANKS) {
       bool peer = tid < n && tid != me;
       bool dstPeer = peer && push && pushesTo(tid);
-      sh.sigVal[tid] = dstPeer ? ctr(CTR_SEND_AG, tid) + 1 : 0;
-      sh.sigPtr[tid] = dstPeer ? dc.flags[tid] + flagIndex(c, FLG_AG_READY, me) : nullptr;
+      sh.sigVal[tid] = dstPeer ? (agPull ? ctr(CTR_PULL_PUB, 0) : ctr(CTR_SEND_AG, tid)) + 1 : 0;
+      sh.sigPtr[tid] = dstPeer ? dc.flags[tid] + flagIndex(c, agPull ? FLG_PULL_READY : FLG_AG_READY, me) : nullptr;
       bool ack = peer && COLL != COLL_AG;
       sh.sigVal[NCCL_AMD_MAX_RANKS + tid] = ack ? ctr(CTR_RECV_RS, tid) + 1 : 0;
       sh.sigPtr[NCCL_AMD_MAX_RANKS + tid] = ack ? dc.flags[tid] + flagIndex(c, FLG_RS_ACK, me) : nullptr;
@@ -447,8 +450,9 @@ struct Channel {
     signalAll(sh.sigPtr, sh.sigVal, 2 * NCCL_AMD_MAX_RANKS, (push && !noRel) || forceRel);
     if (tid < n && tid != me) {
       if (COLL != COLL_AG) ctr(CTR_RECV_RS, tid)++;
-      if (push && pushesTo(tid)) ctr(CTR_SEND_AG, tid)++;
+      if (push && pushesTo(tid) && !agPull) ctr(CTR_SEND_AG, tid)++;
     }
+    if (agPull && tid == 0) ctr(CTR_PULL_PUB, 0)++;
     __syncthreads();
     return true;
   }
@@ -524,15 +528,16 @@ struct Channel {
   // C: gather the other blocks from my AG staging into the output (AR, AG, REDUCE at root)
   __device__ bool phaseC(int step) {
     int tid = threadIdx.x;
-    if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_AG, tid) + 1 : 0;
+    const int recvKind = agPull ? CTR_PULL_GOT : CTR_RECV_AG;
+    if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(recvKind, tid) + 1 : 0;
     __syncthreads();
-    if (!waitAll(dc, sh.st, myFlags(FLG_AG_READY), sh.want, true)) return false;
+    if (!waitAll(dc, sh.st, myFlags(agPull ? FLG_PULL_READY : FLG_AG_READY), sh.want, true)) return false;
     for (int k = 1; k < n; k++) {
       int q = (me + n - k) % n;
       const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
       uint64_t lo, hi;
       sliceRange(a, c, step, blockLen(b), lo, hi);
-      const int slot = (int)(ctr(CTR_RECV_AG, q) % nSlots);
+      const int slot = (int)(ctr(recvKind, q) % nSlots);
       const char* src = agPull ? dc.staging[q] + stagingOffset(dc, c, STG_AG, slot, q)  // q's own copy, remote
                                : dc.staging[me] + stagingOffset(dc, c, STG_AG, slot, q);
       char* dst = (char*)a.recvbuff + ((uint64_t)b * a.chunk + lo) * ts;
@@ -540,12 +545,12 @@ struct Channel {
     }
     if (tid < NCCL_AMD_MAX_RANKS) {
       bool peer = tid < n && tid != me;
-      sh.sigVal[tid] = peer ? ctr(CTR_RECV_AG, tid) + 1 : 0;
-      sh.sigPtr[tid] = peer ? dc.flags[tid] + flagIndex(c, FLG_AG_ACK, me) : nullptr;
+      sh.sigVal[tid] = peer ? ctr(recvKind, tid) + 1 : 0;
+      sh.sigPtr[tid] = peer ? dc.flags[tid] + flagIndex(c, agPull ? FLG_PULL_ACK : FLG_AG_ACK, me) : nullptr;
     }
     __syncthreads();
     signalAll(sh.sigPtr, sh.sigVal, NCCL_AMD_MAX_RANKS, forceRel);  // credits only
-    if (tid < n && tid != me) ctr(CTR_RECV_AG, tid)++;
+    if (tid < n && tid != me) ctr(recvKind, tid)++;
     __syncthreads();
     return true;
   }

@@ -108,7 +108,8 @@ ncclResult_t transportDrainCredits(ncclComm* comm) {
       for (int p = 0; p < comm->nRanks && done; p++) {
         if (p == comm->rank) continue;
         done = flg[flagIndex(c, FLG_RS_ACK, p)] >= ctr[ctrIndex(c, CTR_SEND_RS, p)] &&
-               flg[flagIndex(c, FLG_AG_ACK, p)] >= ctr[ctrIndex(c, CTR_SEND_AG, p)];
+               flg[flagIndex(c, FLG_AG_ACK, p)] >= ctr[ctrIndex(c, CTR_SEND_AG, p)] &&
+               flg[flagIndex(c, FLG_PULL_ACK, p)] >= ctr[ctrIndex(c, CTR_PULL_PUB, 0)];
       }
     if (done) return ncclSuccess;
     if (waited >= limitMs) {

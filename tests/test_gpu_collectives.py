@@ -380,3 +380,40 @@ def test_special_float_values(built, dtype):
     for c in comms:
         c.destroy()
     assert not errs, "\n".join(errs[:20])
+
+
+@pytest.mark.parametrize("env", [{"NCCL_AMD_AG_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"},
+                                 {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
+                         ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots"])
+def test_pull_modes_interleaved_with_reduce(built, env):
+    """Pull-mode gathers after Reduces on the same communicator: a Reduce pushes to its root only, so the
+    per-pair AG sequences diverge; the pull gather must run on its own sequence (found by scripts/fuzz.py:
+    an AllGather after a Reduce read a stale slot)."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        torch.cuda.set_device(0)
+        comms = nccl_amd.Communicator.init_all([0, 0, 0])
+    finally:
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    cs = list(zip(comms, streams))
+    seq = [("reduce", 7, 0, 100_003, 2), ("allgather", 6, 0, 7, 0), ("allreduce", 7, 0, 300_001, 0),
+           ("reduce", 2, 3, 50_000, 0), ("reduce", 9, 0, 4099, 1), ("allgather", 7, 0, 70_001, 0),
+           ("allreduce", 9, 2, 1_000_003, 0), ("reducescatter", 7, 0, 3 * 40_000, 0), ("allgather", 2, 0, 5, 0)]
+    errs = []
+    for rep in range(2):
+        for i, (coll, dt, op, count, root) in enumerate(seq):
+            errs += G.run_case(cs, coll, dt, op, count, 0, seed=1000 * rep + i, root=root)
+            if errs:
+                break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:10])
