@@ -48,8 +48,13 @@ constexpr int kThreads = 512;  // 8 waves of 64 per channel workgroup
 
 __device__ __forceinline__ uint64_t clockTicks() { return __builtin_amdgcn_s_memrealtime(); }
 
+// The stores are inline asm (the compiler has no builtin for a write-through system-scope store), so the
+// compiler's hazard recognizer cannot see them: each one carries its own trailing wait states, or a VALU /
+// LDS write that reuses its address or data VGPRs right behind it can be picked up by the store (seen as
+// pointer-valued garbage in 16-byte-pack-sized holes of the uint32/uint64 kernels once register allocation
+// placed such a write there).
 __device__ __forceinline__ void storeRemote(void* p, u32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 __device__ __forceinline__ void drainStores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -59,19 +64,19 @@ __device__ __forceinline__ void storeRemoteElt(T* p, T v) {
   if constexpr (sizeof(T) == 1) {
     uint32_t x = 0;
     __builtin_memcpy(&x, &v, 1);
-    asm volatile("global_store_byte %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+    asm volatile("global_store_byte %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
   } else if constexpr (sizeof(T) == 2) {
     uint32_t x = 0;
     __builtin_memcpy(&x, &v, 2);
-    asm volatile("global_store_short %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+    asm volatile("global_store_short %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
   } else if constexpr (sizeof(T) == 4) {
     uint32_t x;
     __builtin_memcpy(&x, &v, 4);
-    asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+    asm volatile("global_store_dword %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
   } else {
     uint64_t x;
     __builtin_memcpy(&x, &v, 8);
-    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(x) : "memory");
+    asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(x) : "memory");
   }
 }
 

@@ -417,3 +417,49 @@ def test_pull_modes_interleaved_with_reduce(built, env):
     for c in comms:
         c.destroy()
     assert not errs, "\n".join(errs[:10])
+
+
+def test_multistep_integer_pipelines(built):
+    """Multi-step channel pipelines (64 KiB slots, 7 channels) for the 32/64-bit integer kernels: the
+    inline-asm write-through stores need their own trailing wait states, or a register reuse right behind a
+    store (which register allocation put there for these kernels only) sends pointer-valued garbage in
+    16-byte-pack holes. Found by scripts/fuzz.py; bit-exact vs the oracle."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    env = {"NCCL_AMD_SLOT_BYTES": "65536", "NCCL_MAX_CTAS": "7"}
+    saved = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        torch.cuda.set_device(0)
+        comms = nccl_amd.Communicator.init_all([0, 0, 0])
+    finally:
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+    cs = list(zip(comms, [torch.cuda.Stream() for _ in range(3)]))
+    errs = []
+    for i, (coll, dt, op, count, root) in enumerate([
+            ("allreduce", 2, 0, 1 << 20, 0), ("allreduce", 4, 2, 1048587, 0), ("allreduce", 3, 1, 3 << 19, 0),
+            ("reduce", 2, 0, 1048587, 1), ("reduce", 4, 2, 1048587, 2), ("reducescatter", 5, 0, 3 << 19, 0),
+            ("allgather", 2, 0, 1 << 18, 0)]):
+        errs += G.run_case(cs, coll, dt, op, count, 0, seed=4000 + i, root=root)
+        if errs:
+            break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:10])
+
+
+def test_fuzz_short(built):
+    """A short randomized sweep (scripts/fuzz.py): random communicator settings x random collectives,
+    bit-exact vs the oracle."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "fuzz.py"), "25", "7"],
+                         capture_output=True, text=True, timeout=180)
+    assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
+    assert "FUZZ OK" in out.stdout
