@@ -1,6 +1,7 @@
 """Randomized parity fuzzing on the GPU: random communicator settings (ranks 2-4 in one process, slot size,
 slot count, channel cap, protocol / algorithm, pull variants) and, per communicator, random collectives
-(type, op, count incl. ragged and tiny, misaligned bases, in place, root, grouped batches) checked bit-exact
+(type, op, count incl. ragged and tiny, misaligned bases, in place, root; sometimes a group of several
+collectives, so small AllReduces aggregate into LL batches between other ops) checked bit-exact
 against the CPU oracle. Usage: python scripts/fuzz.py SECONDS [SEED]. Prints one line per communicator."""
 import os
 import random
@@ -42,6 +43,48 @@ def settings(rng):
     return env
 
 
+def run_group(cs, ops, rng):
+    """Several collectives in ONE group (ops outer, ranks inner: every rank issues the same sequence), so
+    runs of small AllReduces aggregate into LL batches between the other ops; every output checked."""
+    import numpy as np
+    import oracle
+    n = len(cs)
+    dev = torch.device("cuda", 0)
+    plans = []
+    for coll, dt, op, count, root in ops:
+        ins = G.make_inputs(n, dt, count, rng.randrange(1 << 30))
+        exp = G.expected(coll, ins, dt, op, root)
+        npdt = oracle.NP_STORAGE[dt]
+        bufs = []
+        for r in range(n):
+            b1, sv = G.to_device(ins[r], dev)
+            rv, b2 = None, None
+            if coll != "reduce" or r == root:
+                b2, rv = G.to_device(np.zeros(G.out_count(coll, n, count), dtype=npdt), dev)
+            bufs.append((b1, sv, b2, rv))
+        plans.append((coll, dt, op, count, root, exp, npdt, bufs))
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for coll, dt, op, count, root, exp, npdt, bufs in plans:
+            for (comm, stream), (b1, sv, b2, rv) in zip(cs, bufs):
+                G.launch(comm, coll, sv, rv, count, dt, op, root, stream.cuda_stream)
+    torch.cuda.synchronize()
+    errs = []
+    for k, (coll, dt, op, count, root, exp, npdt, bufs) in enumerate(plans):
+        for r, (b1, sv, b2, rv) in enumerate(bufs):
+            if rv is None:
+                continue
+            got = G.from_device(rv, npdt)
+            want = exp[0] if coll == "reduce" else exp[r]
+            if not G.same_bits(got, want, dt):
+                errs.append(f"group op {k} {coll} dt={dt} op={op} count={count} root={root} rank {r}: "
+                            f"{int((got != want).sum())} mismatches")
+    for comm, _ in cs:
+        if comm.async_error():
+            errs.append(f"rank {comm.rank}: async error {comm.async_error()}")
+    return errs
+
+
 def main():
     budget = float(sys.argv[1]) if len(sys.argv) > 1 else 60
     seed = int(sys.argv[2]) if len(sys.argv) > 2 else 1
@@ -60,6 +103,23 @@ def main():
         cs = list(zip(comms, streams))
         done = 0
         for _ in range(rng.randint(4, 12)):
+            if rng.random() < 0.2:  # a group of several ops: LL batches between other collectives
+                dt = rng.choice([2, 6, 7, 9])
+                op = rng.choice([0, 2, 3])
+                ops = []
+                for _k in range(rng.randint(2, 12)):
+                    coll = rng.choice(["allreduce"] * 4 + ["reducescatter", "allgather", "reduce"])
+                    count = rng.choice([1, 5, 64, 1000, 2048, 4099, 30_000, 200_001])
+                    if coll == "reducescatter":
+                        count = max(1, count // n) * n
+                    ops.append((coll, dt, 0 if coll == "allgather" else op, count, rng.randrange(n)))
+                errs = run_group(cs, ops, rng)
+                total += len(ops)
+                done += len(ops)
+                if errs:
+                    failures.append(f"n={n} env={env} group {ops}: {errs[:3]}")
+                    break
+                continue
             coll = rng.choice(["allreduce", "allreduce", "reducescatter", "allgather", "reduce"])
             dt = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
             op = 0 if coll == "allgather" else rng.choice([0, 1, 2, 3, 4])
