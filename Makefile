@@ -14,7 +14,7 @@ SRCDIR   := nccl_amd/csrc
 COMMON   := -O3 -fPIC -std=c++17 -ffp-contract=off -fvisibility=hidden -Wall -Wno-unused-function \
             -Wno-unused-variable -Wno-unused-but-set-variable -Iinclude
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics
-HOSTSRC  := debug.cc bootstrap.cc transport.cc init.cc group.cc enqueue.cc register.cc tuner.cc
+HOSTSRC  := debug.cc bootstrap.cc ipc.cc transport.cc init.cc group.cc enqueue.cc register.cc tuner.cc
 HOSTOBJ  := $(HOSTSRC:%.cc=$(BUILD)/%.o)
 DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)

@@ -128,6 +128,14 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64 (same soname as /opt/rocm's). If this
+    # library were loaded first it would pull in /opt/rocm's runtime and torch would later bring a second
+    # one ("no ROCm-capable device" from whichever initialises second), so let torch load its runtime first
+    # and bind to that one.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     p = path or os.environ.get("NCCL_AMD_LIB", LIB_PATH)
     if not os.path.exists(p):
         raise RuntimeError(f"nccl_amd: HIP library {p} is missing — build it first (make, or __graft_entry__.build())")
@@ -359,25 +367,42 @@ class Communicator:
         return v.value
 
     # ---- collectives on torch tensors ----
+    def _check_tensors(self, where: str, *ts) -> None:
+        """Buffers handed to the C ABI are raw pointers: they must be dense and on this communicator's GPU."""
+        for t in ts:
+            if t is None:
+                continue
+            if not t.is_contiguous():
+                raise ValueError(f"{where}: tensors must be contiguous")
+            if t.device.type != "cuda" or t.device.index != self.device:
+                raise ValueError(f"{where}: tensor on {t.device}, communicator on cuda:{self.device}")
+
     def allreduce(self, sendbuf, recvbuf, op=RedOp.SUM, *, stream=None) -> None:
+        self._check_tensors("allreduce", sendbuf, recvbuf)
         if sendbuf.numel() != recvbuf.numel() or sendbuf.dtype != recvbuf.dtype:
             raise ValueError("allreduce: sendbuf/recvbuf must match in dtype and count")
         self.all_reduce_raw(sendbuf.data_ptr(), recvbuf.data_ptr(), sendbuf.numel(),
                             torch_dtype_to_nccl(sendbuf.dtype), int(op), _stream_ptr(stream, self.device))
 
     def reduce_scatter(self, sendbuf, recvbuf, op=RedOp.SUM, *, stream=None) -> None:
+        self._check_tensors("reduce_scatter", sendbuf, recvbuf)
         if sendbuf.numel() != recvbuf.numel() * self.nranks or sendbuf.dtype != recvbuf.dtype:
             raise ValueError("reduce_scatter: sendbuf must hold nranks * recvbuf.numel() elements of the same dtype")
         self.reduce_scatter_raw(sendbuf.data_ptr(), recvbuf.data_ptr(), recvbuf.numel(),
                                 torch_dtype_to_nccl(sendbuf.dtype), int(op), _stream_ptr(stream, self.device))
 
     def allgather(self, sendbuf, recvbuf, *, stream=None) -> None:
+        self._check_tensors("allgather", sendbuf, recvbuf)
         if recvbuf.numel() != sendbuf.numel() * self.nranks or sendbuf.dtype != recvbuf.dtype:
             raise ValueError("allgather: recvbuf must hold nranks * sendbuf.numel() elements of the same dtype")
         self.all_gather_raw(sendbuf.data_ptr(), recvbuf.data_ptr(), sendbuf.numel(),
                             torch_dtype_to_nccl(sendbuf.dtype), _stream_ptr(stream, self.device))
 
     def reduce(self, sendbuf, recvbuf, op=RedOp.SUM, root: int = 0, *, stream=None) -> None:
+        self._check_tensors("reduce", sendbuf, recvbuf if self.rank == root else None)
+        if self.rank == root and (recvbuf is None or recvbuf.numel() != sendbuf.numel()
+                                  or recvbuf.dtype != sendbuf.dtype):
+            raise ValueError("reduce: the root's recvbuf must match sendbuf in dtype and count")
         self.reduce_raw(sendbuf.data_ptr(), _ptr(recvbuf), sendbuf.numel(), torch_dtype_to_nccl(sendbuf.dtype),
                         int(op), root, _stream_ptr(stream, self.device))
 

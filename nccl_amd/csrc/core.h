@@ -88,6 +88,31 @@ ncclResult_t cliqueAllGather(LocalClique* c, int rank, void* data, size_t bytesP
 // ---------------------------------------------------------------- communicator (reference src/include/comm.h)
 constexpr uint64_t kCommMagic = 0x4d493335584e4343ull;  // "MI35XNCC"
 
+// ---------------------------------------------------------------- cross-process memory (ipc.cc)
+// An exported allocation as a peer sees it: the dma-buf fd server and key to fetch it from (reference: cuMem
+// POSIX fd handles, src/transport/p2p.cc:220-325), or a legacy hipIpc handle (NCCL_AMD_IPC=legacy).
+struct IpcDesc {
+  uint64_t key;
+  uint64_t size;
+  char server[40];  // abstract UNIX socket name of the exporter's fd server
+  int legacy;
+  hipIpcMemHandle_t handle;
+};
+struct IpcImport {  // one mapping of a peer's allocation in this process
+  void* ptr;
+  void* ext;  // hipExternalMemory_t
+  int fd;
+  int legacy;
+};
+struct FdServer;
+bool ipcLegacy();
+ncclResult_t ipcServerStart(ncclComm* comm);
+void ipcServerStop(ncclComm* comm);
+ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d);
+void ipcUnexport(ncclComm* comm, const IpcDesc& d);
+ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out);
+void ipcRelease(IpcImport* m);
+
 struct PeerInfo {  // exchanged once at init (reference: struct ncclPeerInfo, src/init.cc:1035-1037)
   int rank;
   int device;
@@ -95,8 +120,8 @@ struct PeerInfo {  // exchanged once at init (reference: struct ncclPeerInfo, sr
   uint64_t hostHash;
   char busId[32];
   int numCUs;
-  hipIpcMemHandle_t stagingHandle;
-  hipIpcMemHandle_t flagsHandle;
+  IpcDesc stagingDesc;  // other processes import these
+  IpcDesc flagsDesc;
   uint64_t stagingPtr;  // raw pointers, valid only inside the same process
   uint64_t flagsPtr;
 };
@@ -110,11 +135,11 @@ struct UserRedOp {  // ncclRedOpCreatePreMulSum state (reference src/enqueue.cc:
 };
 
 
-// One peer mapping of a registered allocation (HIP IPC, refcounted per comm: a segment is opened once).
+// One peer mapping of a registered allocation (refcounted per comm: a segment is imported once).
 struct IpcMapping {
   int peer;
   uint64_t base;   // allocation base in the peer's address space
-  void* mapped;    // the same allocation as mapped here
+  IpcImport map;   // the same allocation as mapped here
   int refs;
 };
 
@@ -128,6 +153,7 @@ struct CommTuning {
   int algo;                 // NCCL_ALGO: 0 unset, 1 ONESHOT, 2 DIRECT (RING / TREE)
   int llOn, simpleOn;       // NCCL_PROTO
   int symDisable;           // NCCL_AMD_SYM_DISABLE
+  int symOneShot;           // NCCL_AMD_SYM_ONESHOT: caller promises out-of-place window AllReduces
   int noAggregation;        // NCCL_AMD_NO_AGGREGATION
   int64_t oneShotBytes;     // NCCL_AMD_ONESHOT_BYTES
   int64_t llBytes;          // NCCL_AMD_LL_BYTES
@@ -169,7 +195,9 @@ struct ncclComm {
   uint64_t* counters = nullptr;     // local connection step counters [ch][ctrKind][peer]
   void* peerStaging[NCCL_AMD_MAX_RANKS] = {};
   uint64_t* peerFlags[NCCL_AMD_MAX_RANKS] = {};
-  bool peerIsIpc[NCCL_AMD_MAX_RANKS] = {};
+  ncclamd::IpcImport peerStagingMap[NCCL_AMD_MAX_RANKS] = {};  // other-process peers' slabs as mapped here
+  ncclamd::IpcImport peerFlagsMap[NCCL_AMD_MAX_RANKS] = {};
+  ncclamd::FdServer* fdServer = nullptr;  // serves this rank's exports to other processes (ipc.cc)
   ncclamd::DevComm* devComm = nullptr;  // device copy of the DevComm struct
   ncclamd::DevComm hostDevComm;          // host mirror
   uint32_t* hostAbort = nullptr;         // pinned, mapped: host→device abort flag

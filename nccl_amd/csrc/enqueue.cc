@@ -109,6 +109,7 @@ void loadTuning(CommTuning* t) {
     }
   }
   t->symDisable = (int)paramInt("NCCL_AMD_SYM_DISABLE", 0);
+  t->symOneShot = (int)paramInt("NCCL_AMD_SYM_ONESHOT", 0);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
   t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks)
   t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)
@@ -191,9 +192,11 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
 }
 
 // LL eligibility and channel plan of one AllReduce, ReduceScatter, AllGather or Reduce (reference tuning: LL for
-// the smallest sizes, or as NCCL_PROTO dictates). Needs 8-byte aligned buffers (and, for the blocked
-// collectives, 8-byte aligned rank blocks) and room in the comm's line area. The payload space is the
-// AllReduce / Reduce buffer or one ReduceScatter / AllGather rank block; the size limit applies to it.
+// the smallest sizes, or as NCCL_PROTO dictates). Every rank must take the same decision from the same
+// inputs, so it depends only on what all ranks share — count, type, op and the agreed knobs — never on the
+// alignment of this rank's buffers (the kernel loads and stores payloads at any alignment). The blocked
+// collectives need 8-byte multiples as rank blocks (a payload never straddles two blocks) and the line area
+// must hold the payload space: the AllReduce / Reduce buffer or one ReduceScatter / AllGather rank block.
 bool llPlan(const CollInfo& info, LLOp* op) {
   ncclComm* comm = info.comm;
   if (comm->nRanks == 1) return false;
@@ -202,10 +205,9 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   const size_t bytes = info.count * (size_t)ts;  // payload space
   const size_t npk = (bytes + 7) / 8;
   const CommTuning& t = comm->tune;
-  bool al8 = ((((uintptr_t)info.sendbuff) | ((uintptr_t)info.recvbuff)) & 7) == 0;
   const bool blocked = info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER;
-  if (blocked) al8 = al8 && (bytes & 7) == 0;
-  const bool fits = t.llOn && al8 && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
+  const bool shape = !blocked || (bytes & 7) == 0;
+  const bool fits = t.llOn && shape && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
   // NCCL_PROTO leaves only LL enabled.
   // LL lines carry 2x the payload to each of the n-1 peers: its range shrinks with n like the one-shot's
@@ -227,6 +229,11 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   if (nch > comm->chanCap) nch = comm->chanCap;
   uint64_t part = (npk + nch - 1) / nch;
   if (part * 16 > comm->llBytes) return false;
+  // every channel of the op must carry at least one payload: an empty channel would advance its epoch
+  // without exchanging lines, and the parity double-buffering (kernels.h llChannelOp) relies on each epoch
+  // of a channel waiting for every peer's lines of the previous one (a tuner's channel count, or a tiny
+  // NCCL_AMD_LL_CHANNEL_BYTES, can leave [lo,hi) empty for the last channels otherwise)
+  nch = (int)((npk + part - 1) / part);
   const uint64_t epp = 16 / ts;
   uint64_t blockElems = info.count;
   if (info.func == FUNC_ALLREDUCE) {
@@ -419,9 +426,16 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
       size_t minPart = (size_t)comm->tune.minChannelBytes;
       int maxCh = comm->chanCap;
       if (info.func == FUNC_ALLREDUCE) {
-        // one-shot needs out-of-place buffers: in place, peers would still read what this rank overwrites
+        // One-shot needs out-of-place buffers on EVERY rank (in place, peers would still read what a rank
+        // overwrites), and whether a peer runs in place is not known here: ranks choosing different kernels
+        // would run different handshake sequences. So one-shot only when NCCL_AMD_SYM_ONESHOT=1 declares
+        // every call out of place; the default two-shot kernel is correct either way.
         bool out = info.sendbuff != info.recvbuff;
-        sp.coll = (oneShotAR && out) ? 1 /*SYM_AR1*/ : 0 /*SYM_AR*/;
+        if (comm->tune.symOneShot && !out) {
+          WARN("%s: NCCL_AMD_SYM_ONESHOT=1 but the call is in place", info.opName);
+          return ncclInvalidUsage;
+        }
+        sp.coll = (oneShotAR && comm->tune.symOneShot) ? 1 /*SYM_AR1*/ : 0 /*SYM_AR*/;
         if (sp.coll == 1) {
           spanBytes = count * ts;
           minPart = (size_t)comm->tune.oneShotChannelBytes;

@@ -18,6 +18,7 @@
 
 namespace ncclamd {
 ncclResult_t exportHandles(ncclComm* comm, PeerInfo* info);
+void unexportHandles(ncclComm* comm);
 
 ncclResult_t commCheck(const ncclComm* comm, const char* opname, const char* what) {
   if (comm == nullptr) {
@@ -44,19 +45,18 @@ static uint64_t hostHash() {
   return h;
 }
 
-// Hard cap on one rank's staging slab (one IPC-exported allocation): on this platform (ROCm 7.2, dmabuf
-// IPC) importing a peer's 2 GiB uncached slab blocked hipIpcOpenMemHandle forever in multi-process runs
-// (4 ranks, 512 KiB slots; 1 GiB slabs never did), so slot-size overrides that would exceed 1 GiB are
-// scaled down instead.
-// Every rank adopts rank 0's (already capped) shape.
+// Sanity cap on one rank's staging slab (NCCL_AMD_STAGING_CAP_MIB, default 8 GiB of the 288 GB): slot-size
+// overrides beyond it are scaled down with a warning. (Round 1 capped the slab at 1 GiB because importing a
+// 2 GiB slab hung; the cause was hipIpcOpenMemHandle in torch's bundled HIP runtime, which the dma-buf
+// transport of ipc.cc no longer uses — DESIGN.md §3.) Every rank adopts rank 0's (already capped) shape.
 static void clampStaging(ncclComm* c, int nranks) {
-  const int64_t cap = (int64_t)1 << 30;
+  const int64_t cap = paramInt("NCCL_AMD_STAGING_CAP_MIB", 8192) << 20;
   const int64_t per = (int64_t)c->maxChannels * 2 * c->nSlots * (nranks > 1 ? nranks : 2);
   if ((int64_t)c->slotBytes * per <= cap) return;
   int64_t sb = cap / per / 4096 * 4096;
   if (sb < 4096) sb = 4096;
-  WARN("staging slab %lld MiB exceeds the 1 GiB cap: slot size %zu -> %lld bytes",
-       (long long)(((int64_t)c->slotBytes * per) >> 20), c->slotBytes, (long long)sb);
+  WARN("staging slab %lld MiB exceeds the %lld MiB cap: slot size %zu -> %lld bytes",
+       (long long)(((int64_t)c->slotBytes * per) >> 20), (long long)(cap >> 20), c->slotBytes, (long long)sb);
   c->slotBytes = (size_t)sb;
 }
 
@@ -149,7 +149,7 @@ static void computeChannelCap(ncclComm* c) {
 
 // Shape parameters every rank must agree on (exchanged with the PeerInfo block).
 struct ShapeInfo {
-  int maxChannels, nSlots;
+  int maxChannels, minChannels, nSlots;
   uint64_t slotBytes;
   CommTuning tune;
 };
@@ -168,12 +168,15 @@ static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id
   // Agree on the channel/slot shape and the tuning knobs: rank 0's parameters win (env may differ).
   {
     std::vector<ShapeInfo> shapes(nranks);
-    shapes[rank] = {comm->maxChannels, comm->nSlots, comm->slotBytes, comm->tune};
+    shapes[rank] = {comm->maxChannels, comm->minCTAs, comm->nSlots, comm->slotBytes, comm->tune};
     if ((res = bootstrapAllGather(comm->bootstrap, shapes.data(), sizeof(ShapeInfo))) != ncclSuccess) goto fail;
     comm->maxChannels = comm->maxCTAs = shapes[0].maxChannels;
     comm->nSlots = shapes[0].nSlots;
     comm->slotBytes = shapes[0].slotBytes;
     comm->tune = shapes[0].tune;
+    // minCTAs raises every plan's channel count (planChannels), so it must agree too: a rank planning more
+    // channels than its peers would wait on channels that never arrive
+    comm->minCTAs = shapes[0].minChannels;
     if (comm->minCTAs > comm->maxCTAs) comm->minCTAs = comm->maxCTAs;
   }
   if ((res = transportSetup(comm)) != ncclSuccess) goto fail;
@@ -190,6 +193,7 @@ static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id
   TRACE("rank %d: device state ready", rank);
   if ((res = tunerLoad(comm)) != ncclSuccess) goto fail;
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
+  unexportHandles(comm);  // every peer has mapped our slab and flags
   INFO("comm %p rank %d nRanks %d dev %d busId %s - Init COMPLETE", (void*)comm, rank, nranks, dev,
        comm->peers[rank].busId);
   return ncclSuccess;

@@ -1,0 +1,297 @@
+// ipc.cc — sharing device memory with the other processes of a communicator (staging slabs, flag blocks,
+// registered windows).
+//
+// Reference: src/transport/p2p.cc:220-325 exports each buffer as a cuMem POSIX file descriptor and hands the
+// fd to the peer over a UNIX socket (its proxy thread), instead of legacy cudaIpc handles. This is the same
+// design on HIP: the exporter turns the allocation into a dma-buf fd (hipMemGetHandleForAddressRange), a
+// per-communicator fd server passes it to each importing peer over an abstract UNIX socket (SCM_RIGHTS),
+// and the importer maps it with hipImportExternalMemory + hipExternalMemoryGetMappedBuffer.
+//
+// Why not hipIpcGetMemHandle / hipIpcOpenMemHandle: inside any process that imports torch, this library
+// binds to torch's bundled HIP runtime (torch/lib/libamdhip64.so, ROCm 7.0 in this image; same soname,
+// loaded first), and there hipIpcOpenMemHandle of an allocation of 2 GiB or more never returns (the
+// importing thread spins in user space), for hipMalloc and uncached memory alike. The dma-buf path maps
+// 1-3 GiB allocations on both that runtime and /opt/rocm 7.2 (scripts/ipc_paths_torchrt.py,
+// tests/native/ipc_paths_probe.hip). NCCL_AMD_IPC=legacy keeps the hipIpc path for
+// comparison and refuses allocations of 2 GiB or more on runtimes older than 7.2 instead of hanging.
+//
+// Every socket operation is bounded (NCCL_AMD_IPC_TIMEOUT_MS): an import whose exporter died or never
+// published returns ncclSystemError / ncclRemoteError rather than blocking the caller.
+#include <errno.h>
+#include <fcntl.h>
+#include <poll.h>
+#include <string.h>
+#include <sys/socket.h>
+#include <sys/un.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <map>
+#include <mutex>
+#include <thread>
+
+#include "core.h"
+
+namespace ncclamd {
+
+struct FdServer {
+  int listenFd = -1;
+  int wakePipe[2] = {-1, -1};
+  std::thread thread;
+  std::mutex mu;
+  std::map<uint64_t, int> table;  // key -> exported dma-buf fd
+  char name[40] = {};  // fits IpcDesc::server
+};
+
+static std::atomic<uint64_t> gServerSerial{0};
+static std::atomic<uint64_t> gKeySerial{1};
+
+static int64_t ipcTimeoutMs() { return paramInt("NCCL_AMD_IPC_TIMEOUT_MS", 60000); }
+
+bool ipcLegacy() {
+  const char* m = paramStr("NCCL_AMD_IPC");
+  return m && !strcasecmp(m, "legacy");
+}
+
+static socklen_t abstractAddr(const char* name, struct sockaddr_un* a) {
+  memset(a, 0, sizeof(*a));
+  a->sun_family = AF_UNIX;
+  size_t n = strlen(name);
+  memcpy(a->sun_path + 1, name, n);  // abstract namespace: leading NUL, nothing on the filesystem
+  return (socklen_t)(offsetof(struct sockaddr_un, sun_path) + 1 + n);
+}
+
+static void setTimeouts(int fd) {
+  int64_t ms = ipcTimeoutMs();
+  struct timeval tv = {(time_t)(ms / 1000), (suseconds_t)((ms % 1000) * 1000)};
+  setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
+  setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
+}
+
+// One request per connection: the client sends an 8-byte key; the server answers {status, 0} with the
+// fd attached (SCM_RIGHTS) when the key is published and the client runs under our uid.
+static void serveOne(FdServer* s, int c) {
+  setTimeouts(c);
+  struct ucred cred;
+  socklen_t cl = sizeof(cred);
+  uint64_t key = 0;
+  int32_t reply[2] = {-1, 0};
+  int fd = -1;
+  if (getsockopt(c, SOL_SOCKET, SO_PEERCRED, &cred, &cl) == 0 && cred.uid == getuid() &&
+      recv(c, &key, sizeof(key), MSG_WAITALL) == (ssize_t)sizeof(key)) {
+    std::lock_guard<std::mutex> g(s->mu);
+    auto it = s->table.find(key);
+    if (it != s->table.end()) {
+      fd = it->second;
+      reply[0] = 0;
+    }
+  }
+  struct msghdr m = {};
+  struct iovec io = {reply, sizeof(reply)};
+  m.msg_iov = &io;
+  m.msg_iovlen = 1;
+  char ctl[CMSG_SPACE(sizeof(int))] = {};
+  if (fd >= 0) {
+    m.msg_control = ctl;
+    m.msg_controllen = sizeof(ctl);
+    struct cmsghdr* h = CMSG_FIRSTHDR(&m);
+    h->cmsg_level = SOL_SOCKET;
+    h->cmsg_type = SCM_RIGHTS;
+    h->cmsg_len = CMSG_LEN(sizeof(int));
+    memcpy(CMSG_DATA(h), &fd, sizeof(int));
+  }
+  (void)sendmsg(c, &m, MSG_NOSIGNAL);
+  close(c);
+}
+
+static void serverLoop(FdServer* s) {
+  while (true) {
+    struct pollfd p[2] = {{s->listenFd, POLLIN, 0}, {s->wakePipe[0], POLLIN, 0}};
+    int r = poll(p, 2, -1);
+    if (r < 0 && errno == EINTR) continue;
+    if (r < 0 || (p[1].revents & (POLLIN | POLLHUP))) break;
+    if (p[0].revents & POLLIN) {
+      int c = accept(s->listenFd, nullptr, nullptr);
+      if (c >= 0) serveOne(s, c);
+    }
+  }
+}
+
+ncclResult_t ipcServerStart(ncclComm* comm) {
+  if (comm->fdServer || ipcLegacy()) return ncclSuccess;
+  FdServer* s = new FdServer();
+  snprintf(s->name, sizeof(s->name), "ncclamd.%d.%llu", (int)getpid(), (unsigned long long)gServerSerial++);
+  s->listenFd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  struct sockaddr_un a;
+  socklen_t al = abstractAddr(s->name, &a);
+  if (s->listenFd < 0 || bind(s->listenFd, (struct sockaddr*)&a, al) != 0 || listen(s->listenFd, 64) != 0 ||
+      pipe2(s->wakePipe, O_CLOEXEC) != 0) {
+    WARN("ipc: fd server %s: %s", s->name, strerror(errno));
+    if (s->listenFd >= 0) close(s->listenFd);
+    delete s;
+    return ncclSystemError;
+  }
+  s->thread = std::thread(serverLoop, s);
+  comm->fdServer = s;
+  TRACE("rank %d: fd server %s", comm->rank, s->name);
+  return ncclSuccess;
+}
+
+void ipcServerStop(ncclComm* comm) {
+  FdServer* s = comm->fdServer;
+  if (!s) return;
+  if (s->wakePipe[1] >= 0) (void)!write(s->wakePipe[1], "x", 1);
+  if (s->thread.joinable()) s->thread.join();
+  for (auto& kv : s->table) close(kv.second);
+  close(s->listenFd);
+  close(s->wakePipe[0]);
+  close(s->wakePipe[1]);
+  delete s;
+  comm->fdServer = nullptr;
+}
+
+static int runtimeVersion() {
+  int v = 0;
+  (void)hipRuntimeGetVersion(&v);
+  return v;  // major * 10000000 + minor * 100000 + patch
+}
+
+ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
+  memset(d, 0, sizeof(*d));
+  d->size = size;
+  if (ipcLegacy()) {
+    if (size >= ((size_t)2 << 30) && runtimeVersion() < 70200000) {
+      // torch's bundled ROCm 7.0 runtime never returns from hipIpcOpenMemHandle at this size (ipc.cc header)
+      WARN("ipc: a %zu MiB allocation cannot be shared with NCCL_AMD_IPC=legacy on HIP runtime %d "
+           "(hipIpcOpenMemHandle stalls at >= 2 GiB); use the default dma-buf path", size >> 20, runtimeVersion());
+      return ncclSystemError;
+    }
+    d->legacy = 1;
+    HIPCHECK(hipIpcGetMemHandle(&d->handle, base));
+    return ncclSuccess;
+  }
+  FdServer* s = comm->fdServer;
+  if (!s) {
+    WARN("ipc: no fd server on rank %d", comm->rank);
+    return ncclInternalError;
+  }
+  int fd = -1;
+  HIPCHECK(hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0));
+  d->key = gKeySerial++;
+  memcpy(d->server, s->name, sizeof(d->server));
+  std::lock_guard<std::mutex> g(s->mu);
+  s->table[d->key] = fd;
+  return ncclSuccess;
+}
+
+// Stop serving an export (every peer has imported it: its mapping keeps the memory referenced).
+void ipcUnexport(ncclComm* comm, const IpcDesc& d) {
+  FdServer* s = comm->fdServer;
+  if (d.legacy || !s) return;
+  std::lock_guard<std::mutex> g(s->mu);
+  auto it = s->table.find(d.key);
+  if (it == s->table.end()) return;
+  close(it->second);
+  s->table.erase(it);
+}
+
+static ncclResult_t fetchFd(const IpcDesc& d, int* out) {
+  struct sockaddr_un a;
+  socklen_t al = abstractAddr(d.server, &a);
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ipcTimeoutMs());
+  int c = -1;
+  while (true) {
+    c = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    SYSCHECK(c >= 0, "socket");
+    if (connect(c, (struct sockaddr*)&a, al) == 0) break;
+    int err = errno;
+    close(c);
+    if (std::chrono::steady_clock::now() > deadline) {
+      WARN("ipc: connect to %s failed: %s", d.server, strerror(err));
+      return ncclRemoteError;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  setTimeouts(c);
+  int32_t reply[2] = {-1, 0};
+  struct msghdr m = {};
+  struct iovec io = {reply, sizeof(reply)};
+  m.msg_iov = &io;
+  m.msg_iovlen = 1;
+  char ctl[CMSG_SPACE(sizeof(int))] = {};
+  m.msg_control = ctl;
+  m.msg_controllen = sizeof(ctl);
+  int fd = -1;
+  if (send(c, &d.key, sizeof(d.key), MSG_NOSIGNAL) == (ssize_t)sizeof(d.key) &&
+      recvmsg(c, &m, MSG_WAITALL | MSG_CMSG_CLOEXEC) == (ssize_t)sizeof(reply) && reply[0] == 0) {
+    for (struct cmsghdr* h = CMSG_FIRSTHDR(&m); h; h = CMSG_NXTHDR(&m, h))
+      if (h->cmsg_level == SOL_SOCKET && h->cmsg_type == SCM_RIGHTS) memcpy(&fd, CMSG_DATA(h), sizeof(int));
+  }
+  close(c);
+  if (fd < 0) {
+    WARN("ipc: %s did not hand over export %llu (%s)", d.server, (unsigned long long)d.key,
+         reply[0] == 0 ? "no descriptor attached" : "unknown key, timeout or peer gone");
+    return ncclRemoteError;
+  }
+  *out = fd;
+  return ncclSuccess;
+}
+
+ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
+  memset(out, 0, sizeof(*out));
+  if (d.legacy) {
+    HIPCHECK(hipIpcOpenMemHandle(&out->ptr, d.handle, hipIpcMemLazyEnablePeerAccess));
+    out->legacy = 1;
+    return ncclSuccess;
+  }
+  int fd = -1;
+  NCCLCHECK(fetchFd(d, &fd));
+  hipExternalMemoryHandleDesc hd;
+  memset(&hd, 0, sizeof(hd));
+  hd.type = hipExternalMemoryHandleTypeOpaqueFd;
+  hd.handle.fd = fd;
+  hd.size = d.size;
+  hipExternalMemory_t em = nullptr;
+  hipError_t e = hipImportExternalMemory(&em, &hd);
+  if (e != hipSuccess) {
+    close(fd);
+    WARN("ipc: hipImportExternalMemory(%zu MiB): %s", (size_t)(d.size >> 20), hipGetErrorString(e));
+    return ncclUnhandledCudaError;
+  }
+  // Descriptor ownership: kept until the mapping is released (ipcRelease), then closed if the runtime has
+  // not closed it itself (the runtime's behaviour is logged at TRACE level)
+  TRACE("ipc: imported %zu MiB from %s (fd %d %s after import)", (size_t)(d.size >> 20), d.server, fd,
+        fcntl(fd, F_GETFD) != -1 ? "open" : "closed by the runtime");
+  out->fd = fd;
+  hipExternalMemoryBufferDesc bd;
+  memset(&bd, 0, sizeof(bd));
+  bd.offset = 0;
+  bd.size = d.size;
+  void* p = nullptr;
+  e = hipExternalMemoryGetMappedBuffer(&p, em, &bd);
+  if (e != hipSuccess) {
+    (void)hipDestroyExternalMemory(em);
+    WARN("ipc: hipExternalMemoryGetMappedBuffer: %s", hipGetErrorString(e));
+    return ncclUnhandledCudaError;
+  }
+  out->ptr = p;
+  out->ext = em;
+  return ncclSuccess;
+}
+
+void ipcRelease(IpcImport* m) {
+  if (!m->ptr) return;
+  if (m->legacy) {
+    (void)hipIpcCloseMemHandle(m->ptr);
+  } else {
+    (void)hipFree(m->ptr);
+    (void)hipDestroyExternalMemory((hipExternalMemory_t)m->ext);
+    const bool open = m->fd >= 0 && fcntl(m->fd, F_GETFD) != -1;
+    TRACE("ipc: released mapping (fd %d %s)", m->fd, open ? "open: closing it" : "closed by the runtime");
+    if (open) close(m->fd);
+  }
+  memset(m, 0, sizeof(*m));
+}
+
+}  // namespace ncclamd

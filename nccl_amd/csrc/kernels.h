@@ -643,15 +643,36 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
   const uint64_t lo = min((uint64_t)j * op.part, npk), hi = min(lo + op.part, npk);
   const char* send = (const char*)op.send;
   char* recv = (char*)op.recv;
+  // Payloads are 8 bytes of the user buffer at any alignment: the LL decision is rank-uniform (enqueue.cc
+  // llPlan), so a buffer that is only 4-, 2- or 1-byte aligned on some rank still takes this path there.
   auto payload = [&](const char* base, uint64_t pk) -> uint64_t {
+    const char* p = base + pk * 8;
+    const uintptr_t al = (uintptr_t)p;
     uint64_t v = 0;
-    if (pk * 8 + 8 <= nbytes) v = *(const uint64_t*)(base + pk * 8);
-    else for (uint64_t b = pk * 8; b < nbytes; b++) v |= (uint64_t)(unsigned char)base[b] << (8 * (b - pk * 8));
+    if (pk * 8 + 8 <= nbytes) {
+      if ((al & 7) == 0) v = *(const uint64_t*)p;
+      else if ((al & 3) == 0) v = ((const uint32_t*)p)[0] | ((uint64_t)((const uint32_t*)p)[1] << 32);
+      else for (int b = 0; b < 8; b++) v |= (uint64_t)(unsigned char)p[b] << (8 * b);
+    } else {
+      for (uint64_t b = pk * 8; b < nbytes; b++) v |= (uint64_t)(unsigned char)base[b] << (8 * (b - pk * 8));
+    }
     return v;
   };
   auto storePayload = [&](char* base, uint64_t pk, uint64_t v) {
-    if (pk * 8 + 8 <= nbytes) *(uint64_t*)(base + pk * 8) = v;
-    else for (uint64_t b = pk * 8; b < nbytes; b++) base[b] = (char)(v >> (8 * (b - pk * 8)));
+    char* p = base + pk * 8;
+    const uintptr_t al = (uintptr_t)p;
+    if (pk * 8 + 8 <= nbytes) {
+      if ((al & 7) == 0) {
+        *(uint64_t*)p = v;
+      } else if ((al & 3) == 0) {
+        ((uint32_t*)p)[0] = (uint32_t)v;
+        ((uint32_t*)p)[1] = (uint32_t)(v >> 32);
+      } else {
+        for (int b = 0; b < 8; b++) p[b] = (char)(v >> (8 * b));
+      }
+    } else {
+      for (uint64_t b = pk * 8; b < nbytes; b++) base[b] = (char)(v >> (8 * (b - pk * 8)));
+    }
   };
 
   // send: payloads [lo,hi) to every peer, 16-byte lines (two 8-byte payloads per thread step)

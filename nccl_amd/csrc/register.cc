@@ -9,8 +9,8 @@
 // exchange data through the comm's own uncached staging), so there is nothing to map: the call
 // validates and records the buffer and returns a handle, like the reference does when local
 // registration is disabled (register.cc:156-159). Zero-copy is what windows are for:
-// ncclCommWindowRegister maps every peer's buffer into this process (HIP IPC across processes, the raw
-// pointer inside one process) and collectives whose buffers lie in NCCL_WIN_COLL_SYMMETRIC windows
+// ncclCommWindowRegister maps every peer's buffer into this process (a dma-buf fd across processes, ipc.cc;
+// the raw pointer inside one process) and collectives whose buffers lie in NCCL_WIN_COLL_SYMMETRIC windows
 // run the symmetric kernels (kernels.h symKernel), which read peers' windows directly.
 #include <string.h>
 #include <unistd.h>
@@ -35,20 +35,20 @@ struct WinInfo {  // exchanged by ncclCommWindowRegister
   uint64_t ptr;      // user pointer (valid in the owner's process)
   uint64_t base;     // its allocation's base
   uint64_t size;
-  hipIpcMemHandle_t handle;  // of the allocation base
+  IpcDesc desc;      // the whole allocation, exported to other processes (ipc.cc)
 };
 
 static ncclResult_t ipcMap(ncclComm* comm, int peer, const WinInfo& w, char** out) {
   for (IpcMapping& m : comm->ipcMaps)
     if (m.peer == peer && m.base == w.base) {
       m.refs++;
-      *out = (char*)m.mapped + (w.ptr - w.base);
+      *out = (char*)m.map.ptr + (w.ptr - w.base);
       return ncclSuccess;
     }
-  void* p = nullptr;
-  HIPCHECK(hipIpcOpenMemHandle(&p, w.handle, hipIpcMemLazyEnablePeerAccess));
-  comm->ipcMaps.push_back({peer, w.base, p, 1});
-  *out = (char*)p + (w.ptr - w.base);
+  IpcMapping m = {peer, w.base, {}, 1};
+  NCCLCHECK(ipcImport(w.desc, &m.map));
+  comm->ipcMaps.push_back(m);
+  *out = (char*)m.map.ptr + (w.ptr - w.base);
   return ncclSuccess;
 }
 
@@ -57,12 +57,14 @@ static void ipcUnmap(ncclComm* comm, int peer, uint64_t base) {
     IpcMapping& m = comm->ipcMaps[i];
     if (m.peer != peer || m.base != base) continue;
     if (--m.refs == 0) {
-      (void)hipIpcCloseMemHandle(m.mapped);
+      ipcRelease(&m.map);
       comm->ipcMaps.erase(comm->ipcMaps.begin() + i);
     }
     return;
   }
 }
+
+static void windowRelease(ncclComm* comm, ncclWindow_vidmem* w);
 
 static ncclResult_t windowRegister(ncclComm* comm, void* buff, size_t size, ncclWindow_t* win, int flags) {
   HIPCHECK(hipSetDevice(comm->device));
@@ -83,8 +85,15 @@ static ncclResult_t windowRegister(ncclComm* comm, void* buff, size_t size, nccl
   }
   bool needIpc = false;
   for (const PeerInfo& p : comm->peers) needIpc |= p.pid != me.pid;
-  if (needIpc) HIPCHECK(hipIpcGetMemHandle(&me.handle, (void*)base));
-  NCCLCHECK(commAllGather(comm, all.data(), sizeof(WinInfo)));
+  if (needIpc) {
+    NCCLCHECK(ipcServerStart(comm));
+    NCCLCHECK(ipcExport(comm, (void*)base, allocSize, &me.desc));
+  }
+  ncclResult_t gres = commAllGather(comm, all.data(), sizeof(WinInfo));
+  if (gres != ncclSuccess) {
+    if (needIpc) ipcUnexport(comm, me.desc);
+    return gres;
+  }
 
   ncclWindow_vidmem* w = new ncclWindow_vidmem();
   w->comm = comm;
@@ -107,10 +116,21 @@ static ncclResult_t windowRegister(ncclComm* comm, void* buff, size_t size, nccl
     if (res != ncclSuccess) {
       for (int q = 0; q < r; q++)
         if (w->peerBase[q]) ipcUnmap(comm, q, w->peerBase[q]);
+      if (needIpc) ipcUnexport(comm, me.desc);
       delete w;
       return res;
     }
     w->peerBase[r] = p.base;
+  }
+  if (needIpc) {
+    // every peer has mapped my allocation (its mapping keeps it referenced): stop serving the descriptor
+    std::vector<char> sync(comm->nRanks);
+    ncclResult_t bres = commAllGather(comm, sync.data(), 1);
+    ipcUnexport(comm, me.desc);
+    if (bres != ncclSuccess) {
+      windowRelease(comm, w);
+      return bres;
+    }
   }
   comm->windows.push_back(w);
   *win = w;
@@ -137,7 +157,7 @@ void windowsFree(ncclComm* comm) {
   (void)hipSetDevice(comm->device);
   for (ncclWindow_vidmem* w : comm->windows) windowRelease(comm, w);
   comm->windows.clear();
-  for (IpcMapping& m : comm->ipcMaps) (void)hipIpcCloseMemHandle(m.mapped);
+  for (IpcMapping& m : comm->ipcMaps) ipcRelease(&m.map);
   comm->ipcMaps.clear();
   for (void* h : comm->regHandles) free(h);
   comm->regHandles.clear();

@@ -7,7 +7,8 @@
 // each rank allocates ONE staging slab and ONE flag block that ALL peers write into (full mesh), and
 // maps every peer's slab once at init:
 //   - same process (ncclCommInitAll / threads): raw pointer + hipDeviceEnablePeerAccess;
-//   - other process: hipIpcGetMemHandle / hipIpcOpenMemHandle (dmabuf IPC on this platform).
+//   - other process: a dma-buf fd handed over by the exporter's fd server and mapped with
+//     hipImportExternalMemory (ipc.cc; the reference's cuMem fd path, p2p.cc:220-325).
 // Staging and flags are allocated UNCACHED (hipDeviceMallocUncached): they are written by remote
 // GPUs over xGMI and read locally, so no L2 anywhere may hold a stale copy.
 #include <string.h>
@@ -32,7 +33,10 @@ ncclResult_t transportSetup(ncclComm* comm) {
   HIPCHECK(hipSetDevice(comm->device));
   if (comm->nRanks == 1) return ncclSuccess;  // nranks==1 never touches peers (onerank.cu:49-110)
   size_t sb = stagingBytes(comm), fb = flagsBytes(comm);
-  HIPCHECK(hipExtMallocWithFlags(&comm->staging, sb, hipDeviceMallocUncached));
+  if (paramInt("NCCL_AMD_STAGING_PLAIN", 0))  // diagnostics only (scripts/ipc_hang_diag.py): cached staging
+    HIPCHECK(hipMalloc(&comm->staging, sb));
+  else
+    HIPCHECK(hipExtMallocWithFlags(&comm->staging, sb, hipDeviceMallocUncached));
   HIPCHECK(hipExtMallocWithFlags((void**)&comm->flags, fb, hipDeviceMallocUncached));
   HIPCHECK(hipMemset(comm->flags, 0, fb));
   HIPCHECK(hipDeviceSynchronize());
@@ -44,6 +48,9 @@ ncclResult_t transportSetup(ncclComm* comm) {
 ncclResult_t transportConnect(ncclComm* comm) {
   if (comm->nRanks == 1) return ncclSuccess;
   HIPCHECK(hipSetDevice(comm->device));
+  // diagnostics (scripts/ipc_hang_diag.py): NCCL_AMD_IMPORT_SERIAL=1 lets one rank at a time import
+  const bool serial = comm->bootstrap && paramInt("NCCL_AMD_IMPORT_SERIAL", 0);
+  for (int turn = 0; serial && turn < comm->rank; turn++) NCCLCHECK(bootstrapBarrier(comm->bootstrap));
   const PeerInfo& me = comm->peers[comm->rank];
   for (int r = 0; r < comm->nRanks; r++) {
     const PeerInfo& p = comm->peers[r];
@@ -74,19 +81,17 @@ ncclResult_t transportConnect(ncclComm* comm) {
       }
       comm->peerStaging[r] = (void*)p.stagingPtr;
       comm->peerFlags[r] = (uint64_t*)p.flagsPtr;
-      comm->peerIsIpc[r] = false;
     } else {
-      void* s = nullptr;
-      void* f = nullptr;
-      TRACE("rank %d: importing rank %d's staging", comm->rank, r);
-      HIPCHECK(hipIpcOpenMemHandle(&s, p.stagingHandle, hipIpcMemLazyEnablePeerAccess));
+      TRACE("rank %d: importing rank %d's staging (%zu MiB)", comm->rank, r, (size_t)(p.stagingDesc.size >> 20));
+      NCCLCHECK(ipcImport(p.stagingDesc, &comm->peerStagingMap[r]));
       TRACE("rank %d: importing rank %d's flags", comm->rank, r);
-      HIPCHECK(hipIpcOpenMemHandle(&f, p.flagsHandle, hipIpcMemLazyEnablePeerAccess));
-      comm->peerStaging[r] = s;
-      comm->peerFlags[r] = (uint64_t*)f;
-      comm->peerIsIpc[r] = true;
+      NCCLCHECK(ipcImport(p.flagsDesc, &comm->peerFlagsMap[r]));
+      TRACE("rank %d: rank %d mapped", comm->rank, r);
+      comm->peerStaging[r] = comm->peerStagingMap[r].ptr;
+      comm->peerFlags[r] = (uint64_t*)comm->peerFlagsMap[r].ptr;
     }
   }
+  for (int turn = comm->rank; serial && turn < comm->nRanks; turn++) NCCLCHECK(bootstrapBarrier(comm->bootstrap));
   return ncclSuccess;
 }
 
@@ -123,14 +128,12 @@ ncclResult_t transportDrainCredits(ncclComm* comm) {
 ncclResult_t transportFree(ncclComm* comm) {
   (void)hipSetDevice(comm->device);
   for (int r = 0; r < comm->nRanks && r < NCCL_AMD_MAX_RANKS; r++) {
-    if (comm->peerIsIpc[r]) {
-      if (comm->peerStaging[r]) (void)hipIpcCloseMemHandle(comm->peerStaging[r]);
-      if (comm->peerFlags[r]) (void)hipIpcCloseMemHandle(comm->peerFlags[r]);
-    }
+    ipcRelease(&comm->peerStagingMap[r]);
+    ipcRelease(&comm->peerFlagsMap[r]);
     comm->peerStaging[r] = nullptr;
     comm->peerFlags[r] = nullptr;
-    comm->peerIsIpc[r] = false;
   }
+  ipcServerStop(comm);
   if (comm->staging) (void)hipFree(comm->staging);
   if (comm->flags) (void)hipFree(comm->flags);
   if (comm->counters) (void)hipFree(comm->counters);
@@ -209,15 +212,25 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
   return ncclSuccess;
 }
 
+// Export the slab and the flag block to other processes (only communicators built by ncclCommInitRank
+// can have peers in other processes; ncclCommInitAll clique members share this process).
 ncclResult_t exportHandles(ncclComm* comm, PeerInfo* info) {
-  memset(&info->stagingHandle, 0, sizeof(info->stagingHandle));
-  memset(&info->flagsHandle, 0, sizeof(info->flagsHandle));
+  memset(&info->stagingDesc, 0, sizeof(info->stagingDesc));
+  memset(&info->flagsDesc, 0, sizeof(info->flagsDesc));
   info->stagingPtr = (uint64_t)comm->staging;
   info->flagsPtr = (uint64_t)comm->flags;
-  if (comm->nRanks == 1) return ncclSuccess;
-  HIPCHECK(hipIpcGetMemHandle(&info->stagingHandle, comm->staging));
-  HIPCHECK(hipIpcGetMemHandle(&info->flagsHandle, comm->flags));
+  if (comm->nRanks == 1 || !comm->bootstrap) return ncclSuccess;
+  NCCLCHECK(ipcServerStart(comm));
+  NCCLCHECK(ipcExport(comm, comm->staging, stagingBytes(comm), &info->stagingDesc));
+  NCCLCHECK(ipcExport(comm, comm->flags, flagsBytes(comm), &info->flagsDesc));
   return ncclSuccess;
+}
+
+// Every peer has mapped our slab and flags (called after the init barrier): stop serving them.
+void unexportHandles(ncclComm* comm) {
+  if (comm->peers.empty()) return;
+  ipcUnexport(comm, comm->peers[comm->rank].stagingDesc);
+  ipcUnexport(comm, comm->peers[comm->rank].flagsDesc);
 }
 
 }  // namespace ncclamd

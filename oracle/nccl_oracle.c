@@ -334,6 +334,8 @@ int oracle_all_reduce(int dt, int devop, uint64_t arg, int n, const void* const*
   size_t epp = (size_t)(16 / ts);
   size_t rc = (count + n - 1) / n;
   rc = (rc + epp - 1) / epp * epp;
+  /* elements are independent: OpenMP over them keeps full-config sizes (C2..C5) checkable in seconds */
+#pragma omp parallel for schedule(static)
   for (size_t i = 0; i < count; i++) {
     int owner = (int)(i / rc);
     st(dt, out, i, fold_elem(dt, devop, arg, n, in, i, (owner + 1) % n));
@@ -345,15 +347,18 @@ int oracle_all_reduce(int dt, int devop, uint64_t arg, int n, const void* const*
 int oracle_reduce_scatter(int dt, int devop, uint64_t arg, int n, const void* const* in, size_t recvcount,
                           void* const* out) {
   if (oracle_type_size(dt) <= 0 || n <= 0) return 4;
-  for (int d = 0; d < n; d++)
+  for (int d = 0; d < n; d++) {
+#pragma omp parallel for schedule(static)
     for (size_t j = 0; j < recvcount; j++)
       st(dt, out[d], j, fold_elem(dt, devop, arg, n, in, (size_t)d * recvcount + j, (d + 1) % n));
+  }
   return 0;
 }
 
 /* Reduce to root: chain root+1 -> ... -> root (reduce.h:34-52). */
 int oracle_reduce(int dt, int devop, uint64_t arg, int n, int root, const void* const* in, size_t count, void* out) {
   if (oracle_type_size(dt) <= 0 || n <= 0 || root < 0 || root >= n) return 4;
+#pragma omp parallel for schedule(static)
   for (size_t i = 0; i < count; i++) st(dt, out, i, fold_elem(dt, devop, arg, n, in, i, (root + 1) % n));
   return 0;
 }
@@ -371,6 +376,7 @@ static inline uint64_t splitmix64(uint64_t x) {
  *         with INT_MIN/INT_MAX-style extremes at i%1024==1 / ==2);
  * kind 1: dyadic k/256 with |k| <= 1024 (exact sums for fp32 up to 2^14 terms). */
 void oracle_fill(int dt, uint64_t seed, size_t count, void* out, int kind) {
+#pragma omp parallel for schedule(static)
   for (size_t i = 0; i < count; i++) {
     uint64_t r = splitmix64(seed * 0x100000001b3ull ^ (uint64_t)i);
     if (is_int(dt)) {

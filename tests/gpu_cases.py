@@ -107,8 +107,11 @@ def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=
     es = np.dtype(npdt).itemsize
     ocount = out_count(coll, n, count)
     keep, views = [], []
+    per_rank = misalign if isinstance(misalign, (list, tuple)) else None
     for comm, stream in comms_and_streams:
         r = comm.rank
+        if per_rank is not None:  # each rank's buffers misaligned differently (protocol choice must not care)
+            misalign = per_rank[r % len(per_rank)]
         dev = torch.device("cuda", comm.device)
         with torch.cuda.device(dev):
             if inplace:

@@ -463,3 +463,26 @@ def test_fuzz_short(built):
                          capture_output=True, text=True, timeout=180)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-2000:]
     assert "FUZZ OK" in out.stdout
+
+
+def test_rank_dependent_misalignment(built):
+    """Ranks whose buffers are aligned differently must still pick the same protocol and batch (ADVICE r1:
+    LL eligibility used to follow each rank's own alignment, so ranks could launch different kernels and
+    spin until the timeout). 3 ranks in one process, offsets 0 / 1 / 3 elements, LL and staged sizes."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0, 0])
+    cs = list(zip(comms, [torch.cuda.Stream() for _ in comms]))
+    errs = []
+    for i, (coll, dt, op, count) in enumerate([("allreduce", 7, 0, 1001), ("allreduce", 9, 2, 40_003),
+                                               ("allreduce", 6, 0, 3), ("reduce", 2, 3, 5_001),
+                                               ("reducescatter", 7, 0, 3 * 2_000), ("allgather", 8, 0, 1_000),
+                                               ("allreduce", 7, 0, 700_001), ("reducescatter", 0, 1, 3 * 300)]):
+        for mis in ([0, 1, 3], [3, 0, 1], [1, 1, 0]):
+            errs += G.run_case(cs, coll, dt, op, count, list(mis), seed=100 + i, root=i % 3)
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])

@@ -1,6 +1,6 @@
 """GPU parity tests of the symmetric-window (zero-copy) kernels: ncclCommWindowRegister with
-NCCL_WIN_COLL_SYMMETRIC, then AllReduce (two-shot and one-shot), ReduceScatter and AllGather whose buffers
-lie in the windows run kernels.h symKernel, which pulls peers' buffers directly. Results must be
+NCCL_WIN_COLL_SYMMETRIC, then AllReduce (two-shot; one-shot when NCCL_AMD_SYM_ONESHOT=1 promises every call
+is out of place), ReduceScatter and AllGather whose buffers lie in the windows run kernels.h symKernel, which pulls peers' buffers directly. Results must be
 bit-identical to the oracle (same fold order as the staged path). Reduce and non-symmetric windows fall
 back to the staged path. All ranks share the box's one GPU (single process: raw pointers; multi-process:
 HIP IPC of the window allocations)."""
@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True)
 def _no_ll(monkeypatch):
     """Small AllReduce would take the LL protocol (which needs no window); exclude it so the symmetric
-    one-shot kernel is what these tests exercise."""
+    kernels are what these tests exercise."""
     monkeypatch.setenv("NCCL_PROTO", "^LL")
 
 WIN_BYTES = 8 << 20          # per-rank window; send at [0, half), recv at [half, WIN_BYTES)
@@ -120,11 +120,13 @@ def _windows(comms, streams_dev=0):
     return bufs, wins
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_windows_single_process(built, nranks):
+@pytest.mark.parametrize("nranks,oneshot", [(2, False), (3, False), (2, True)])
+def test_windows_single_process(built, nranks, oneshot, monkeypatch):
     import torch
     import nccl_amd
     os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    if oneshot:  # the one-shot window kernel: a rank-uniform promise that every AllReduce is out of place
+        monkeypatch.setenv("NCCL_AMD_SYM_ONESHOT", "1")
     torch.cuda.set_device(0)
     comms = nccl_amd.Communicator.init_all([0] * nranks)
     streams = [torch.cuda.Stream() for _ in range(nranks)]
@@ -133,6 +135,8 @@ def test_windows_single_process(built, nranks):
     bases = [(b, b.data_ptr()) for b in bufs]
     errs = []
     for i, case in enumerate(_cases(nranks, quick=nranks > 2)):
+        if oneshot and case[5]:
+            continue
         errs += _run(cs, bases, *case, seed=i, root=i % nranks)
         if errs:
             break
@@ -214,3 +218,69 @@ def test_windows_multi_process(built, nranks):
     assert len(results) == nranks, f"only {len(results)} of {nranks} ranks reported"
     bad = [e for r in sorted(results) for e in results[r]]
     assert not bad, "\n".join(bad[:20])
+
+
+def _large_worker(rank, nranks, uid, q):
+    try:
+        os.environ["NCCL_PROTO"] = "^LL"
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        win_bytes = 2 << 30                      # one 2 GiB allocation per rank, mapped whole by every peer
+        half = win_bytes // 2
+        count = half // 4                        # 268,435,456 fp32: 1 GiB in, 1 GiB out
+        buf = torch.empty(win_bytes, dtype=torch.uint8, device="cuda")
+        win = comm.register_window(buf.data_ptr(), win_bytes)
+        inputs = [oracle.fill(7, 0x5EED0000 + r, count) for r in range(nranks)]
+        want = oracle.all_reduce(inputs, 7, 0)
+        buf[:half].copy_(torch.from_numpy(inputs[rank].view(np.uint8)))
+        buf[half:].zero_()
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        comm.all_reduce_raw(buf.data_ptr(), buf.data_ptr() + half, count, 7, 0, s.cuda_stream)
+        s.synchronize()
+        errs = [] if comm.async_error() == 0 else [f"rank {rank}: async error {comm.async_error()}"]
+        got = buf[half:].cpu().numpy().view(np.float32)
+        if not errs and not G.same_bits(got, want, 7):
+            bad = np.nonzero(got != want)[0]
+            errs.append(f"rank {rank}: {bad.size} mismatches in the 1 GiB result, first {bad[:5].tolist()}")
+        comm.deregister_window(win)
+        comm.destroy()
+        q.put((rank, errs))
+    except Exception as e:
+        q.put((rank, [f"rank {rank} exception: {e!r}"]))
+
+
+def test_two_gib_window_multi_process(built):
+    """DESIGN.md §3 / VERDICT r1 item 1: a 2 GiB window shared between two processes. hipIpcOpenMemHandle
+    never returns for allocations of 2 GiB or more in torch's bundled HIP runtime; the dma-buf transport
+    (ipc.cc) maps them. Symmetric AllReduce of 1 GiB fp32 per rank, bit-exact vs the oracle."""
+    import queue
+    import time
+    import nccl_amd
+    uid = nccl_amd.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_large_worker, args=(r, 2, uid, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    results = {}
+    t0 = time.time()
+    while len(results) < 2 and time.time() - t0 < 300:
+        try:
+            r, errs = q.get(timeout=20)
+            results[r] = errs
+        except queue.Empty:
+            print(f"[two_gib_window] waiting: {len(results)} done, {time.time() - t0:.0f}s", flush=True)
+            if not any(p.is_alive() for p in ps):
+                break
+    for p in ps:
+        if p.is_alive() and len(results) < 2:
+            p.kill()
+        p.join(timeout=60)
+    assert len(results) == 2, f"only {len(results)} of 2 ranks reported"
+    bad = [e for r in sorted(results) for e in results[r]]
+    assert not bad, "\n".join(bad)

@@ -55,9 +55,12 @@ def test_proto_and_algo_overrides(exe):
     assert plan(exe, 2, "ar", 7, 4_000_000, NCCL_AMD_ONESHOT_BYTES=64 << 20)["algo"] == "oneshot"
 
 
-def test_ll_needs_8_byte_alignment_and_room(exe):
-    assert plan(exe, 2, "ar", 7, 1001, offset=4)["algo"] == "oneshot"     # 4-byte aligned only
-    assert plan(exe, 2, "ar", 7, 1001, offset=8)["algo"] == "ll"
+def test_ll_choice_is_rank_uniform_and_needs_room(exe):
+    # the protocol must not depend on this rank's buffer alignment (peers may be aligned differently):
+    # misaligned buffers take LL too and the kernel handles any alignment (enqueue.cc:205)
+    for off in (1, 2, 4, 8):
+        assert plan(exe, 2, "ar", 7, 1001, offset=off)["algo"] == "ll"
+    assert plan(exe, 8, "reduce", 7, 1001, offset=4)["algo"] == "ll"
     big = plan(exe, 2, "ar", 7, (512 << 10) // 4, NCCL_PROTO="LL")        # exactly the line area
     assert big["algo"] == "ll" and big["part"] * 16 <= 32 << 10
     assert plan(exe, 2, "ar", 7, (1 << 20) // 4, NCCL_PROTO="LL,Simple", NCCL_AMD_LL_BYTES=4 << 20)["algo"] == "oneshot"
@@ -71,7 +74,6 @@ def test_reduce_size_table(exe):
     assert plan(exe, 2, "reduce", 7, (128 << 10) // 4 + 1)["algo"] == "direct"
     assert plan(exe, 8, "reduce", 9, 1 << 20)["algo"] == "direct"
     assert plan(exe, 8, "reduce", 9, 1000, NCCL_PROTO="^LL")["algo"] == "direct"
-    assert plan(exe, 8, "reduce", 7, 1001, offset=4)["algo"] == "direct"
 
 
 @pytest.mark.parametrize("func", ["rs", "ag"])
@@ -86,7 +88,7 @@ def test_blocked_collectives_size_table(exe, func):
         assert plan(exe, n, func, 7, 1)["algo"] == "direct"   # 4-byte blocks: no LL
         assert plan(exe, n, func, 8, 1)["algo"] == "ll"       # one fp64 per block
     assert plan(exe, 2, func, 7, 1000, NCCL_PROTO="^LL")["algo"] == "direct"
-    assert plan(exe, 2, func, 7, 1000, offset=4)["algo"] == "direct"
+    assert plan(exe, 2, func, 7, 1000, offset=4)["algo"] == "ll"   # alignment is rank-local: never decides
     p = plan(exe, 8, func, 7, 1000)
     assert p["chunk"] == 1000 and p["part"] * p["nch"] * 8 >= 4000
 
@@ -127,3 +129,14 @@ def test_channel_cap(exe):
     for cap in (1, 7, 64):
         assert plan(exe, 4, "ar", 7, 64 << 20, chancap=cap)["nch"] <= cap
         assert plan(exe, 4, "ar", 7, 1000, chancap=cap, NCCL_PROTO="LL")["nch"] <= cap
+
+
+def test_ll_channels_never_empty(exe):
+    # every LL channel of an op carries >= 1 payload: an empty channel would advance its epoch without
+    # exchanging lines and break the parity double-buffering (enqueue.cc:224)
+    for count, env in ((80, {"NCCL_AMD_LL_CHANNEL_BYTES": 8}), (7, {"NCCL_AMD_LL_CHANNEL_BYTES": 8}),
+                       (1000, {}), (33, {"NCCL_AMD_LL_CHANNEL_BYTES": 16})):
+        p = plan(exe, 2, "ar", 7, count, **env)
+        npk = -(-count * 4 // 8)
+        assert p["algo"] == "ll"
+        assert p["nch"] * p["part"] >= npk and (p["nch"] - 1) * p["part"] < npk, (count, env, p)
