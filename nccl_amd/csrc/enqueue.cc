@@ -80,7 +80,9 @@ void loadTuning(CommTuning* t) {
   memset(t, 0, sizeof(*t));
   t->checkPointers = (int)paramInt("NCCL_CHECK_POINTERS", 0);
   t->forceElementwise = (int)paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0);
-  t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 1) ? 0 : 8) |
+  // no release fence before data flags by default: every byte a peer reads from this rank's writes is a
+  // write-through system-scope store, drained before the flag store
+  t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 0) ? 0 : 8) |
                   (paramInt("NCCL_AMD_AG_PULL", 0) ? 16 : 0) | (paramInt("NCCL_AMD_RS_PULL", 0) ? 32 : 0);
   if (const char* algo = paramStr("NCCL_ALGO")) {
     if (!strcasecmp(algo, "ONESHOT")) t->algo = 1;
@@ -354,8 +356,8 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   if (info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER) aligned = aligned && ((count * ts) & 15) == 0;
   if (comm->tune.forceElementwise) aligned = false;  // diagnostics: T-sized accesses only
   p.args.aligned = aligned ? 1 : 0;
-  // NCCL_AMD_P2P_FENCE=0 drops the system release fence before data flags (all published bytes are
-  // already stored write-through at system scope and drained). Default: keep it.
+  // NCCL_AMD_P2P_FENCE=1 puts a system release fence (buffer_wbl2) back before data flags; the default
+  // omits it: all published bytes are already stored write-through at system scope and drained (§4).
   p.args.protoFlags = comm->tune.protoFlags;
   // Algorithm choice (reference: NCCL_ALGO / tuning.cc cost model): one-shot for small AllReduce
   // (latency: one handshake), direct scatter-reduce-gather otherwise (bandwidth). NCCL_ALGO may force

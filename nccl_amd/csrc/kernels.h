@@ -158,6 +158,13 @@ __device__ void signalAll(uint64_t* const* ptr, const uint64_t* val, int nsig, b
 
 // ------------------------------------------------------------------------------------ data movement
 
+// 16-byte packs each thread keeps in flight in copyRange: 8 x 16 B x 512 threads = 64 KiB per channel, enough
+// to keep one CU's share of HBM (and, on the 8-GPU node, its xGMI writes) busy at moderate channel counts.
+#ifndef NCCL_AMD_COPY_UNROLL
+#define NCCL_AMD_COPY_UNROLL 8
+#endif
+constexpr int kCopyUnroll = NCCL_AMD_COPY_UNROLL;
+
 // Copy [0,nbytes) from src to dst. Both 16-byte aligned when `aligned`; nbytes multiple of sizeof(T).
 template <typename T, bool REMOTE>
 __device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t nbytes, bool aligned) {
@@ -165,7 +172,7 @@ __device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t n
     uint64_t npk = nbytes >> 4;
     const u32x4* s = (const u32x4*)src;
     u32x4* d = (u32x4*)dst;
-    constexpr int U = 4;
+    constexpr int U = kCopyUnroll;
     uint64_t i = threadIdx.x;
     for (; i + (U - 1) * kThreads < npk; i += U * kThreads) {
       u32x4 v[U];
@@ -311,7 +318,7 @@ struct Channel {
   Shared& sh;
   const Red<T, OP>& fn;
   int c, me, n, nSlots;
-  bool aligned, isRoot, forceAcq, forceRel, noRel;
+  bool aligned, isRoot, forceAcq, forceRel, noRel, noAcq;
   // AG pull (NCCL_AMD_AG_PULL=1, AllReduce / AllGather): phase B leaves ONE copy of the owner's block in
   // its own AG staging and phase C reads it from there over xGMI, instead of B pushing n-1 copies into
   // the peers' staging. Same link bytes, reads instead of writes. The copy is shared by all readers, so
@@ -391,7 +398,7 @@ struct Channel {
     if (COLL != COLL_AG) {
       if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
       __syncthreads();
-      if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, true)) return false;
+      if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, !noAcq)) return false;
     }
     if (push) {
       if (tid < NCCL_AMD_MAX_RANKS) {
@@ -497,7 +504,7 @@ struct Channel {
     int tid = threadIdx.x;
     if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
     __syncthreads();
-    if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, true)) return false;
+    if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, !noAcq)) return false;
     uint64_t lo, hi;
     sliceRange(a, c, step, a.count, lo, hi);
     for (uint64_t x = lo; x < hi;) {
@@ -536,7 +543,7 @@ struct Channel {
     const int recvKind = agPull ? CTR_PULL_GOT : CTR_RECV_AG;
     if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(recvKind, tid) + 1 : 0;
     __syncthreads();
-    if (!waitAll(dc, sh.st, myFlags(agPull ? FLG_PULL_READY : FLG_AG_READY), sh.want, true)) return false;
+    if (!waitAll(dc, sh.st, myFlags(agPull ? FLG_PULL_READY : FLG_AG_READY), sh.want, !noAcq)) return false;
     for (int k = 1; k < n; k++) {
       int q = (me + n - k) % n;
       const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
@@ -580,12 +587,14 @@ __global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
     __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
   }
   const Red<T, OP> fn(opArg);
-  // protoFlags (NCCL_AMD_PROTO_FLAGS, diagnostics): 1 = acquire on credit waits too, 2 = release on
-  // credit signals too, 4 = C(s) before A(s+1), 8 = NO release fence before data flags (unsafe, measures
-  // the fence cost only), 16 = AG pull (NCCL_AMD_AG_PULL=1), 32 = RS pull (NCCL_AMD_RS_PULL=1)
+  // protoFlags: 1 = acquire on credit waits too, 2 = release on credit signals too, 4 = C(s) before A(s+1),
+  // 8 = no release fence before data flags (the default: every published byte is a write-through system-scope
+  // store drained before the flag; NCCL_AMD_P2P_FENCE=1 clears it), 16 = AG pull
+  // (NCCL_AMD_AG_PULL=1), 32 = RS pull (NCCL_AMD_RS_PULL=1), 64 = no acquire after data waits (diagnostics
+  // only: measures the acquire's cost)
   Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
                           (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
-                          (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0,
+                          (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0, (a.protoFlags & 64) != 0,
                           (COLL == COLL_AR || COLL == COLL_AG) && (a.protoFlags & 16) != 0,
                           (COLL == COLL_AR || COLL == COLL_RS) && (a.protoFlags & 32) != 0};
   if (COLL == COLL_AR1) {
