@@ -30,6 +30,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "core.h"
 #include "numerics.h"
@@ -224,9 +225,14 @@ template <typename T, int OP>
 __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const char* const* src, uint64_t nelem,
                                           char* dstLocal, char* const* dstPush, int nPush, bool aligned) {
   constexpr int EPP = 16 / sizeof(T);
-  // 1-byte types unpack 16 elements per pack into separate registers: one pack per batch keeps the kernel
-  // within its register budget (kWavesPerEU)
-  constexpr int U = sizeof(T) == 1 ? 1 : 4;
+  // uint8 / int8 Sum and MinMax fold four bytes per dword (numerics.h Swar8) and keep 2 packs in flight
+  // (4 reach the 128-VGPR cap and spill in MinMax); other 1-byte folds (fp8, Prod, PreMulSum, integer avg) unpack 16 elements per pack into
+  // separate registers, so they keep one pack per batch to stay within the register budget (kCoResident;
+  // two packs spilled up to 55 VGPRs for fp8)
+  constexpr bool kSwar = std::is_same<T, uint8_t>::value && Swar8<OP>::ok;
+  constexpr int U = sizeof(T) > 1 ? 4 : kSwar ? 2 : 1;
+  uint32_t swarMask = 0;
+  if constexpr (kSwar) swarMask = (uint32_t)(uint8_t)fn.arg * 0x01010101u;
   if (aligned) {
     const uint64_t npk = nelem / EPP;
     for (uint64_t base = threadIdx.x; base < npk; base += (uint64_t)U * kThreads) {
@@ -247,10 +253,15 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
         }
 #pragma unroll
         for (int u = 0; u < U; u++) {
+          if constexpr (kSwar) {
 #pragma unroll
-          for (int e = 0; e < EPP; e++) {
-            T x = fn.pre(cur[u].e[e]);
-            acc[u].e[e] = k == 0 ? x : fn.red(x, acc[u].e[e]);
+            for (int w = 0; w < 4; w++) acc[u].v[w] = k == 0 ? cur[u].v[w] : Swar8<OP>::red(cur[u].v[w], acc[u].v[w], swarMask);
+          } else {
+#pragma unroll
+            for (int e = 0; e < EPP; e++) {
+              T x = fn.pre(cur[u].e[e]);
+              acc[u].e[e] = k == 0 ? x : fn.red(x, acc[u].e[e]);
+            }
           }
           cur[u] = nxt[u];
         }

@@ -233,9 +233,73 @@ struct RedSmall {
   }
   __host__ __device__ T post(T x) const { return x; }
 };
-template <int OP> struct Red<half_t, OP> : RedSmall<half_t, OP> { using RedSmall<half_t, OP>::RedSmall; };
-template <int OP> struct Red<bf16_t, OP> : RedSmall<bf16_t, OP> { using RedSmall<bf16_t, OP>::RedSmall; };
+// fp16: native half arithmetic (reference __hadd/__hmul/__hadd2, reduce_kernel.h:411-459). One IEEE fp16
+// add or multiply, rounded RNE, is exactly the oracle's f32 operation rounded once to half (the exact sum of
+// two 11-bit significands fits f32 whenever it can matter; their product always does), so results are
+// bit-identical — and a fold over 16-byte packs compiles to v_pk_add_f16 / v_pk_mul_f16, two lanes per
+// instruction. Min/max keep the f32 path with the defined signed-zero order (minOrdered).
+template <int OP>
+struct Red<half_t, OP> {
+  _Float16 s;
+  bool isMin;
+  __host__ __device__ static _Float16 h(half_t v) { return __builtin_bit_cast(_Float16, v.x); }
+  __host__ __device__ static half_t w(_Float16 v) { return half_t{__builtin_bit_cast(uint16_t, v)}; }
+  __host__ __device__ explicit Red(uint64_t a) : s(__builtin_bit_cast(_Float16, (uint16_t)a)), isMin((a & 1) == 0) {}
+  __host__ __device__ half_t pre(half_t x) const { return OP == 3 ? w(h(x) * s) : x; }
+  __host__ __device__ half_t red(half_t a, half_t b) const {
+    if (OP == 1) return w(h(a) * h(b));
+    if (OP == 2) {
+      float x = halfToF32(a.x), y = halfToF32(b.x);
+      return half_t{f32ToHalf(isMin ? minOrdered(x, y) : maxOrdered(x, y))};
+    }
+    return w(h(a) + h(b));
+  }
+  __host__ __device__ half_t post(half_t x) const { return x; }
+};
+// bf16: f32 arithmetic on the widened values, then one RNE rounding (gfx950 has no bf16 VALU add; the
+// widening is a shift / mask, the f32 pairs go to v_pk_add_f32 / v_pk_mul_f32 and the rounding of two
+// results to v_cvt_pk_bf16_f32). No opaque barrier is needed here: there is no mixed-precision bf16 FMA
+// the backend could fold a rounded product into (that hazard is fp16 / fp8 only, see opaqueF).
+template <int OP>
+struct Red<bf16_t, OP> {
+  float s;
+  bool isMin;
+  __host__ __device__ explicit Red(uint64_t a) : s(bf16ToF32((uint16_t)a)), isMin((a & 1) == 0) {}
+  __host__ __device__ bf16_t pre(bf16_t x) const { return OP == 3 ? bf16_t{f32ToBf16(bf16ToF32(x.x) * s)} : x; }
+  __host__ __device__ bf16_t red(bf16_t a, bf16_t b) const {
+    float x = bf16ToF32(a.x), y = bf16ToF32(b.x), r;
+    if (OP == 1) r = x * y;
+    else if (OP == 2) r = isMin ? minOrdered(x, y) : maxOrdered(x, y);
+    else r = x + y;
+    return bf16_t{f32ToBf16(r)};
+  }
+  __host__ __device__ bf16_t post(bf16_t x) const { return x; }
+};
 template <int OP> struct Red<e4m3_t, OP> : RedSmall<e4m3_t, OP> { using RedSmall<e4m3_t, OP>::RedSmall; };
 template <int OP> struct Red<e5m2_t, OP> : RedSmall<e5m2_t, OP> { using RedSmall<e5m2_t, OP>::RedSmall; };
+
+// ---- 1-byte integer Sum / MinMax on four bytes per dword (SWAR) ----
+// Bit-identical to Red<uint8_t, OP>::red on each byte (tests/test_numerics.py checks every byte pair). The fold
+// uses it for uint8 / int8 so a 16-byte pack stays four registers instead of sixteen unpacked bytes, which
+// lets it keep four packs per thread in flight within the 128-VGPR co-residency budget.
+template <int OP> struct Swar8 { static constexpr bool ok = false; };
+template <> struct Swar8<0> {  // DEV_SUM: byte-wise add mod 256 (carries masked out of each byte)
+  static constexpr bool ok = true;
+  __host__ __device__ static uint32_t red(uint32_t a, uint32_t b, uint32_t) {
+    return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
+  }
+};
+template <> struct Swar8<2> {  // DEV_MINMAX: (a^m) < (b^m) ? a : b per byte; M = the xormask in every byte
+  static constexpr bool ok = true;
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
+  __host__ __device__ static uint32_t red(uint32_t a, uint32_t b, uint32_t M) {
+    const uint32_t x = a ^ M, y = b ^ M;  // unsigned order of x, y = the functor's order of a, b
+    const us2 lo = __builtin_elementwise_min(__builtin_bit_cast(us2, x & 0x00ff00ffu),
+                                             __builtin_bit_cast(us2, y & 0x00ff00ffu));  // v_pk_min_u16
+    const us2 hi = __builtin_elementwise_min(__builtin_bit_cast(us2, (x >> 8) & 0x00ff00ffu),
+                                             __builtin_bit_cast(us2, (y >> 8) & 0x00ff00ffu));
+    return (__builtin_bit_cast(uint32_t, lo) | (__builtin_bit_cast(uint32_t, hi) << 8)) ^ M;
+  }
+};
 
 }  // namespace ncclamd

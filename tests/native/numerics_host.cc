@@ -13,6 +13,11 @@ uint8_t nx_f32_to_fp8(float f, int e5m2) { return e5m2 ? f32ToFp8Sat<true>(f) : 
 uint64_t nx_red(int dtype, int op, uint64_t arg, uint64_t a, uint64_t b);
 uint64_t nx_pre(int dtype, int op, uint64_t arg, uint64_t a);
 uint64_t nx_post(int dtype, int op, uint64_t arg, uint64_t a);
+uint32_t nx_swar8(int op, uint32_t mask, uint32_t a, uint32_t b);
+}
+uint32_t nx_swar8(int op, uint32_t mask, uint32_t a, uint32_t b) {
+  uint32_t M = (mask & 0xff) * 0x01010101u;
+  return op == 0 ? Swar8<0>::red(a, b, M) : Swar8<2>::red(a, b, M);
 }
 template <typename T, int OP> static uint64_t red1(uint64_t arg, uint64_t a, uint64_t b, int which) {
   Red<T, OP> fn(arg);

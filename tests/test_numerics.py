@@ -26,6 +26,8 @@ def nx(built):
     for f in ("nx_pre", "nx_post"):
         getattr(L, f).restype = U64
         getattr(L, f).argtypes = [I, I, U64, U64]
+    L.nx_swar8.restype = ctypes.c_uint32
+    L.nx_swar8.argtypes = [I, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
     L.nx_f32_to_fp8.restype = ctypes.c_uint8
     L.nx_f32_to_fp8.argtypes = [ctypes.c_float, I]
     L.nx_fp8_to_f32.restype = ctypes.c_float
@@ -123,3 +125,24 @@ def test_integer_functors(nx, dtype, bits):
         signed = dtype in (0, 2, 4)
         want = [(-(-int(v) // n) if (signed and int(v) < 0) else int(v) // n) for v in vals.tolist()]
         assert [int(x) for x in got] == want
+
+
+@pytest.mark.parametrize("op,mask", [(0, 0), (2, 0x80), (2, 0x7f), (2, 0x00), (2, 0xff)])
+def test_swar_bytes_match_functor(nx, op, mask):
+    """numerics.h Swar8 (4 bytes per dword, used by the uint8/int8 Sum and MinMax folds) equals the per-byte
+    functor Red<uint8_t, OP>::red for every byte pair in every lane position (masks: int8 min / max, uint8
+    min / max)."""
+    a = np.arange(256, dtype=np.uint32)
+    pairs = [(int(x), int(y)) for x in a for y in a]
+    rng = np.random.default_rng(7)
+    for lane in range(4):
+        for x, y in pairs[lane::4]:  # every pair once across the four lanes
+            fill_a, fill_b = (int(v) for v in rng.integers(0, 2**32, 2, dtype=np.uint64))
+            sh = 8 * lane
+            wa = (fill_a & ~(0xff << sh)) | (x << sh)
+            wb = (fill_b & ~(0xff << sh)) | (y << sh)
+            got = nx.nx_swar8(op, mask, wa, wb)
+            for l in range(4):
+                ea, eb = (wa >> (8 * l)) & 0xff, (wb >> (8 * l)) & 0xff
+                want = nx.nx_red(1, op, mask, ea, eb)
+                assert (got >> (8 * l)) & 0xff == want, (op, mask, hex(wa), hex(wb), l)
