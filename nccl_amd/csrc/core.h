@@ -150,7 +150,7 @@ struct CommTuning {
   int checkPointers;        // NCCL_CHECK_POINTERS
   int forceElementwise;     // NCCL_AMD_FORCE_ELEMENTWISE (diagnostics)
   int protoFlags;           // NCCL_AMD_PROTO_FLAGS | (NCCL_AMD_P2P_FENCE=0 ? 8 : 0)
-  int algo;                 // NCCL_ALGO: 0 unset, 1 ONESHOT, 2 DIRECT (RING / TREE)
+  int algo;                 // NCCL_ALGO: TuneAlgoForce (ONESHOT, DIRECT, RING, TREE)
   int llOn, simpleOn;       // NCCL_PROTO
   int symDisable;           // NCCL_AMD_SYM_DISABLE
   int symOneShot;           // NCCL_AMD_SYM_ONESHOT: caller promises out-of-place window AllReduces
@@ -231,6 +231,7 @@ struct ncclComm {
   bool destroyed = false;
   std::thread initThread;  // non-blocking ncclCommInitRankConfig (config.blocking = 0)
   uint64_t opCount = 0;
+  uint32_t warnedAlgo = 0;  // NCCL_ALGO forced but unavailable for a collective: warned once per CollFunc
   uint64_t endMagic;
 };
 
@@ -259,7 +260,9 @@ struct CollInfo {  // reference: struct ncclInfo, src/include/info.h:17-41
   hipStream_t stream;
 };
 
-enum Algo { ALGO_COPY = 0, ALGO_ONERANK = 1, ALGO_DIRECT = 2, ALGO_ONESHOT = 3, ALGO_LL = 4 };
+enum Algo { ALGO_COPY = 0, ALGO_ONERANK = 1, ALGO_DIRECT = 2, ALGO_ONESHOT = 3, ALGO_LL = 4, ALGO_PIPE = 5 };
+// NCCL_ALGO values of CommTuning::algo
+enum TuneAlgoForce { FORCE_NONE = 0, FORCE_ONESHOT = 1, FORCE_DIRECT = 2, FORCE_RING = 3, FORCE_TREE = 4 };
 
 struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src/include/comm.h)
   CollFunc func;
@@ -274,6 +277,7 @@ struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src
   LLBatchArgs ll;  // ALGO_LL
   int copyVariant;  // ALGO_COPY
   int64_t copyGrid;
+  int pipeKind;     // ALGO_PIPE: PipeKind (pipe.h)
 };
 
 ncclResult_t enqueueCheck(CollInfo* info);

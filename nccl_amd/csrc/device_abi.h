@@ -45,6 +45,9 @@ enum CtrKind {
   CTR_PULL_PUB = 6, CTR_PULL_GOT = 7, CTR_KINDS = 8
 };
 
+// Ring / chain kernels (pipe.h; NCCL_ALGO=RING / TREE)
+enum PipeKind { PIPE_RING_AR = 0, PIPE_RING_RS = 1, PIPE_RING_AG = 2, PIPE_CHAIN_AR = 3, PIPE_CHAIN_REDUCE = 4 };
+
 // Device reduction kinds (reference ncclDevRedOp_t subset, src/include/device.h)
 enum DevRedOp { DEV_SUM = 0, DEV_PROD = 1, DEV_MINMAX = 2, DEV_PREMULSUM = 3, DEV_SUMPOSTDIV = 4, DEV_NUMOPS = 5 };
 

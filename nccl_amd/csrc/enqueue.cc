@@ -85,8 +85,10 @@ void loadTuning(CommTuning* t) {
   t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 0) ? 0 : 8) |
                   (paramInt("NCCL_AMD_AG_PULL", 0) ? 16 : 0) | (paramInt("NCCL_AMD_RS_PULL", 0) ? 32 : 0);
   if (const char* algo = paramStr("NCCL_ALGO")) {
-    if (!strcasecmp(algo, "ONESHOT")) t->algo = 1;
-    else if (!strcasecmp(algo, "DIRECT") || !strcasecmp(algo, "RING") || !strcasecmp(algo, "TREE")) t->algo = 2;
+    if (!strcasecmp(algo, "ONESHOT")) t->algo = FORCE_ONESHOT;
+    else if (!strcasecmp(algo, "DIRECT")) t->algo = FORCE_DIRECT;
+    else if (!strcasecmp(algo, "RING")) t->algo = FORCE_RING;
+    else if (!strcasecmp(algo, "TREE")) t->algo = FORCE_TREE;
     else WARN("NCCL_ALGO=%s: unknown here (ONESHOT, DIRECT, RING, TREE); using the size table", algo);
   }
   t->llOn = t->simpleOn = 1;
@@ -216,7 +218,7 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   // (default 256 KiB / n: 128 KiB at n=2, 32 KiB at n=8; for ReduceScatter / AllGather that is per rank
   // block, i.e. 256 KiB of total data at any n, the same per-rank link bytes)
   const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : std::max<size_t>(16 << 10, ((size_t)256 << 10) / n);
-  bool useLL = fits && (!t.simpleOn || (t.algo == 0 && bytes <= llLim));
+  bool useLL = fits && (!t.simpleOn || (t.algo == FORCE_NONE && bytes <= llLim));
   int tuned = TUNE_DEFAULT, tunedNch = 0;
   if (comm->tunerLoaded) {  // an external tuner plugin may overrule the size table (tuner.cc)
     tunerPick(comm, info.func, blocked ? bytes * n : bytes, 1, fits, &tuned, &tunedNch);
@@ -368,7 +370,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     // handshakes: the crossover shrinks with n (default 2 MiB / n: 1 MiB at n=2, 256 KiB at n=8)
     size_t bytes = count * (size_t)ts;
     size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes : ((size_t)2 << 20) / n;
-    oneShot = comm->tune.algo == 1 || (comm->tune.algo == 0 && bytes <= lim);
+    oneShot = comm->tune.algo == FORCE_ONESHOT || (comm->tune.algo == FORCE_NONE && bytes <= lim);
   }
   int tunedNch = 0;
   if (comm->tunerLoaded) {  // external tuner plugin: one-shot (TREE/SIMPLE) vs direct (RING/SIMPLE), channels
@@ -391,6 +393,41 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     TRACE("%s: LL count %zu nch %d part %lu payloads", info.opName, count, p.nChannels,
           (unsigned long)p.ll.ops[0].part);
     goto launch;
+  }
+  // The reference's own algorithms, forced with NCCL_ALGO=RING / TREE (pipe.h): the ring for AllReduce,
+  // ReduceScatter and AllGather, the chain (the intra-node tree) for AllReduce; Reduce's ring is the chain
+  // to the root (reduce.h). Where the reference has no such algorithm the default plan runs, with a warning.
+  if (comm->tune.algo == FORCE_RING || comm->tune.algo == FORCE_TREE) {
+    const bool ring = comm->tune.algo == FORCE_RING;
+    int kind = -1;
+    if (info.func == FUNC_ALLREDUCE) kind = ring ? PIPE_RING_AR : PIPE_CHAIN_AR;
+    else if (ring) kind = info.func == FUNC_REDUCESCATTER ? PIPE_RING_RS : info.func == FUNC_ALLGATHER ? PIPE_RING_AG
+                                                                                                   : PIPE_CHAIN_REDUCE;
+    // A ring hop receives and sends on the same cycle of links: with one staging slot per link every rank
+    // would hold its outgoing slot full while waiting for its successor to drain it (a cyclic wait), so the
+    // ring needs at least two slots; the chain is acyclic and runs with one.
+    const bool cyclic = kind == PIPE_RING_AR || kind == PIPE_RING_RS || kind == PIPE_RING_AG;
+    if (kind < 0 || (cyclic && comm->nSlots < 2)) {
+      if (!(comm->warnedAlgo & (1u << info.func))) {
+        comm->warnedAlgo |= 1u << info.func;
+        if (kind < 0)
+          WARN("NCCL_ALGO=TREE: no tree algorithm for %s (the reference has none either); using the default plan",
+               info.opName);
+        else
+          WARN("NCCL_ALGO=RING needs NCCL_AMD_NSLOTS >= 2 (have %d); %s uses the default plan", comm->nSlots,
+               info.opName);
+      }
+    } else {
+      p.algo = ALGO_PIPE;
+      p.pipeKind = kind;
+      const bool chain = kind == PIPE_CHAIN_AR || kind == PIPE_CHAIN_REDUCE;
+      if (chain) p.args.chunk = count;  // one block: the chain folds every element in the same order
+      const size_t span = chain ? count * ts : blockElems * ts;
+      planChannels(comm, span, ts, p, (size_t)comm->tune.minChannelBytes, comm->chanCap);
+      TRACE("%s: %s kind %d nch %d part %lu slice %lu steps %d", info.opName, ring ? "RING" : "TREE", kind,
+            p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps);
+      goto launch;
+    }
   }
   // Symmetric windows (reference: symmetric kernels for buffers in NCCL_WIN_COLL_SYMMETRIC windows,
   // src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*): zero-copy pull kernels.

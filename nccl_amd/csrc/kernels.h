@@ -632,6 +632,10 @@ __global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
   }
 }
 
+}  // namespace ncclamd
+#include "pipe.h"  // ring and chain (NCCL_ALGO=RING / TREE) on the same staging and credits
+namespace ncclamd {
+
 // ------------------------------------------------------------------------------------ LL one-shot
 //
 // Low-latency AllReduce for small buffers (reference prims_ll.h:108-158, LL protocol). Every 8 bytes of
@@ -1025,6 +1029,18 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((oneRankKernel<T, OP>), dim3(grid), dim3(256), 0, p.stream, (T*)p.args.recvbuff,
                        (const T*)p.args.sendbuff, p.args.count, p.args.redArg, p.args.redArgPtr);
+    HIPCHECK(hipGetLastError());
+    return ncclSuccess;
+  }
+  if (p.algo == ALGO_PIPE) {  // ring / chain (pipe.h); AllGather is type-erased (launchKernGather)
+    switch (p.pipeKind) {
+      case PIPE_RING_AR: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_RING_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_RING_RS: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_RING_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_RING_AG: hipLaunchKernelGGL((pipeKernel<T, 0, PIPE_RING_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_CHAIN_AR: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_CHAIN_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_CHAIN_REDUCE: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_CHAIN_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      default: return ncclInternalError;
+    }
     HIPCHECK(hipGetLastError());
     return ncclSuccess;
   }

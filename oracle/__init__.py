@@ -33,6 +33,7 @@ def lib() -> ctypes.CDLL:
         PP = ctypes.POINTER(ctypes.c_void_p)
         L.oracle_host_to_dev_op.argtypes = [I, I, I, ctypes.POINTER(I), ctypes.POINTER(U64)]
         L.oracle_all_reduce.argtypes = [I, I, U64, I, PP, S, P]
+        L.oracle_all_reduce_chain.argtypes = [I, I, U64, I, PP, S, P]
         L.oracle_reduce_scatter.argtypes = [I, I, U64, I, PP, S, PP]
         L.oracle_reduce.argtypes = [I, I, U64, I, I, PP, S, P]
         L.oracle_fill.argtypes = [I, U64, S, P, I]
@@ -79,6 +80,17 @@ def all_reduce(inputs: Sequence[np.ndarray], dtype: int, op: int = 0, premul_sca
     ins = [np.ascontiguousarray(x) for x in inputs]
     out = np.empty_like(ins[0])
     rc = lib().oracle_all_reduce(dtype, d, arg, n, _ptrs(ins), ins[0].size, out.ctypes.data)
+    assert rc == 0
+    return out
+
+
+def all_reduce_chain(inputs: Sequence[np.ndarray], dtype: int, op: int = 0):
+    """ncclAllReduce with NCCL_ALGO=TREE on one node: the chain 0 <- 1 <- ... <- n-1 (fold order n-1 .. 0)."""
+    n = len(inputs)
+    d, arg = dev_op(op, dtype, n)
+    ins = [np.ascontiguousarray(x) for x in inputs]
+    out = np.empty_like(ins[0])
+    rc = lib().oracle_all_reduce_chain(dtype, d, arg, n, _ptrs(ins), ins[0].size, out.ctypes.data)
     assert rc == 0
     return out
 

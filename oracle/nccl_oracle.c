@@ -343,6 +343,21 @@ int oracle_all_reduce(int dt, int devop, uint64_t arg, int n, const void* const*
   return 0;
 }
 
+/* AllReduce over the reference's intra-node TREE (NCCL_ALGO=TREE): a chain with root 0 and leaf n-1
+ * (src/graph/connect.cc:53-63, treeIntra = 0..n-1): the leaf sends pre(x[n-1]), rank k folds
+ * red(pre(x[k]), acc) on the way up (all_reduce.h:86-118 runTreeUpDown), the root applies post and the
+ * result is broadcast back down. Every element folds in the order n-1, n-2, ..., 0. */
+int oracle_all_reduce_chain(int dt, int devop, uint64_t arg, int n, const void* const* in, size_t count, void* out) {
+  if (oracle_type_size(dt) <= 0 || n <= 0) return 4;
+#pragma omp parallel for schedule(static)
+  for (size_t i = 0; i < count; i++) {
+    uint64_t acc = pre_op(dt, devop, arg, ld(dt, in[n - 1], i));
+    for (int r = n - 2; r >= 0; r--) acc = reduce2(dt, devop, arg, pre_op(dt, devop, arg, ld(dt, in[r], i)), acc);
+    st(dt, out, i, post_op(dt, devop, arg, acc));
+  }
+  return 0;
+}
+
 /* ReduceScatter: out[d][j] = fold over ranks of in[r][d*recvcount + j], from d+1 (reduce_scatter.h:34-55). */
 int oracle_reduce_scatter(int dt, int devop, uint64_t arg, int n, const void* const* in, size_t recvcount,
                           void* const* out) {

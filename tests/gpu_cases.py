@@ -43,9 +43,10 @@ def make_inputs(n: int, dtype: int, count: int, seed: int, kind: int = 0):
     return [oracle.fill(dtype, seed * 131 + r, count, kind) for r in range(n)]
 
 
-def expected(coll: str, inputs, dtype: int, op: int, root: int = 0):
+def expected(coll: str, inputs, dtype: int, op: int, root: int = 0, algo: str = ""):
     if coll == "allreduce":
-        out = oracle.all_reduce(inputs, dtype, op)
+        # NCCL_ALGO=TREE folds every element in the chain's order; every other path in the ring's
+        out = oracle.all_reduce_chain(inputs, dtype, op) if algo == "TREE" else oracle.all_reduce(inputs, dtype, op)
         return [out] * len(inputs)
     if coll == "reducescatter":
         return oracle.reduce_scatter(inputs, dtype, op)
@@ -94,7 +95,7 @@ def case_list(n: int, quick: bool = False):
 
 
 def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=False, root=0, sync=True,
-             inputs=None):
+             inputs=None, algo=""):
     """Run one collective on every (comm, stream) of this process; returns list of error strings.
     `comms_and_streams` holds the ranks owned by this process: [(comm, torch stream), ...]; the
     inputs of ALL ranks are regenerated deterministically so each process can check its own ranks."""
@@ -102,7 +103,7 @@ def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=
     n = comms_and_streams[0][0].nranks
     if inputs is None:
         inputs = make_inputs(n, dtype, count, seed)
-    exp = expected(coll, inputs, dtype, op, root)
+    exp = expected(coll, inputs, dtype, op, root, algo)
     npdt = oracle.NP_STORAGE[dtype]
     es = np.dtype(npdt).itemsize
     ocount = out_count(coll, n, count)

@@ -4,7 +4,7 @@
 // enqueue.cc makes are stubbed so every plan is recorded and printed instead of launched.
 //
 //   plan_test NRANKS FUNC(ar|rs|ag|reduce) DTYPE COUNT [ALIGN_OFFSET_BYTES] [CHANCAP]
-// prints one line: algo=<copy|onerank|direct|oneshot|ll> nch=<channels> part=<elements|payloads>
+// prints one line: algo=<copy|onerank|direct|oneshot|ll|ring|chain> nch=<channels> part=<elements|payloads>
 //                  slice=<elements> steps=<n> chunk=<elements>
 #include <stdio.h>
 #include <stdlib.h>
@@ -93,8 +93,15 @@ int main(int argc, char** argv) {
            (unsigned long)gSym.args.chunk);
     return 0;
   }
-  const char* names[] = {"copy", "onerank", "direct", "oneshot", "ll"};
+  const char* names[] = {"copy", "onerank", "direct", "oneshot", "ll", "pipe"};
+  const char* pipes[] = {"ring", "ring", "ring", "chain", "chain"};
   const LaunchPlan& p = gPlan;
+  if (p.algo == ALGO_PIPE) {
+    printf("algo=%s kind=%d nch=%d part=%lu slice=%lu steps=%d chunk=%lu\n", pipes[p.pipeKind], p.pipeKind,
+           p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps,
+           (unsigned long)p.args.chunk);
+    return 0;
+  }
   if (p.algo == ALGO_LL)
     printf("algo=ll nch=%d part=%lu slice=0 steps=1 chunk=%lu\n", p.nChannels, (unsigned long)p.ll.ops[0].part,
            (unsigned long)p.ll.ops[0].chunk);

@@ -73,7 +73,8 @@ def _mp_worker(rank, nranks, uid, quick, q, env=None):
         errs = []
         for i, (coll, dt, op, count, mis) in enumerate(G.case_list(nranks, quick=quick)):
             root = i % nranks
-            errs += G.run_case([(comm, s)], coll, dt, op, count, mis, seed=i, root=root)
+            errs += G.run_case([(comm, s)], coll, dt, op, count, mis, seed=i, root=root,
+                               algo=(env or {}).get("NCCL_ALGO", ""))
             if errs:
                 break
         comm.destroy()
@@ -95,7 +96,8 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (3, {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
             (4, {"NCCL_AMD_AG_PULL": "1"}),
             (3, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
-            (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"})]
+            (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}),
+            (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"})]
 
 
 @pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
@@ -485,4 +487,38 @@ def test_rank_dependent_misalignment(built):
             errs += G.run_case(cs, coll, dt, op, count, list(mis), seed=100 + i, root=i % 3)
     for c in comms:
         c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
+@pytest.mark.parametrize("algo,nranks", [("RING", 2), ("RING", 3), ("TREE", 2), ("TREE", 4)])
+def test_forced_ring_and_tree(built, algo, nranks, monkeypatch):
+    """NCCL_ALGO=RING / TREE run the reference's own algorithms (pipe.h): the ring for AllReduce /
+    ReduceScatter / AllGather and the chain to the root for Reduce (RING), the intra-node tree = chain for
+    AllReduce (TREE; RS / AG / Reduce fall back to the default plan, as the reference has no tree for them).
+    Bit-exact vs the oracle: the ring folds in the oracle's order, the chain in oracle_all_reduce_chain's.
+    Tiny slots force many pipeline hops and credit wrap-around."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    monkeypatch.setenv("NCCL_MULTI_RANK_GPU_ENABLE", "1")
+    monkeypatch.setenv("NCCL_ALGO", algo)
+    torch.cuda.set_device(0)
+    errs = []
+    # (the ring needs >= 2 slots per link, enqueue.cc; the chain also runs with 1)
+    for env in ({}, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2" if algo == "RING" else "1"}):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        comms = nccl_amd.Communicator.init_all([0] * nranks)
+        cs = list(zip(comms, [torch.cuda.Stream() for _ in comms]))
+        for i, (coll, dt, op, count, mis) in enumerate(G.case_list(nranks, quick=True)):
+            for root in ([0] if coll != "reduce" else [nranks - 1]):
+                errs += G.run_case(cs, coll, dt, op, count, mis, seed=300 + i, root=root, algo=algo)
+            if mis == 0 and i % 3 == 0:
+                errs += G.run_case(cs, coll, dt, op, count, mis, seed=300 + i, inplace=True, algo=algo)
+            if errs:
+                break
+        for c in comms:
+            c.destroy()
+        if errs:
+            break
     assert not errs, "\n".join(errs[:20])

@@ -48,7 +48,7 @@ def test_proto_and_algo_overrides(exe):
     assert plan(exe, 2, "ar", 7, 1024, NCCL_PROTO="Simple")["algo"] == "oneshot"
     assert plan(exe, 2, "ar", 7, 1024, NCCL_PROTO="LL,Simple")["algo"] == "ll"
     assert plan(exe, 2, "ar", 7, 1024, NCCL_ALGO="DIRECT")["algo"] == "direct"
-    assert plan(exe, 2, "ar", 7, 1024, NCCL_ALGO="RING")["algo"] == "direct"
+    assert plan(exe, 2, "ar", 7, 1024, NCCL_ALGO="RING")["algo"] == "ring"
     assert plan(exe, 8, "ar", 7, 64 << 20, NCCL_ALGO="ONESHOT")["algo"] == "oneshot"
     assert plan(exe, 2, "ar", 7, 1024, NCCL_ALGO="DIRECT", NCCL_PROTO="LL")["algo"] == "ll"  # only LL left
     assert plan(exe, 2, "ar", 7, 100_000, NCCL_AMD_LL_BYTES=1 << 20)["algo"] == "ll"
@@ -140,3 +140,21 @@ def test_ll_channels_never_empty(exe):
         npk = -(-count * 4 // 8)
         assert p["algo"] == "ll"
         assert p["nch"] * p["part"] >= npk and (p["nch"] - 1) * p["part"] < npk, (count, env, p)
+
+
+@pytest.mark.parametrize("func,algo,want", [
+    ("ar", "RING", ("ring", 0)), ("rs", "RING", ("ring", 1)), ("ag", "RING", ("ring", 2)),
+    ("ar", "TREE", ("chain", 3)), ("reduce", "RING", ("chain", 4)),
+    ("rs", "TREE", ("direct", None)), ("ag", "TREE", ("direct", None)), ("reduce", "TREE", ("direct", None)),
+])
+def test_forced_reference_algorithms(exe, func, algo, want):
+    # NCCL_ALGO=RING / TREE run the reference's own algorithms (pipe.h); where the reference has none
+    # (TREE for RS / AG / Reduce) the default plan runs, with a warning
+    for n, count in ((2, 1000), (8, 1 << 20), (3, 7)):
+        p = plan(exe, n, func, 7, count * (n if func == "rs" else 1), NCCL_ALGO=algo)
+        assert p["algo"] == want[0], (n, count, p)
+        if want[1] is not None:
+            assert p["kind"] == want[1]
+            assert p["part"] * p["nch"] >= p["chunk"] and p["steps"] == -(-p["part"] // p["slice"])
+            if want[0] == "chain":
+                assert p["chunk"] == count
