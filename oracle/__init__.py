@@ -37,6 +37,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_reduce_scatter.argtypes = [I, I, U64, I, PP, S, PP]
         L.oracle_reduce.argtypes = [I, I, U64, I, I, PP, S, P]
         L.oracle_fill.argtypes = [I, U64, S, P, I]
+        L.oracle_fill_at.argtypes = [I, U64, S, S, P, I]
         L.oracle_cpu_allreduce_f32.argtypes = [I, PP, S, P, I]
         L.oracle_f32_to_f16.argtypes = [ctypes.c_float]
         L.oracle_f32_to_f16.restype = ctypes.c_uint16
@@ -127,6 +128,13 @@ def fill(dtype: int, seed: int, count: int, kind: int = 0) -> np.ndarray:
     """splitmix64 synthetic input: kind 0 uniform [-1,1) / full-range ints, 1 dyadic."""
     out = np.empty(count, dtype=NP_STORAGE[dtype])
     lib().oracle_fill(dtype, seed, count, out.ctypes.data, kind)
+    return out
+
+
+def fill_at(dtype: int, seed: int, start: int, count: int, kind: int = 0) -> np.ndarray:
+    """Elements [start, start + count) of fill(dtype, seed, ...) (a rank's slice without the whole buffer)."""
+    out = np.empty(count, dtype=NP_STORAGE[dtype])
+    lib().oracle_fill_at(dtype, seed, start, count, out.ctypes.data, kind)
     return out
 
 

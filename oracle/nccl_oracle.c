@@ -390,28 +390,32 @@ static inline uint64_t splitmix64(uint64_t x) {
 /* kind 0: uniform in [-1,1) (24-bit grid, rounded RNE to T for small floats; full range for ints,
  *         with INT_MIN/INT_MAX-style extremes at i%1024==1 / ==2);
  * kind 1: dyadic k/256 with |k| <= 1024 (exact sums for fp32 up to 2^14 terms). */
-void oracle_fill(int dt, uint64_t seed, size_t count, void* out, int kind) {
+/* elements [start, start + count) of the sequence oracle_fill produces (out[0] = element start) */
+void oracle_fill_at(int dt, uint64_t seed, size_t start, size_t count, void* out, int kind) {
 #pragma omp parallel for schedule(static)
-  for (size_t i = 0; i < count; i++) {
+  for (size_t j = 0; j < count; j++) {
+    const size_t i = start + j;
     uint64_t r = splitmix64(seed * 0x100000001b3ull ^ (uint64_t)i);
     if (is_int(dt)) {
       uint64_t m = mask_of(dt), sign = m ^ (m >> 1);
       uint64_t v = r & m;
       if (i % 1024 == 1) v = sign;       /* INT_MIN bit pattern for signed types */
       else if (i % 1024 == 2) v = sign - 1; /* INT_MAX */
-      st(dt, out, i, v);
+      st(dt, out, j, v);
       continue;
     }
     double x;
     if (kind == 1) x = (double)((int64_t)(r % 2049) - 1024) / 256.0;
     else x = (double)((int64_t)(r >> 40) - (1ll << 23)) / (double)(1 << 23);
     switch (dt) {
-      case DT_F32: st(dt, out, i, f2u((float)x)); break;
-      case DT_F64: { uint64_t u; memcpy(&u, &x, 8); st(dt, out, i, u); break; }
-      default: st(dt, out, i, f_to_sf(dt, (float)x)); break;
+      case DT_F32: st(dt, out, j, f2u((float)x)); break;
+      case DT_F64: { uint64_t u; memcpy(&u, &x, 8); st(dt, out, j, u); break; }
+      default: st(dt, out, j, f_to_sf(dt, (float)x)); break;
     }
   }
 }
+
+void oracle_fill(int dt, uint64_t seed, size_t count, void* out, int kind) { oracle_fill_at(dt, seed, 0, count, out, kind); }
 
 /* ---------------- naive OpenMP CPU baseline ---------------- */
 
