@@ -109,7 +109,7 @@ def _time_ms(fn, stream, iters: int, warmup: int = 3) -> float:
 def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: dict | None = None) -> dict:
     """The other BASELINE.json configs at this N (the driver runs bench.py on the 8-GPU node, so this is
     where they get measured): RS+AG bf16 1 GiB bucket (configs[2]), AllReduce fp16 8 B..256 MiB sweep,
-    one-shot vs direct (configs[3]), Reduce int32 min/max 128 MiB root 0 (configs[4]); each with a
+    LL / one-shot / direct / ring / tree (configs[3]: the reference's ring vs tree), Reduce int32 min/max 128 MiB root 0 (configs[4]); each with a
     size-independent exactness check, plus xGMI peer-copy probes for the roofline denominator."""
     import torch
     import nccl_amd
@@ -173,7 +173,8 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     buf = torch.empty(top // 2, dtype=torch.float16, device="cuda").uniform_(-1, 1)
     res = torch.empty_like(buf)
     cols = {"ll": {"NCCL_PROTO": "LL"}, "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
-            "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"}, "default": {}}
+            "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
+            "ring": {"NCCL_ALGO": "RING"}, "tree": {"NCCL_ALGO": "TREE"}, "default": {}}
     limits = {"ll": 512 * 1024, "oneshot": 64 * MIB}
     rows = {}
     saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION")}
@@ -374,12 +375,13 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
             "method": "pinned hipMemcpyAsync H2D + ncclAllReduce + D2H on one stream, HIP events"}
 
 
-def cpu_baseline(n: int, count: int, budget_s: float):
-    """Naive OpenMP host reduction of n synthetic buffers, bounded to ~budget_s."""
+def cpu_baseline(count: int, budget_s: float, nbuf: int = 8):
+    """Naive host-core OpenMP element-wise sum of `nbuf` fp32 buffers of `count` elements (BASELINE.md §3:
+    the same splitmix64 inputs as the oracle, the oracle's fold order), bounded to ~budget_s. The default
+    nbuf = 8 is the 8-GPU node's reduction (one buffer per rank); GB/s over (nbuf + 1) * S host bytes."""
     import numpy as np
     import oracle
-    rng = np.random.default_rng(0x5EED0000)
-    bufs = [rng.random(count, dtype=np.float32) * 2 - 1 for _ in range(n)]
+    bufs = [oracle.fill(7, 0x5EED0000 + r, count) for r in range(nbuf)]
     out, used = oracle.cpu_allreduce_f32(bufs)  # warm-up
     times = []
     t_end = time.perf_counter() + budget_s
@@ -400,9 +402,38 @@ def cpu_baseline(n: int, count: int, budget_s: float):
                     break
     except OSError:
         pass
-    return {"value": round((n + 1) * S / t / 1e9, 2), "unit": "GB/s (host bytes: n reads + 1 write)",
-            "cores": int(used), "kind": "port",
-            "sample": f"{len(times)} runs x {n} x {S // MIB} MiB fp32 host buffers, median; cpu '{model}'"}
+    del bufs, out
+    return {"value": round((nbuf + 1) * S / t / 1e9, 2), "unit": f"GB/s (host bytes: {nbuf} reads + 1 write)",
+            "cores": int(used), "kind": "port", "ms_per_reduction": round(t * 1e3, 3),
+            "sample": f"{len(times)} runs of an OpenMP fp32 sum of {nbuf} x {S // MIB} MiB host buffers "
+                      f"(splitmix64, oracle fold order), median; {used} threads; cpu '{model}'"}
+
+
+def xgmi_denominator(n: int) -> dict | None:
+    """Measured link rates (tests/native/xgmi_probe, rank 0, GPU 0 -> its peers) as the xGMI roofline
+    denominator: n == 2 -> one link, unidirectional; n > 2 -> the fan-out to all peers scaled to n-1 links,
+    capped by (n-1) single links. The collective's own store flavour (write-through stores into uncached
+    staging) is measured beside the nontemporal rate and is what the kernel can reach."""
+    exe = os.path.join(ROOT, "tests", "native", "xgmi_probe")
+    if not os.path.exists(exe):
+        return None
+    import subprocess
+    try:
+        r = subprocess.run([exe, "256", "5"], capture_output=True, text=True, timeout=120)
+        pr = json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as e:  # a secondary measurement never costs the headline
+        return {"error": repr(e)}
+    if "error" in pr:
+        return pr
+    peers = pr["peers"]
+    one = pr.get("wt_uncached_write_1link_GBps") or pr["write_1link_GBps"]
+    fan = pr.get("wt_uncached_write_fanout_GBps") or pr["write_fanout_GBps"]
+    peak = one if n == 2 else min((n - 1) * one, fan * (n - 1) / peers)
+    return {"peak": round(peak, 1), "probe": pr,
+            "peak_basis": ("measured: one link, write-through stores into uncached peer memory (the kernel's own "
+                           "store flavour), GPU 0 -> GPU 1" if n == 2 else
+                           f"measured: GPU 0's write-through fan-out to all {peers} peers x {n - 1}/{peers}, capped "
+                           f"at {n - 1} x one link")}
 
 
 def load_pmc(workload_key: str):
@@ -507,10 +538,21 @@ def main(argv=None):
             "kernel": "copyKernel<4,true,true>" if n == 1 else "collKernel<float,0,0> (AllReduce, direct)",
             "algorithmic_bytes_per_launch": hbm_bytes, "kernel_avg_ms": round(gpu_ms, 5)}
     if n > 1:
-        link_peak = (n - 1) * XGMI_LINK_GBPS_DIR
-        roof["xgmi"] = {"busbw": round(busbw, 1), "peak": round(link_peak, 1), "unit": "GB/s",
-                        "frac": round(busbw / link_peak, 4),
-                        "peak_basis": f"{n - 1} links x {XGMI_LINK_GBPS_DIR} GB/s per direction (spec/2)"}
+        spec_peak = (n - 1) * XGMI_LINK_GBPS_DIR
+        meas = None
+        if rank == 0 and torch.cuda.device_count() >= n:  # ranks on separate GPUs: a real xGMI measurement
+            meas = xgmi_denominator(n)
+        xg = {"busbw": round(busbw, 1), "unit": "GB/s", "spec_peak": round(spec_peak, 1),
+              "spec_frac": round(busbw / spec_peak, 4),
+              "spec_basis": f"{n - 1} links x {XGMI_LINK_GBPS_DIR} GB/s per direction (153.6 GB/s spec / 2)"}
+        if meas and "peak" in meas:
+            xg.update(peak=meas["peak"], frac=round(busbw / meas["peak"], 4), peak_basis=meas["peak_basis"],
+                      probe=meas["probe"])
+        else:
+            xg.update(peak=round(spec_peak, 1), frac=round(busbw / spec_peak, 4),
+                      peak_basis="spec/2 (no multi-GPU link measurement in this run)" +
+                                 (f": {meas['error']}" if meas and "error" in meas else ""))
+        roof["xgmi"] = xg
 
     extra = {}
     if n == 1 and not args.no_extra and rank == 0:
@@ -536,7 +578,7 @@ def main(argv=None):
     cpu = None  # the contract's CPU baseline is an N=1 figure (rank 0 only)
     if n == 1 and rank == 0 and not args.no_cpu_baseline:
         try:
-            cpu = cpu_baseline(n, count, args.cpu_seconds)
+            cpu = cpu_baseline(count, args.cpu_seconds)
         except Exception as e:  # the baseline is reported, never required
             cpu = {"value": None, "error": repr(e)}
     barrier()

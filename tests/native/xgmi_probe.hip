@@ -26,14 +26,20 @@ struct Targets {
 };
 
 // workgroup b moves its share of pair (b % n): a grid-stride copy of `vecs` 16-byte vectors per pair
+template <bool WT>
 __global__ void __launch_bounds__(512) copyPairs(Targets t, size_t vecs) {
   const int pair = blockIdx.x % t.n;
   const size_t wgPerPair = gridDim.x / t.n;
   const size_t w = blockIdx.x / t.n;
   u32x4* d = t.dst[pair];
   const u32x4* s = t.src[pair];
-  for (size_t i = w * blockDim.x + threadIdx.x; i < vecs; i += wgPerPair * blockDim.x)
-    __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+  for (size_t i = w * blockDim.x + threadIdx.x; i < vecs; i += wgPerPair * blockDim.x) {
+    u32x4 v = __builtin_nontemporal_load(s + i);
+    if (WT)  // the collective kernels' remote store: write-through at system scope (kernels.h storeRemote)
+      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(d + i), "v"(v) : "memory");
+    else
+      __builtin_nontemporal_store(v, d + i);
+  }
 }
 
 int main(int argc, char** argv) {
@@ -52,10 +58,12 @@ int main(int argc, char** argv) {
   if (ndev > 8) ndev = 8;
   const size_t bytes = mib << 20;
   std::vector<void*> buf(ndev);
+  std::vector<void*> ubuf(ndev, nullptr);  // uncached peer buffers, like the collective's staging slabs
   for (int d = 0; d < ndev; d++) {
     CK(hipSetDevice(loop ? 0 : d));
     CK(hipMalloc(&buf[d], bytes));
     CK(hipMemset(buf[d], d, bytes));
+    CK(hipExtMallocWithFlags(&ubuf[d], bytes, hipDeviceMallocUncached));
   }
   CK(hipSetDevice(0));
   void* local2 = nullptr;
@@ -73,23 +81,27 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  auto run = [&](bool write, int npeers) -> double {
+  auto run = [&](bool write, int npeers, bool wt = false) -> double {
     Targets t = {};
     t.n = npeers;
     for (int k = 0; k < npeers; k++) {
       char* mine = (char*)local2 + (size_t)k * bytes;
       if (write) {
         t.src[k] = (const u32x4*)mine;
-        t.dst[k] = (u32x4*)buf[1 + k];
+        t.dst[k] = (u32x4*)(wt ? ubuf[1 + k] : buf[1 + k]);
       } else {
         t.src[k] = (const u32x4*)buf[1 + k];
         t.dst[k] = (u32x4*)mine;
       }
     }
     const int grid = (2 * cus / npeers) * npeers;
-    hipLaunchKernelGGL(copyPairs, dim3(grid), dim3(512), 0, s, t, bytes / 16);
+    auto launch = [&]() {
+      if (wt) hipLaunchKernelGGL(copyPairs<true>, dim3(grid), dim3(512), 0, s, t, bytes / 16);
+      else hipLaunchKernelGGL(copyPairs<false>, dim3(grid), dim3(512), 0, s, t, bytes / 16);
+    };
+    launch();
     CK(hipEventRecord(e0, s));
-    for (int i = 0; i < iters; i++) hipLaunchKernelGGL(copyPairs, dim3(grid), dim3(512), 0, s, t, bytes / 16);
+    for (int i = 0; i < iters; i++) launch();
     CK(hipEventRecord(e1, s));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -106,9 +118,12 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < bytes; i++) wrong += host[i] != 0xA5;
   }
   double r1 = run(false, 1), ra = run(false, all);
+  // the collective's own store flavour: write-through system-scope stores into uncached peer memory
+  double u1 = run(true, 1, true), ua = run(true, all, true);
   printf("{\"method\": \"CU copy kernel on GPU 0, 16-byte nontemporal vectors, %zu MiB per peer, %d iters%s\", "
          "\"peers\": %d, \"write_1link_GBps\": %.1f, \"read_1link_GBps\": %.1f, \"write_fanout_GBps\": %.1f, "
-         "\"read_fanin_GBps\": %.1f, \"wrong_bytes\": %zu}\n", mib, iters, loop ? ", LOOPBACK on one GPU" : "",
-         all, w1, r1, wa, ra, wrong);
+         "\"read_fanin_GBps\": %.1f, \"wt_uncached_write_1link_GBps\": %.1f, \"wt_uncached_write_fanout_GBps\": %.1f, "
+         "\"wrong_bytes\": %zu}\n", mib, iters, loop ? ", LOOPBACK on one GPU" : "",
+         all, w1, r1, wa, ra, u1, ua, wrong);
   return wrong ? 1 : 0;
 }
