@@ -275,6 +275,7 @@ struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src
   hipStream_t stream;
   CollArgs args;
   LLBatchArgs ll;  // ALGO_LL
+  CollBatchArgs batch;  // ALGO_DIRECT / ALGO_ONESHOT group batch when batch.nOps > 1 (collBatchKernel)
   int copyVariant;  // ALGO_COPY
   int64_t copyGrid;
   int pipeKind;     // ALGO_PIPE: PipeKind (pipe.h)
@@ -285,8 +286,6 @@ ncclResult_t enqueueCheck(CollInfo* info);
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin = true);
 ncclResult_t collFork(const CollInfo& info);
 bool llPlan(const CollInfo& info, LLOp* op);                  // LL eligibility + plan (enqueue.cc)
-bool llBatchable(const CollInfo& a, const CollInfo& b);
-ncclResult_t launchLLBatch(const std::vector<CollInfo>& ops);  // one LL launch for a group's small ARs
 
 // ---------------------------------------------------------------- tuner plugin (reference src/plugin/tuner.cc)
 enum TuneAlgo { TUNE_DEFAULT = 0, TUNE_LL = 1, TUNE_ONESHOT = 2, TUNE_DIRECT = 3 };
@@ -306,6 +305,18 @@ struct SymPlan {  // one symmetric (window) kernel launch
   SymArgs args;
 };
 ncclResult_t launchSymPlan(const SymPlan& plan);  // kernels.hip
+
+// planColl's outcome: a kernel launch (LaunchPlan), a symmetric-window launch (SymPlan) or nothing
+enum PlanKind { PLAN_KERNEL = 0, PLAN_SYM = 1, PLAN_NONE = 2 };
+struct PlannedColl {  // one op of a group, planned (group.cc)
+  CollInfo info;
+  int kind;
+  LaunchPlan p;
+  SymPlan sp;
+};
+ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kind);
+bool batchable(const std::vector<PlannedColl>& run, const PlannedColl& b);  // can b join run's launch?
+ncclResult_t launchBatch(std::vector<PlannedColl>& run);  // one launch for a run of batchable ops
 // window lookup: the window holding [p, p+bytes) with NCCL_WIN_COLL_SYMMETRIC, or nullptr (register.cc)
 ncclWindow_vidmem* findSymWindow(ncclComm* comm, const void* p, size_t bytes);
 void windowsFree(ncclComm* comm);  // release every window and IPC mapping (destroy/abort)

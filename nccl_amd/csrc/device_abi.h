@@ -89,8 +89,19 @@ struct CollArgs {
   int protoFlags;      // NCCL_AMD_PROTO_FLAGS diagnostics (kernels.h collKernel)
 };
 
-// LL AllReduce batch: up to kMaxLLBatch small AllReduce ops of one group (same comm, stream, type and
-// op) run by ONE launch (reference: ops of a group aggregated into one kernel plan, enqueue.cc:405-470).
+// Staged batch: up to kMaxCollBatch ops of one group with the same collective, type and op (and the same
+// one-shot / direct choice) in ONE collBatchKernel launch; op k runs on channels chOff[k] .. + nch[k] - 1.
+constexpr int kMaxCollBatch = 8;
+struct CollBatchArgs {
+  CollArgs op[kMaxCollBatch];
+  int chOff[kMaxCollBatch];
+  int nch[kMaxCollBatch];
+  int nOps;
+};
+
+// LL batch: up to kMaxLLBatch small ops of one group (same comm, stream, type and op; any of AllReduce,
+// ReduceScatter, AllGather, Reduce) run by ONE launch (reference: ops of a group aggregated into one kernel
+// plan, enqueue.cc:405-470).
 constexpr int kMaxLLBatch = 32;
 enum LLColl { LL_AR = 0, LL_RS = 1, LL_AG = 2, LL_REDUCE = 3 };
 struct LLOp {

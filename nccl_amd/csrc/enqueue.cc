@@ -257,50 +257,13 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   return true;
 }
 
-// Group aggregation: consecutive small AllReduce ops of one comm with the same stream, type and
-// operator become ONE LL launch (reference: a group's ops aggregated into one kernel plan,
-// enqueue.cc:405-470). ops[0..k) all passed llPlan; the caller forks/joins shared-GPU comms.
-ncclResult_t launchLLBatch(const std::vector<CollInfo>& ops) {
-  const CollInfo& f = ops[0];
-  ncclComm* comm = f.comm;
-  HIPCHECK(hipSetDevice(comm->device));
-  LaunchPlan p;
-  memset(&p, 0, sizeof(p));
-  p.func = FUNC_ALLREDUCE;
-  p.algo = ALGO_LL;
-  p.datatype = f.datatype;
-  p.eltSize = typeSize(f.datatype);
-  p.stream = comm->sharedDevInProcess ? comm->internalStream : f.stream;
-  const void* argPtr = nullptr;
-  NCCLCHECK(hostToDevRedOp(comm, f.op, f.datatype, &p.devOp, &p.ll.redArg, &argPtr));
-  p.ll.redArgPtr = argPtr;
-  p.ll.comm = comm->devComm;
-  p.ll.nOps = (int)ops.size();
-  int off = 0, used = 0;
-  for (size_t k = 0; k < ops.size(); k++) {
-    if (!llPlan(ops[k], &p.ll.ops[k])) return ncclInternalError;
-    p.ll.ops[k].chOff = off;
-    off = (off + p.ll.ops[k].nch) % comm->llChannels;
-    used += p.ll.ops[k].nch;
-    comm->opCount++;
-  }
-  p.nChannels = used < comm->llChannels ? used : comm->llChannels;
-  TRACE("LL batch: %d AllReduce ops, %d channels", p.ll.nOps, p.nChannels);
-  return launchPlan(p);
-}
-
-// Can `b` join the LL batch that `a` opened?
-bool llBatchable(const CollInfo& a, const CollInfo& b) {
-  return a.comm == b.comm && a.stream == b.stream && a.datatype == b.datatype && a.op == b.op &&
-         b.func == FUNC_ALLREDUCE && !a.comm->tune.noAggregation;
-}
-
-ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
+// Plan one op: the kernel launch (PLAN_KERNEL, in p), the symmetric-window launch (PLAN_SYM, in sp) or
+// nothing (PLAN_NONE). Every rank derives the same plan from what all ranks share.
+ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kind) {
   ncclComm* comm = info.comm;
-  HIPCHECK(hipSetDevice(comm->device));
   const int ts = typeSize(info.datatype);
-  LaunchPlan p;
   memset(&p, 0, sizeof(p));
+  *kind = PLAN_KERNEL;
   p.func = info.func;
   p.datatype = info.datatype;
   p.eltSize = ts;
@@ -320,17 +283,20 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   if (n == 1) {
     // reference taskAppend → ncclLaunchOneRank (enqueue.cc:3039-3041, onerank.cu:49-110)
     size_t bytes = info.count * (size_t)ts;
-    if (info.func == FUNC_REDUCE && info.recvbuff == nullptr) return ncclSuccess;
+    if (info.func == FUNC_REDUCE && info.recvbuff == nullptr) {
+      *kind = PLAN_NONE;
+      return ncclSuccess;
+    }
     if (p.devOp == DEV_PREMULSUM) {
       p.algo = ALGO_ONERANK;
       p.args.count = info.count;
-      return launchPlan(p);
+      return ncclSuccess;
     }
     p.algo = ALGO_COPY;
     p.bytes = bytes;
     p.copyVariant = comm->tune.copyVariant;
     p.copyGrid = comm->tune.copyGrid;
-    return launchPlan(p);
+    return ncclSuccess;
   }
 
   p.algo = ALGO_DIRECT;
@@ -392,7 +358,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     p.nChannels = p.ll.ops[0].nch;
     TRACE("%s: LL count %zu nch %d part %lu payloads", info.opName, count, p.nChannels,
           (unsigned long)p.ll.ops[0].part);
-    goto launch;
+    return ncclSuccess;
   }
   // The reference's own algorithms, forced with NCCL_ALGO=RING / TREE (pipe.h): the ring for AllReduce,
   // ReduceScatter and AllGather, the chain (the intra-node tree) for AllReduce; Reduce's ring is the chain
@@ -426,7 +392,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
       planChannels(comm, span, ts, p, (size_t)comm->tune.minChannelBytes, comm->chanCap);
       TRACE("%s: %s kind %d nch %d part %lu slice %lu steps %d", info.opName, ring ? "RING" : "TREE", kind,
             p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps);
-      goto launch;
+      return ncclSuccess;
     }
   }
   // Symmetric windows (reference: symmetric kernels for buffers in NCCL_WIN_COLL_SYMMETRIC windows,
@@ -438,7 +404,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     ncclWindow_vidmem* ws = findSymWindow(comm, info.sendbuff, sb);
     ncclWindow_vidmem* wr = ws ? findSymWindow(comm, info.recvbuff, rb) : nullptr;
     if (ws && wr) {
-      SymPlan sp;
+      *kind = PLAN_SYM;
       memset(&sp, 0, sizeof(sp));
       sp.datatype = info.datatype;
       sp.eltSize = ts;
@@ -496,11 +462,6 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
       sp.stream = info.stream;
       TRACE("%s: symmetric coll %d nch %d part %lu aligned %d", info.opName, sp.coll, nch, (unsigned long)part,
             sp.args.aligned);
-      if (!comm->sharedDevInProcess) return launchSymPlan(sp);
-      if (forkJoin) NCCLCHECK(collFork(info));
-      sp.stream = comm->internalStream;
-      NCCLCHECK(launchSymPlan(sp));
-      if (forkJoin) NCCLCHECK(collJoin(info));
       return ncclSuccess;
     }
   }
@@ -515,14 +476,106 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,
         p.args.nSteps, p.args.aligned);
-launch:
-  if (!comm->sharedDevInProcess) return launchPlan(p);
-  // on the comm's own hardware queue, between a fork and a join (see ncclComm::internalStream)
+  return ncclSuccess;
+}
+
+ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
+  ncclComm* comm = info.comm;
+  HIPCHECK(hipSetDevice(comm->device));
+  LaunchPlan p;
+  SymPlan sp;
+  int kind;
+  NCCLCHECK(planColl(info, p, sp, &kind));
+  if (kind == PLAN_NONE) return ncclSuccess;
+  // a comm sharing its GPU with other ranks of this process runs on its own hardware queue, between a fork
+  // and a join (see ncclComm::internalStream)
+  const bool shared =
+      comm->sharedDevInProcess && !(kind == PLAN_KERNEL && (p.algo == ALGO_COPY || p.algo == ALGO_ONERANK));
+  if (!shared) return kind == PLAN_SYM ? launchSymPlan(sp) : launchPlan(p);
   if (forkJoin) NCCLCHECK(collFork(info));
-  p.stream = comm->internalStream;
-  NCCLCHECK(launchPlan(p));
+  p.stream = sp.stream = comm->internalStream;
+  NCCLCHECK(kind == PLAN_SYM ? launchSymPlan(sp) : launchPlan(p));
   if (forkJoin) NCCLCHECK(collJoin(info));
   return ncclSuccess;
+}
+
+// ---- group aggregation (reference: a group's ops aggregated into one kernel plan, enqueue.cc:405-470) ----
+// Consecutive planned ops of one comm become one launch when they share the stream, type and operator and
+// were planned onto the same kernel: LL (any mix of AllReduce / ReduceScatter / AllGather / Reduce; the LL
+// kernel dispatches per op) or the staged kernel with the same collective and one-shot / direct choice
+// (collBatchKernel). Every rank of a comm issues the same op sequence and plans each op alike, so every
+// rank forms the same batches.
+static bool sameRedOp(const LaunchPlan& a, const LaunchPlan& b) {
+  return a.devOp == b.devOp && a.args.redArg == b.args.redArg && a.args.redArgPtr == b.args.redArgPtr;
+}
+
+bool batchable(const std::vector<PlannedColl>& run, const PlannedColl& b) {
+  if (run.empty()) return false;
+  const PlannedColl& a = run[0];
+  if (a.kind != PLAN_KERNEL || b.kind != PLAN_KERNEL || a.info.comm != b.info.comm || a.info.stream != b.info.stream ||
+      a.info.datatype != b.info.datatype || a.info.comm->tune.noAggregation || a.p.algo != b.p.algo)
+    return false;
+  if (a.p.algo == ALGO_LL) {
+    if (run.size() >= (size_t)kMaxLLBatch) return false;
+    // AllGather folds nothing: it joins any operator (its own plan carries none)
+    if (b.info.func == FUNC_ALLGATHER) return true;
+    for (const PlannedColl& x : run)
+      if (x.info.func != FUNC_ALLGATHER && !sameRedOp(x.p, b.p)) return false;
+    return true;
+  }
+  if (a.p.algo == ALGO_DIRECT || a.p.algo == ALGO_ONESHOT)
+    return run.size() < (size_t)kMaxCollBatch && a.info.func == b.info.func && sameRedOp(a.p, b.p) &&
+           a.p.args.protoFlags == b.p.args.protoFlags;
+  return false;
+}
+
+static const char* const kFuncName[] = {"AllReduce", "ReduceScatter", "AllGather", "Reduce"};
+
+// One launch for run[0..k) (batchable with each other, in order); the caller forks/joins shared-GPU comms.
+ncclResult_t launchBatch(std::vector<PlannedColl>& run) {
+  ncclComm* comm = run[0].info.comm;
+  HIPCHECK(hipSetDevice(comm->device));
+  LaunchPlan& p = run[0].p;
+  if (run[0].kind == PLAN_NONE) return ncclSuccess;
+  const bool shared =
+      comm->sharedDevInProcess && !(run[0].kind == PLAN_KERNEL && (p.algo == ALGO_COPY || p.algo == ALGO_ONERANK));
+  if (shared) p.stream = run[0].sp.stream = comm->internalStream;
+  if (run.size() == 1) return run[0].kind == PLAN_SYM ? launchSymPlan(run[0].sp) : launchPlan(p);
+  if (p.algo == ALGO_LL) {
+    int off = p.ll.ops[0].nch % comm->llChannels, used = p.ll.ops[0].nch;
+    for (size_t k = 1; k < run.size(); k++) {
+      LLOp& o = p.ll.ops[k];
+      o = run[k].p.ll.ops[0];
+      o.chOff = off;
+      off = (off + o.nch) % comm->llChannels;
+      used += o.nch;
+      // the batch kernel is typed by its folding ops; AllGather runs in any element type of its size
+      if (p.func == FUNC_ALLGATHER && run[k].info.func != FUNC_ALLGATHER) {
+        p.func = run[k].info.func;
+        p.devOp = run[k].p.devOp;
+        p.ll.redArg = run[k].p.ll.redArg;
+        p.ll.redArgPtr = run[k].p.ll.redArgPtr;
+      }
+    }
+    p.ll.nOps = (int)run.size();
+    p.nChannels = used < comm->llChannels ? used : comm->llChannels;
+    TRACE("LL batch: %d ops (first %s), %d channels", p.ll.nOps, kFuncName[run[0].info.func], p.nChannels);
+    return launchPlan(p);
+  }
+  CollBatchArgs& b = p.batch;
+  int off = 0, used = 0;
+  for (size_t k = 0; k < run.size(); k++) {
+    b.op[k] = run[k].p.args;
+    b.nch[k] = run[k].p.nChannels;
+    b.chOff[k] = off;
+    off = (off + b.nch[k]) % comm->chanCap;
+    used += b.nch[k];
+  }
+  b.nOps = (int)run.size();
+  p.nChannels = used < comm->chanCap ? used : comm->chanCap;
+  TRACE("staged batch: %d %s ops (%s), %d channels", b.nOps, kFuncName[run[0].info.func],
+        p.algo == ALGO_ONESHOT ? "one-shot" : "direct", p.nChannels);
+  return launchPlan(p);
 }
 
 // Fork / join of a shared-GPU comm's internal stream with the caller's stream. A group issues every

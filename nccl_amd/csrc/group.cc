@@ -74,31 +74,25 @@ ncclResult_t groupEndInternal() {
   (void)hipGetDevice(&dev);
   ncclResult_t r = ncclSuccess;
   for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = collFork(colls[i]);
-  // launches in group order per comm; runs of small AllReduce ops (same comm/stream/type/op) that all
-  // take the LL protocol become one launch. Every rank of a comm issues the same op sequence, so every
-  // rank forms the same batches.
-  std::map<ncclComm*, std::vector<CollInfo>> open;
+  // launches in group order per comm; consecutive ops that planned onto the same kernel with the same stream,
+  // type and operator become one launch (enqueue.cc batchable / launchBatch). Every rank of a comm issues the
+  // same op sequence, so every rank forms the same batches.
+  std::map<ncclComm*, std::vector<PlannedColl>> open;
   auto flush = [&](ncclComm* c) -> ncclResult_t {
-    std::vector<CollInfo>& run = open[c];
-    ncclResult_t res = ncclSuccess;
-    if (run.size() == 1) res = launchColl(run[0], false);
-    else if (run.size() > 1) res = launchLLBatch(run);
+    std::vector<PlannedColl>& run = open[c];
+    ncclResult_t res = run.empty() ? ncclSuccess : launchBatch(run);
     run.clear();
     return res;
   };
-  LLOp probe;
   for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) {
-    const CollInfo& c = colls[i];
-    std::vector<CollInfo>& run = open[c.comm];
-    const bool ll = c.func == FUNC_ALLREDUCE && llPlan(c, &probe);
-    if (ll && !run.empty() && llBatchable(run[0], c) && run.size() < (size_t)kMaxLLBatch) {
-      run.push_back(c);
-      continue;
-    }
-    r = flush(c.comm);
+    PlannedColl pc;
+    pc.info = colls[i];
+    (void)hipSetDevice(pc.info.comm->device);
+    r = planColl(pc.info, pc.p, pc.sp, &pc.kind);
     if (r != ncclSuccess) break;
-    if (ll) run.push_back(c);
-    else r = launchColl(c, false);
+    std::vector<PlannedColl>& run = open[pc.info.comm];
+    if (!batchable(run, pc)) r = flush(pc.info.comm);
+    if (r == ncclSuccess) run.push_back(pc);
   }
   for (auto& kv : open)
     if (r == ncclSuccess) r = flush(kv.first);

@@ -341,6 +341,9 @@ struct Channel {
   // MY OWN RS staging (area "for p", a local copy) and owner p's fold reads it from there over xGMI,
   // instead of A writing it into p's staging. Same link bytes as reads; slots, credits and flags unchanged.
   bool rsPull;
+  // the op's own channel index, which cuts its data (sliceRange); c is the physical channel (workgroup)
+  // whose staging, flags and credits carry it. They differ only inside a group batch (collBatchKernel).
+  int cl;
   static constexpr uint64_t ts = sizeof(T);
 
   __device__ uint64_t blockLen(int q) const {
@@ -382,7 +385,7 @@ struct Channel {
       if (!owns(p)) continue;
       const int b = blockOf(p);
       uint64_t lo, hi;
-      sliceRange(a, c, step, blockLen(b), lo, hi);
+      sliceRange(a, cl, step, blockLen(b), lo, hi);
       int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
       char* dst = rsPull ? dc.staging[me] + stagingOffset(dc, c, STG_RS, slot, p)   // my slab, area for p
                          : dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me);
@@ -423,7 +426,7 @@ struct Channel {
     }
     const int myB = blockOf(me);
     uint64_t lo, hi;
-    sliceRange(a, c, step, blockLen(myB), lo, hi);
+    sliceRange(a, cl, step, blockLen(myB), lo, hi);
     const uint64_t nelem = hi - lo;
     if (tid == 0) {
       int np = 0;
@@ -490,7 +493,7 @@ struct Channel {
     __syncthreads();
     if (!waitAll(dc, sh.st, myFlags(FLG_RS_ACK), sh.want, forceAcq)) return false;
     uint64_t lo, hi;
-    sliceRange(a, c, step, a.count, lo, hi);
+    sliceRange(a, cl, step, a.count, lo, hi);
     const char* src = (const char*)a.sendbuff + lo * ts;
     for (int k = 1; k < n; k++) {
       int p = peerAt(k);
@@ -517,7 +520,7 @@ struct Channel {
     __syncthreads();
     if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, !noAcq)) return false;
     uint64_t lo, hi;
-    sliceRange(a, c, step, a.count, lo, hi);
+    sliceRange(a, cl, step, a.count, lo, hi);
     for (uint64_t x = lo; x < hi;) {
       const int owner = (int)(x / a.chunk);
       const uint64_t end = min(hi, (uint64_t)(owner + 1) * a.chunk);
@@ -559,7 +562,7 @@ struct Channel {
       int q = (me + n - k) % n;
       const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
       uint64_t lo, hi;
-      sliceRange(a, c, step, blockLen(b), lo, hi);
+      sliceRange(a, cl, step, blockLen(b), lo, hi);
       const int slot = (int)(ctr(recvKind, q) % nSlots);
       const char* src = agPull ? dc.staging[q] + stagingOffset(dc, c, STG_AG, slot, q)  // q's own copy, remote
                                : dc.staging[me] + stagingOffset(dc, c, STG_AG, slot, q);
@@ -579,25 +582,37 @@ struct Channel {
   }
 };
 
-template <typename T, int OP, int COLL>
-__global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
-  __shared__ Shared sh;
-  const DevComm& dc = *a.comm;
+// Per-channel credit counters live in device memory between launches; a workgroup keeps them in LDS.
+__device__ __forceinline__ void loadCounters(const DevComm& dc, Shared& sh, int c) {
   const int tid = threadIdx.x;
-  const int c = blockIdx.x;
   if (tid < CTR_KINDS * NCCL_AMD_MAX_RANKS) {
     int k = tid / NCCL_AMD_MAX_RANKS, r = tid % NCCL_AMD_MAX_RANKS;
     sh.st.ctr[k][r] = dc.counters[ctrIndex(c, k, r)];
   }
   if (tid == 0) sh.st.abort = 0;
   __syncthreads();
-
-  uint64_t opArg = a.redArg;
-  if (a.redArgPtr) {  // ncclScalarDevice PreMulSum: dereference at run time (reference onerank.cu:31-41)
-    opArg = 0;
-    __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
+}
+__device__ __forceinline__ void storeCounters(const DevComm& dc, Shared& sh, int c) {
+  __syncthreads();
+  const int tid = threadIdx.x;
+  if (tid < CTR_KINDS * NCCL_AMD_MAX_RANKS) {
+    int k = tid / NCCL_AMD_MAX_RANKS, r = tid % NCCL_AMD_MAX_RANKS;
+    dc.counters[ctrIndex(c, k, r)] = sh.st.ctr[k][r];
   }
-  const Red<T, OP> fn(opArg);
+}
+// The functor's scalar: ncclScalarDevice PreMulSum dereferences it at run time (reference onerank.cu:31-41).
+template <typename T>
+__device__ __forceinline__ uint64_t redArgOf(uint64_t arg, const void* ptr) {
+  if (!ptr) return arg;
+  uint64_t v = 0;
+  __builtin_memcpy(&v, ptr, sizeof(T));
+  return v;
+}
+
+// One op's logical channel cl on physical channel c. False once a wait timed out (the comm aborts).
+template <typename T, int OP, int COLL>
+__device__ __forceinline__ bool runChannel(const CollArgs& a, const DevComm& dc, Shared& sh, const Red<T, OP>& fn,
+                                           int c, int cl) {
   // protoFlags: 1 = acquire on credit waits too, 2 = release on credit signals too, 4 = C(s) before A(s+1),
   // 8 = no release fence before data flags (the default: every published byte is a write-through system-scope
   // store drained before the flag; NCCL_AMD_P2P_FENCE=1 clears it), 16 = AG pull
@@ -607,11 +622,12 @@ __global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
                           (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
                           (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0, (a.protoFlags & 64) != 0,
                           (COLL == COLL_AR || COLL == COLL_AG) && (a.protoFlags & 16) != 0,
-                          (COLL == COLL_AR || COLL == COLL_RS) && (a.protoFlags & 32) != 0};
+                          (COLL == COLL_AR || COLL == COLL_RS) && (a.protoFlags & 32) != 0, cl};
   if (COLL == COLL_AR1) {
-    bool ok1 = true;
-    for (int s = 0; ok1 && s < a.nSteps; s++) ok1 = ch.oneShotA(s) && ch.oneShotB(s);
-  } else {
+    bool ok = true;
+    for (int s = 0; ok && s < a.nSteps; s++) ok = ch.oneShotA(s) && ch.oneShotB(s);
+    return ok;
+  }
   constexpr bool hasA = COLL != COLL_AG;
   const bool hasC = COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && ch.isRoot);
   // Pipeline: A(0); for s: B(s); A(s+1); C(s). Hoisting A(s+1) above C(s) lets the owners start
@@ -624,12 +640,40 @@ __global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
     if (ok && hasA && s + 1 < a.nSteps) ok = ch.phaseA(s + 1);
     if (ok && hasC && !cFirst) ok = ch.phaseC(s);
   }
+  return ok;
+}
+
+template <typename T, int OP, int COLL>
+__global__ void __launch_bounds__(kThreads) kCoResident collKernel(CollArgs a) {
+  __shared__ Shared sh;
+  const DevComm& dc = *a.comm;
+  const int c = blockIdx.x;
+  loadCounters(dc, sh, c);
+  const Red<T, OP> fn(redArgOf<T>(a.redArg, a.redArgPtr));
+  runChannel<T, OP, COLL>(a, dc, sh, fn, c, c);
+  storeCounters(dc, sh, c);
+}
+
+// Group batch (reference: a group's ops aggregated into one kernel plan, enqueue.cc:405-470): up to
+// kMaxCollBatch staged ops of one comm with the same collective, type and operator in ONE launch. Op k's
+// channels are the physical channels chOff[k] .. chOff[k] + nch[k] - 1 (mod the grid), so consecutive ops run
+// side by side on disjoint workgroups while the grid lasts and in op order on a shared one after that. Each
+// rank forms the same batches with the same offsets, so every physical channel runs the same handshake
+// sequence on every rank and its credits and slots carry over from op to op exactly as between launches.
+template <typename T, int OP, int COLL>
+__global__ void __launch_bounds__(kThreads) kCoResident collBatchKernel(CollBatchArgs b) {
+  __shared__ Shared sh;
+  const DevComm& dc = *b.op[0].comm;
+  const int c = blockIdx.x;
+  loadCounters(dc, sh, c);
+  const Red<T, OP> fn(redArgOf<T>(b.op[0].redArg, b.op[0].redArgPtr));
+  for (int k = 0; k < b.nOps; k++) {
+    int j = c - b.chOff[k];
+    if (j < 0) j += (int)gridDim.x;
+    if (j >= b.nch[k]) continue;
+    if (!runChannel<T, OP, COLL>(b.op[k], dc, sh, fn, c, j)) break;
   }
-  __syncthreads();
-  if (tid < CTR_KINDS * NCCL_AMD_MAX_RANKS) {
-    int k = tid / NCCL_AMD_MAX_RANKS, r = tid % NCCL_AMD_MAX_RANKS;
-    dc.counters[ctrIndex(c, k, r)] = sh.st.ctr[k][r];
-  }
+  storeCounters(dc, sh, c);
 }
 
 }  // namespace ncclamd
@@ -1022,6 +1066,15 @@ inline void launchLL(const LaunchPlan& p) {
   else launchLLK<T, OP, kMaxLLBatch>(p);
 }
 
+// the staged kernel: one op, or a group batch (collBatchKernel)
+template <typename T, int OP, int COLL>
+inline void launchColl(const LaunchPlan& p) {
+  if (p.batch.nOps > 1)
+    hipLaunchKernelGGL((collBatchKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.batch);
+  else
+    hipLaunchKernelGGL((collKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+}
+
 template <typename T, int OP>
 inline ncclResult_t launchTyped(const LaunchPlan& p) {
   if (p.algo == ALGO_ONERANK) {
@@ -1046,30 +1099,21 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
   }
   switch (p.func) {
     case FUNC_ALLREDUCE:
-      if (p.algo == ALGO_LL)
-        launchLL<T, OP>(p);
-      else if (p.algo == ALGO_ONESHOT)
-        hipLaunchKernelGGL((collKernel<T, OP, COLL_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
-      else
-        hipLaunchKernelGGL((collKernel<T, OP, COLL_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_LL) launchLL<T, OP>(p);
+      else if (p.algo == ALGO_ONESHOT) launchColl<T, OP, COLL_AR1>(p);
+      else launchColl<T, OP, COLL_AR>(p);
       break;
     case FUNC_REDUCESCATTER:
-      if (p.algo == ALGO_LL)
-        launchLL<T, OP>(p);
-      else
-        hipLaunchKernelGGL((collKernel<T, OP, COLL_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_LL) launchLL<T, OP>(p);
+      else launchColl<T, OP, COLL_RS>(p);
       break;
     case FUNC_REDUCE:
-      if (p.algo == ALGO_LL)
-        launchLL<T, OP>(p);
-      else
-        hipLaunchKernelGGL((collKernel<T, OP, COLL_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_LL) launchLL<T, OP>(p);
+      else launchColl<T, OP, COLL_REDUCE>(p);
       break;
     case FUNC_ALLGATHER:
-      if (p.algo == ALGO_LL)
-        launchLL<T, 0>(p);
-      else
-        hipLaunchKernelGGL((collKernel<T, 0, COLL_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+      if (p.algo == ALGO_LL) launchLL<T, 0>(p);
+      else launchColl<T, 0, COLL_AG>(p);
       break;
   }
   HIPCHECK(hipGetLastError());

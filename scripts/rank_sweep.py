@@ -3,7 +3,7 @@ so rank 0 can run under rocprofv3 without any process being spawned from a profi
 
 usage: rank_sweep.py RANK NRANKS DIR [CONFIGS_JSON]
   CONFIGS_JSON: list of {"name": str, "env": {...}, "coll": "allreduce"|"rs"|"ag", "dtype": int,
-                         "mib": per-rank MiB, "iters": int}
+                         "mib": per-rank MiB, "iters": int, "group": K (allreduce: K ops of mib/K in one group)}
 Each config gets its own communicator (the engine reads its knobs at init). Rank 0 creates the unique id
 of config k and writes DIR/uid_k; the others wait for it. Every rank times its own stream with HIP events
 and appends one JSON line per config to DIR/rank<R>.jsonl; results are checked on dyadic / small-integer
@@ -62,7 +62,18 @@ def main():
         if dt == 7:
             base = base / 256
         send = base * (rank + 1)
-        if coll == "allreduce":
+        K = int(cfg.get("group", 0))
+        if coll == "allreduce" and K:  # one group of K AllReduces over K equal slices of the buffer
+            recv = torch.empty_like(send)
+            per = cnt // K
+
+            def fn():
+                with nccl_amd.group():
+                    for i in range(K):
+                        comm.all_reduce_raw(send.data_ptr() + i * per * es, recv.data_ptr() + i * per * es, per, dt,
+                                            0, s.cuda_stream)
+            want = lambda: base * (n * (n + 1) // 2)
+        elif coll == "allreduce":
             recv = torch.empty_like(send)
             fn = lambda: comm.all_reduce_raw(send.data_ptr(), recv.data_ptr(), cnt, dt, 0, s.cuda_stream)
             want = lambda: base * (n * (n + 1) // 2)

@@ -368,6 +368,110 @@ def test_tuner_plugin(built, force, nch):
         assert sum(" LL count" in l for l in ar) >= 2 and any("nch 2 " in l for l in ar), ar
 
 
+# Group aggregation beyond small AllReduces (group.cc, enqueue.cc batchable / launchBatch; reference
+# enqueue.cc:405-440): each group is (name, dtype, [(coll, count, op, root)], the batches each comm must log).
+# Counts follow gpu_cases.launch: ReduceScatter = total elements (n x recvcount), AllGather = sendcount.
+# n = 2 fp32 size table: LL up to 128 KiB per AllReduce buffer / rank block, one-shot AllReduce up to 1 MiB.
+BATCH_GROUPS = [
+    ("mixed-size ReduceScatters", 9, [("reducescatter", 2 * c, 0, 0) for c in
+                                      (100, 2000, 8192, 30_000, 100_000, 300_000, 70_000, 1_000_000)],
+     [("LL", 4), ("staged", 4)]),
+    ("AllGathers", 7, [("allgather", c, 0, 0) for c in (60_000, 100_000, 500_000)], [("staged", 3)]),
+    ("Reduces max to root 1", 2, [("reduce", c, 2, 1) for c in (100_000, 400_000, 200_004)], [("staged", 3)]),
+    ("one-shot AllReduces", 7, [("allreduce", c, 0, 0) for c in (40_000, 100_000, 250_000)], [("staged", 3)]),
+    ("direct AllReduces, two operators", 7, [("allreduce", 1_000_000, 0, 0), ("allreduce", 600_000, 0, 0),
+                                             ("allreduce", 1_000_000, 2, 0), ("allreduce", 700_001, 2, 0)],
+     [("staged", 2), ("staged", 2)]),
+    ("LL mix of collectives", 7, [("allreduce", 1000, 2, 0), ("allgather", 5000, 0, 0), ("allreduce", 3, 2, 0),
+                                  ("reducescatter", 2 * 500, 2, 0), ("reduce", 100, 0, 0)], [("LL", 4)]),
+]
+
+
+def _batch_worker(q, rank=None, uid=None):
+    """rank None: both ranks in this process (init_all on one GPU); else one rank of a 2-process comm."""
+    try:
+        import re
+        os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "30000"
+        logf = f"/tmp/nccl_amd_batch_{os.getpid()}.log"
+        os.environ["NCCL_DEBUG"] = "TRACE"
+        os.environ["NCCL_DEBUG_FILE"] = logf
+        import torch
+        import nccl_amd
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        n = 2
+        mine = list(range(n)) if rank is None else [rank]
+        comms = nccl_amd.Communicator.init_all([0, 0]) if rank is None else [nccl_amd.Communicator.init(n, rank, uid)]
+        streams = [torch.cuda.Stream() for _ in mine]
+        errs, logs = [], []
+        for gi, (name, dt, ops, _) in enumerate(BATCH_GROUPS):
+            ins = [G.make_inputs(n, dt, cnt, seed=900 + 10 * gi + i) for i, (_, cnt, _, _) in enumerate(ops)]
+            bufs = [[] for _ in mine]
+            for k, r in enumerate(mine):
+                for i, (coll, cnt, op, root) in enumerate(ops):
+                    _, sv = G.to_device(ins[i][r], "cuda")
+                    _, rv = G.to_device(np.zeros(G.out_count(coll, n, cnt), dtype=ins[i][r].dtype), "cuda")
+                    bufs[k].append((sv, rv))
+            torch.cuda.synchronize()
+            pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+            with nccl_amd.group():
+                for k in range(len(mine)):
+                    for i, (coll, cnt, op, root) in enumerate(ops):
+                        G.launch(comms[k], coll, bufs[k][i][0], bufs[k][i][1], cnt, dt, op, root, streams[k].cuda_stream)
+            torch.cuda.synchronize()
+            errs += [f"{name}: async {c.async_error()}" for c in comms if c.async_error()]
+            for i, (coll, cnt, op, root) in enumerate(ops):
+                want = G.expected(coll, ins[i], dt, op, root)
+                for k, r in enumerate(mine):
+                    if coll == "reduce" and r != root:
+                        continue
+                    got = G.from_device(bufs[k][i][1], ins[i][r].dtype)
+                    if not G.same_bits(got, want[0] if coll == "reduce" else want[r], dt):
+                        errs.append(f"{name}: op {i} ({coll} {cnt}) rank {r} differs")
+            with open(logf) as f:
+                f.seek(pos)
+                logs.append(re.findall(r"(LL|staged) batch: (\d+) ", f.read()))
+        for c in comms:
+            c.destroy()
+        q.put((errs, logs))
+    except Exception as e:
+        q.put(([f"exception {e!r}"], []))
+
+
+@pytest.mark.parametrize("procs", [1, 2])
+def test_group_batches_every_collective(built, procs):
+    """Consecutive ops of a group that plan onto the same kernel become ONE launch per comm: mixed-size
+    ReduceScatters (an LL batch and a staged batch), AllGathers, Reduces, one-shot and direct AllReduces
+    (split where the operator changes) and an LL mix of collectives. Every result bit-exact vs the oracle;
+    the launch count is read from the NCCL_DEBUG=TRACE batch lines (fresh processes: logging starts once).
+    procs=1: both ranks in one process (shared-GPU internal streams); procs=2: one process per rank."""
+    import multiprocessing as mp
+    import queue
+    import nccl_amd
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    uid = nccl_amd.get_unique_id() if procs == 2 else None
+    ps = [ctx.Process(target=_batch_worker, args=(q,) + ((r, uid) if procs == 2 else ())) for r in range(procs)]
+    for p in ps:
+        p.start()
+    res = []
+    try:
+        for _ in ps:
+            res.append(q.get(timeout=240))
+    except queue.Empty:
+        for p in ps:
+            p.kill()
+        raise AssertionError("batch worker timed out")
+    for p in ps:
+        p.join(timeout=60)
+    for errs, _ in res:
+        assert not errs, errs
+    for gi, (name, _, _, want) in enumerate(BATCH_GROUPS):
+        got = sorted((k, int(v)) for _, logs in res for k, v in logs[gi])
+        assert got == sorted(want * 2), (name, got)  # one batch per comm (rank)
+
+
 def test_nonblocking_init_from_one_thread(built):
     """config.blocking = 0 (reference init.cc, nccl.h.in:84-108): ncclCommInitRankConfig returns
     ncclInProgress at once, so ONE thread can create both ranks without a group; ncclCommGetAsyncError
