@@ -103,3 +103,29 @@ tests/native/plan_test: tests/native/plan_test.cc $(SRCDIR)/enqueue.cc $(SRCDIR)
 	  $(SRCDIR)/enqueue.cc $(SRCDIR)/debug.cc -lpthread
 
 .PHONY: plan-test
+
+# Host sanitizer builds (SURVEY §5 race detection; tests/test_sanitizers.py): the bootstrap, the IPC fd server
+# and the planning code under ASan+UBSan and, separately, TSan. Host code only — no GPU code is instrumented.
+SANCXX   := $(CXX) -g -O1 -fno-omit-frame-pointer -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude
+ASAN     := -fsanitize=address,undefined -fno-sanitize-recover=undefined
+TSAN     := -fsanitize=thread
+HIPRT    := -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
+SANBIN   := build/asan/bootstrap_test build/asan/plan_test build/asan/ipc_server_test \
+            build/tsan/bootstrap_test build/tsan/ipc_server_test
+sanitize: $(SANBIN)
+
+build/asan/bootstrap_test build/tsan/bootstrap_test: tests/native/bootstrap_test.cc $(SRCDIR)/bootstrap.cc $(SRCDIR)/debug.cc $(HDRS)
+	@mkdir -p $(dir $@)
+	$(SANCXX) $(if $(findstring asan,$@),$(ASAN),$(TSAN)) -o $@ tests/native/bootstrap_test.cc $(SRCDIR)/bootstrap.cc \
+	  $(SRCDIR)/debug.cc -lpthread
+
+build/asan/ipc_server_test build/tsan/ipc_server_test: tests/native/ipc_server_test.cc $(SRCDIR)/ipc.cc $(SRCDIR)/debug.cc $(HDRS)
+	@mkdir -p $(dir $@)
+	$(SANCXX) $(if $(findstring asan,$@),$(ASAN),$(TSAN)) -o $@ tests/native/ipc_server_test.cc $(SRCDIR)/ipc.cc \
+	  $(SRCDIR)/debug.cc -lpthread $(HIPRT)
+
+build/asan/plan_test: tests/native/plan_test.cc $(SRCDIR)/enqueue.cc $(SRCDIR)/debug.cc $(HDRS)
+	@mkdir -p $(dir $@)
+	$(SANCXX) $(ASAN) -o $@ tests/native/plan_test.cc $(SRCDIR)/enqueue.cc $(SRCDIR)/debug.cc -lpthread
+
+.PHONY: sanitize

@@ -110,6 +110,8 @@ ncclResult_t ipcServerStart(ncclComm* comm);
 void ipcServerStop(ncclComm* comm);
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d);
 void ipcUnexport(ncclComm* comm, const IpcDesc& d);
+ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d);  // serve an fd (owned) under a new key
+ncclResult_t ipcFetchFd(const IpcDesc& d, int* fd);  // an exporter's fd for d, over its fd server (bounded)
 ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out);
 void ipcRelease(IpcImport* m);
 

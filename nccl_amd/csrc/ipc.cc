@@ -171,13 +171,24 @@ ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
     HIPCHECK(hipIpcGetMemHandle(&d->handle, base));
     return ncclSuccess;
   }
-  FdServer* s = comm->fdServer;
-  if (!s) {
+  if (!comm->fdServer) {
     WARN("ipc: no fd server on rank %d", comm->rank);
     return ncclInternalError;
   }
   int fd = -1;
   HIPCHECK(hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0));
+  return ipcPublish(comm, fd, size, d);
+}
+
+// Serve fd (owned from here on) under a fresh key until ipcUnexport / ipcServerStop.
+ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d) {
+  FdServer* s = comm->fdServer;
+  if (!s) {
+    close(fd);
+    return ncclInternalError;
+  }
+  d->size = size;
+  d->legacy = 0;
   d->key = gKeySerial++;
   memcpy(d->server, s->name, sizeof(d->server));
   std::lock_guard<std::mutex> g(s->mu);
@@ -196,7 +207,7 @@ void ipcUnexport(ncclComm* comm, const IpcDesc& d) {
   s->table.erase(it);
 }
 
-static ncclResult_t fetchFd(const IpcDesc& d, int* out) {
+ncclResult_t ipcFetchFd(const IpcDesc& d, int* out) {
   struct sockaddr_un a;
   socklen_t al = abstractAddr(d.server, &a);
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ipcTimeoutMs());
@@ -246,7 +257,7 @@ ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
     return ncclSuccess;
   }
   int fd = -1;
-  NCCLCHECK(fetchFd(d, &fd));
+  NCCLCHECK(ipcFetchFd(d, &fd));
   hipExternalMemoryHandleDesc hd;
   memset(&hd, 0, sizeof(hd));
   hd.type = hipExternalMemoryHandleTypeOpaqueFd;

@@ -1,40 +1,55 @@
 // Host-only test of the TCP bootstrap (nccl_amd/csrc/bootstrap.cc): the parent creates a unique id,
 // forks nranks children that rendezvous, all-gather a payload, barrier, and verify. No GPU needed.
+// Mode "threads" runs the ranks as threads of one process instead (as ncclCommInitAll and a group of inits
+// do): the form the TSan build checks (tests/test_sanitizers.py).
 #include <sys/wait.h>
 #include <unistd.h>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 #include "../../nccl_amd/csrc/core.h"
 using namespace ncclamd;
 
+static int runRank(ncclUniqueId* id, int r, int n, int rounds) {
+  Bootstrap* b = nullptr;
+  if (bootstrapInit(id, r, n, &b) != ncclSuccess) return 3;
+  for (int k = 0; k < rounds; k++) {
+    std::vector<uint64_t> v(n * 4, 0);
+    for (int j = 0; j < 4; j++) v[r * 4 + j] = 1000ull * r + k * 10 + j;
+    if (bootstrapAllGather(b, v.data(), 4 * sizeof(uint64_t)) != ncclSuccess) return 4;
+    for (int q = 0; q < n; q++)
+      for (int j = 0; j < 4; j++)
+        if (v[q * 4 + j] != 1000ull * q + k * 10 + j) return 5;
+    if (bootstrapBarrier(b) != ncclSuccess) return 6;
+  }
+  bootstrapClose(b);
+  return 0;
+}
+
 int main(int argc, char** argv) {
   int n = argc > 1 ? atoi(argv[1]) : 4;
   int rounds = argc > 2 ? atoi(argv[2]) : 3;
+  const bool threads = argc > 3 && !strcmp(argv[3], "threads");
   ncclUniqueId id;
   if (bootstrapGetUniqueId(&id) != ncclSuccess) return 2;
+  int bad = 0;
+  if (threads) {
+    std::vector<int> rc(n, -1);
+    std::vector<std::thread> ts;
+    for (int r = 0; r < n; r++) ts.emplace_back([&, r]() { rc[r] = runRank(&id, r, n, rounds); });
+    for (auto& t : ts) t.join();
+    for (int x : rc) bad += x != 0;
+    printf("bootstrap_test threads n=%d rounds=%d failures=%d\n", n, rounds, bad);
+    return bad ? 1 : 0;
+  }
   std::vector<pid_t> kids;
   for (int r = 0; r < n; r++) {
     pid_t p = fork();
-    if (p == 0) {
-      Bootstrap* b = nullptr;
-      if (bootstrapInit(&id, r, n, &b) != ncclSuccess) _exit(3);
-      for (int k = 0; k < rounds; k++) {
-        std::vector<uint64_t> v(n * 4, 0);
-        for (int j = 0; j < 4; j++) v[r * 4 + j] = 1000ull * r + k * 10 + j;
-        if (bootstrapAllGather(b, v.data(), 4 * sizeof(uint64_t)) != ncclSuccess) _exit(4);
-        for (int q = 0; q < n; q++)
-          for (int j = 0; j < 4; j++)
-            if (v[q * 4 + j] != 1000ull * q + k * 10 + j) _exit(5);
-        if (bootstrapBarrier(b) != ncclSuccess) _exit(6);
-      }
-      bootstrapClose(b);
-      _exit(0);
-    }
+    if (p == 0) _exit(runRank(&id, r, n, rounds));
     kids.push_back(p);
   }
-  int bad = 0;
   for (pid_t p : kids) {
     int st = 0;
     waitpid(p, &st, 0);

@@ -6,9 +6,14 @@
 //   plan_test NRANKS FUNC(ar|rs|ag|reduce) DTYPE COUNT [ALIGN_OFFSET_BYTES] [CHANCAP]
 // prints one line: algo=<copy|onerank|direct|oneshot|ll|ring|chain> nch=<channels> part=<elements|payloads>
 //                  slice=<elements> steps=<n> chunk=<elements>
+//   plan_test NRANKS batch FUNC:DTYPE:COUNT[:OP] ...
+// plans the ops as one group (enqueue.cc planColl / batchable / launchBatch, in group.cc's order) and prints one
+// line per launch: algo=<...> ops=<ops in the launch> grid=<workgroups> ranges=<chOff+nch per op, comma-separated>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <vector>
 
 #include "../../nccl_amd/csrc/core.h"
 
@@ -26,9 +31,24 @@ namespace ncclamd {
 static LaunchPlan gPlan;
 static SymPlan gSym;
 static int gKind = -1;  // 0 LaunchPlan, 1 SymPlan
+static bool gBatchMode = false;
+static const char* kAlgoNames[] = {"copy", "onerank", "direct", "oneshot", "ll", "pipe"};
 ncclResult_t launchPlan(const LaunchPlan& p) {
   gPlan = p;
   gKind = 0;
+  if (gBatchMode) {  // one line per launch
+    printf("algo=%s", kAlgoNames[p.algo]);
+    if (p.algo == ALGO_LL) {
+      printf(" ops=%d grid=%d ranges=", p.ll.nOps, p.nChannels);
+      for (int k = 0; k < p.ll.nOps; k++) printf("%s%d+%d", k ? "," : "", p.ll.ops[k].chOff, p.ll.ops[k].nch);
+    } else if (p.batch.nOps > 1) {
+      printf(" ops=%d grid=%d ranges=", p.batch.nOps, p.nChannels);
+      for (int k = 0; k < p.batch.nOps; k++) printf("%s%d+%d", k ? "," : "", p.batch.chOff[k], p.batch.nch[k]);
+    } else {
+      printf(" ops=1 grid=%d ranges=0+%d", p.nChannels, p.nChannels);
+    }
+    printf("\n");
+  }
   return ncclSuccess;
 }
 ncclResult_t launchSymPlan(const SymPlan& p) {
@@ -53,9 +73,10 @@ int main(int argc, char** argv) {
   }
   const int n = atoi(argv[1]);
   const char* f = argv[2];
-  const int dt = atoi(argv[3]);
-  const size_t count = strtoull(argv[4], nullptr, 0);
-  const size_t off = argc > 5 ? strtoull(argv[5], nullptr, 0) : 0;
+  const bool batch = !strcmp(f, "batch");
+  const int dt = batch ? 0 : atoi(argv[3]);
+  const size_t count = batch ? 0 : strtoull(argv[4], nullptr, 0);
+  const size_t off = !batch && argc > 5 ? strtoull(argv[5], nullptr, 0) : 0;
   ncclComm comm;
   comm.startMagic = comm.endMagic = kCommMagic;
   comm.rank = 0;
@@ -68,9 +89,39 @@ int main(int argc, char** argv) {
   comm.slotBytes = ((size_t)1 << 30) / (256 * 2 * 2 * (n > 1 ? n : 2));
   if (comm.slotBytes > ((size_t)1 << 20)) comm.slotBytes = (size_t)1 << 20;
   if (comm.slotBytes < ((size_t)16 << 10)) comm.slotBytes = (size_t)16 << 10;
-  comm.chanCap = argc > 6 ? atoi(argv[6]) : 256;
+  comm.chanCap = !batch && argc > 6 ? atoi(argv[6]) : 256;
   comm.devComm = (DevComm*)0x1000;
   loadTuning(&comm.tune);
+  if (batch) {
+    // the group.cc loop: plan in order, extend the open run while batchable, else launch it
+    gBatchMode = true;
+    std::vector<PlannedColl> run;
+    for (int i = 3; i < argc; i++) {
+      char fn[16] = {};
+      int dtype = 7, op = 0;
+      unsigned long long cnt = 0;
+      if (sscanf(argv[i], "%15[^:]:%d:%llu:%d", fn, &dtype, &cnt, &op) < 3) return 2;
+      PlannedColl pc;
+      memset(&pc.info, 0, sizeof(pc.info));
+      pc.info.func = !strcmp(fn, "rs") ? FUNC_REDUCESCATTER : !strcmp(fn, "ag") ? FUNC_ALLGATHER
+                   : !strcmp(fn, "reduce") ? FUNC_REDUCE : FUNC_ALLREDUCE;
+      pc.info.opName = fn;
+      pc.info.sendbuff = (const void*)(0x10000000ull * (i + 1));
+      pc.info.recvbuff = (void*)(0x10000000ull * (i + 1) + 0x8000000ull);
+      pc.info.count = cnt;
+      pc.info.datatype = (ncclDataType_t)dtype;
+      pc.info.op = (ncclRedOp_t)op;
+      pc.info.comm = &comm;
+      if (planColl(pc.info, pc.p, pc.sp, &pc.kind) != ncclSuccess) return 1;
+      if (!batchable(run, pc)) {
+        if (!run.empty() && launchBatch(run) != ncclSuccess) return 1;
+        run.clear();
+      }
+      run.push_back(pc);
+    }
+    if (!run.empty() && launchBatch(run) != ncclSuccess) return 1;
+    return 0;
+  }
   CollInfo info;
   memset(&info, 0, sizeof(info));
   info.func = !strcmp(f, "rs") ? FUNC_REDUCESCATTER : !strcmp(f, "ag") ? FUNC_ALLGATHER
@@ -93,7 +144,7 @@ int main(int argc, char** argv) {
            (unsigned long)gSym.args.chunk);
     return 0;
   }
-  const char* names[] = {"copy", "onerank", "direct", "oneshot", "ll", "pipe"};
+  const char* const* names = kAlgoNames;
   const char* pipes[] = {"ring", "ring", "ring", "chain", "chain"};
   const LaunchPlan& p = gPlan;
   if (p.algo == ALGO_PIPE) {

@@ -158,3 +158,54 @@ def test_forced_reference_algorithms(exe, func, algo, want):
             assert p["part"] * p["nch"] >= p["chunk"] and p["steps"] == -(-p["part"] // p["slice"])
             if want[0] == "chain":
                 assert p["chunk"] == count
+
+
+def batch(exe, n, *ops, **env):
+    """Plan ops as one group (plan_test batch mode): one dict per launch."""
+    e = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_")}
+    e.update({k: str(v) for k, v in env.items()})
+    out = subprocess.run([exe, str(n), "batch", *ops], env=e, capture_output=True, text=True, timeout=30)
+    assert out.returncode == 0, out.stdout + out.stderr
+    launches = []
+    for line in out.stdout.split("\n"):
+        if not line:
+            continue
+        d = dict(t.split("=") for t in line.split())
+        d["ranges"] = [tuple(int(x) for x in r.split("+")) for r in d["ranges"].split(",")]
+        d["ops"], d["grid"] = int(d["ops"]), int(d["grid"])
+        launches.append(d)
+    return launches
+
+
+def test_group_batches_by_kernel_type_and_operator(exe):
+    """Group aggregation (enqueue.cc batchable / launchBatch; reference enqueue.cc:405-440): consecutive ops
+    planned onto the same kernel with the same type and operator share one launch; the launch's channel ranges
+    stay inside its grid and are disjoint while the grid has room for every op."""
+    rs = [f"rs:9:{2 * c}" for c in (100, 2000, 8192, 30_000, 100_000, 300_000, 70_000, 1_000_000)]
+    got = batch(exe, 2, *rs, "ag:7:5000", "ar:7:1000:2", "ar:7:3:2", "reduce:7:100",
+                "ar:7:40000", "ar:7:100000", "ar:7:250000", "ar:7:1000000", "ar:7:600000:2")
+    assert [(l["algo"], l["ops"]) for l in got] == [("ll", 4), ("direct", 4), ("ll", 3), ("ll", 1), ("oneshot", 3),
+                                                    ("direct", 1), ("direct", 1)]
+    for l in got:
+        cap = 32 if l["algo"] == "ll" else 256
+        assert 1 <= l["grid"] <= cap
+        assert all(0 <= off < l["grid"] and 1 <= nch <= l["grid"] for off, nch in l["ranges"]), l
+        if sum(nch for _, nch in l["ranges"]) <= l["grid"]:
+            used = [c for off, nch in l["ranges"] for c in range(off, off + nch)]
+            assert len(used) == len(set(used)), l
+
+
+def test_group_batch_limits_and_opt_out(exe):
+    # at most 8 staged ops per launch (kMaxCollBatch), 32 LL ops (kMaxLLBatch)
+    got = batch(exe, 4, *(["ar:7:100000"] * 10))
+    assert [(l["algo"], l["ops"]) for l in got] == [("oneshot", 8), ("oneshot", 2)]
+    assert [l["ops"] for l in batch(exe, 8, *(["ar:7:100"] * 40))] == [32, 8]
+    # wrap-around once the ops need more channels than the grid: ranges stay in bounds
+    big = batch(exe, 2, *(["rs:7:40000000"] * 4))
+    assert big[0]["ops"] == 4 and big[0]["grid"] == 256
+    assert all(0 <= off < 256 for off, _ in big[0]["ranges"])
+    # different types never share a launch; NCCL_AMD_NO_AGGREGATION=1 launches every op alone
+    assert [l["ops"] for l in batch(exe, 2, "ar:7:100", "ar:9:100", "ar:7:100")] == [1, 1, 1]
+    assert [l["ops"] for l in batch(exe, 2, *(["ar:7:100"] * 3), NCCL_AMD_NO_AGGREGATION=1)] == [1, 1, 1]
+    # forced ring / chain plans are not batched (their own kernel)
+    assert [l["ops"] for l in batch(exe, 4, *(["ar:7:1000000"] * 3), NCCL_ALGO="RING")] == [1, 1, 1]
