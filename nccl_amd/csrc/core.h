@@ -103,6 +103,7 @@ struct IpcImport {  // one mapping of a peer's allocation in this process
   void* ext;  // hipExternalMemory_t
   int fd;
   int legacy;
+  uint64_t fdDev, fdIno;  // identity of fd at import (ipcRelease closes it only if it still names that file)
 };
 struct FdServer;
 bool ipcLegacy();

@@ -22,6 +22,7 @@
 #include <poll.h>
 #include <string.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/un.h>
 #include <unistd.h>
 
@@ -275,6 +276,11 @@ ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
   TRACE("ipc: imported %zu MiB from %s (fd %d %s after import)", (size_t)(d.size >> 20), d.server, fd,
         fcntl(fd, F_GETFD) != -1 ? "open" : "closed by the runtime");
   out->fd = fd;
+  struct stat st;
+  if (fstat(fd, &st) == 0) {
+    out->fdDev = (uint64_t)st.st_dev;
+    out->fdIno = (uint64_t)st.st_ino;
+  }
   hipExternalMemoryBufferDesc bd;
   memset(&bd, 0, sizeof(bd));
   bd.offset = 0;
@@ -298,9 +304,13 @@ void ipcRelease(IpcImport* m) {
   } else {
     (void)hipFree(m->ptr);
     (void)hipDestroyExternalMemory((hipExternalMemory_t)m->ext);
-    const bool open = m->fd >= 0 && fcntl(m->fd, F_GETFD) != -1;
-    TRACE("ipc: released mapping (fd %d %s)", m->fd, open ? "open: closing it" : "closed by the runtime");
-    if (open) close(m->fd);
+    // If the runtime closed the descriptor, its number may already name another file of this process (opened
+    // by another thread meanwhile): close it only while it still names the imported dma-buf.
+    struct stat st;
+    const bool mine = m->fd >= 0 && fstat(m->fd, &st) == 0 && (uint64_t)st.st_dev == m->fdDev &&
+                      (uint64_t)st.st_ino == m->fdIno;
+    TRACE("ipc: released mapping (fd %d %s)", m->fd, mine ? "still open: closing it" : "closed by the runtime");
+    if (mine) close(m->fd);
   }
   memset(m, 0, sizeof(*m));
 }
