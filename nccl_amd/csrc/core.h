@@ -95,7 +95,8 @@ struct IpcDesc {
   uint64_t key;
   uint64_t size;
   char server[40];  // abstract UNIX socket name of the exporter's fd server
-  int legacy;
+  int legacy;       // NCCL_AMD_IPC=legacy: handle only
+  int hasHandle;    // dma-buf export that also carries a hipIpc handle (import fallback, ipc.cc)
   hipIpcMemHandle_t handle;
 };
 struct IpcImport {  // one mapping of a peer's allocation in this process

@@ -158,11 +158,14 @@ static int runtimeVersion() {
   return v;  // major * 10000000 + minor * 100000 + patch
 }
 
+// torch's bundled ROCm 7.0 runtime never returns from hipIpcOpenMemHandle at 2 GiB or more (ipc.cc header)
+static bool legacyOpenable(size_t size) { return size < ((size_t)2 << 30) || runtimeVersion() >= 70200000; }
+
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
   memset(d, 0, sizeof(*d));
   d->size = size;
   if (ipcLegacy()) {
-    if (size >= ((size_t)2 << 30) && runtimeVersion() < 70200000) {
+    if (!legacyOpenable(size)) {
       // torch's bundled ROCm 7.0 runtime never returns from hipIpcOpenMemHandle at this size (ipc.cc header)
       WARN("ipc: a %zu MiB allocation cannot be shared with NCCL_AMD_IPC=legacy on HIP runtime %d "
            "(hipIpcOpenMemHandle stalls at >= 2 GiB); use the default dma-buf path", size >> 20, runtimeVersion());
@@ -178,7 +181,15 @@ ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
   }
   int fd = -1;
   HIPCHECK(hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0));
-  return ipcPublish(comm, fd, size, d);
+  NCCLCHECK(ipcPublish(comm, fd, size, d));
+  // A hipIpc handle rides along where the runtime can open it (below 2 GiB, or a 7.2+ runtime): an importer
+  // whose runtime cannot map the dma-buf (never seen on one GPU; the first multi-GPU node decides) falls back
+  // to it with a warning instead of failing the communicator.
+  if (legacyOpenable(size) && !paramInt("NCCL_AMD_IPC_NO_FALLBACK", 0)) {
+    if (hipIpcGetMemHandle(&d->handle, base) == hipSuccess) d->hasHandle = 1;
+    else (void)hipGetLastError();
+  }
+  return ncclSuccess;
 }
 
 // Serve fd (owned from here on) under a fresh key until ipcUnexport / ipcServerStop.
@@ -190,6 +201,7 @@ ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d) {
   }
   d->size = size;
   d->legacy = 0;
+  d->hasHandle = 0;
   d->key = gKeySerial++;
   memcpy(d->server, s->name, sizeof(d->server));
   std::lock_guard<std::mutex> g(s->mu);
@@ -250,15 +262,29 @@ ncclResult_t ipcFetchFd(const IpcDesc& d, int* out) {
   return ncclSuccess;
 }
 
-ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
-  memset(out, 0, sizeof(*out));
-  if (d.legacy) {
-    HIPCHECK(hipIpcOpenMemHandle(&out->ptr, d.handle, hipIpcMemLazyEnablePeerAccess));
-    out->legacy = 1;
-    return ncclSuccess;
-  }
+// Close an imported descriptor unless the runtime already did: its number may by then name another file of
+// this process (opened by another thread meanwhile), so only while it still names the imported dma-buf.
+static bool closeIfMine(int fd, uint64_t dev, uint64_t ino) {
+  struct stat st;
+  const bool mine = fd >= 0 && fstat(fd, &st) == 0 && (uint64_t)st.st_dev == dev && (uint64_t)st.st_ino == ino;
+  if (mine) close(fd);
+  return mine;
+}
+
+static ncclResult_t importLegacy(const IpcDesc& d, IpcImport* out) {
+  HIPCHECK(hipIpcOpenMemHandle(&out->ptr, d.handle, hipIpcMemLazyEnablePeerAccess));
+  out->legacy = 1;
+  return ncclSuccess;
+}
+
+static ncclResult_t importDmaBuf(const IpcDesc& d, IpcImport* out) {
   int fd = -1;
   NCCLCHECK(ipcFetchFd(d, &fd));
+  if (paramInt("NCCL_AMD_IPC_FAIL_DMABUF", 0)) {  // tests: exercise the fallback on a box where dma-buf works
+    close(fd);
+    WARN("ipc: NCCL_AMD_IPC_FAIL_DMABUF=1: refusing the dma-buf import");
+    return ncclUnhandledCudaError;
+  }
   hipExternalMemoryHandleDesc hd;
   memset(&hd, 0, sizeof(hd));
   hd.type = hipExternalMemoryHandleTypeOpaqueFd;
@@ -289,12 +315,27 @@ ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
   e = hipExternalMemoryGetMappedBuffer(&p, em, &bd);
   if (e != hipSuccess) {
     (void)hipDestroyExternalMemory(em);
+    closeIfMine(fd, out->fdDev, out->fdIno);
+    out->fd = -1;
     WARN("ipc: hipExternalMemoryGetMappedBuffer: %s", hipGetErrorString(e));
     return ncclUnhandledCudaError;
   }
   out->ptr = p;
   out->ext = em;
   return ncclSuccess;
+}
+
+ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
+  memset(out, 0, sizeof(*out));
+  out->fd = -1;
+  if (d.legacy) return importLegacy(d, out);
+  ncclResult_t r = importDmaBuf(d, out);
+  if (r == ncclSuccess || r == ncclRemoteError || !d.hasHandle) return r;  // exporter gone: nothing to fall back to
+  (void)hipGetLastError();
+  memset(out, 0, sizeof(*out));
+  WARN("ipc: dma-buf import of %zu MiB from %s failed; falling back to its hipIpc handle", (size_t)(d.size >> 20),
+       d.server);
+  return importLegacy(d, out);
 }
 
 void ipcRelease(IpcImport* m) {
@@ -304,13 +345,8 @@ void ipcRelease(IpcImport* m) {
   } else {
     (void)hipFree(m->ptr);
     (void)hipDestroyExternalMemory((hipExternalMemory_t)m->ext);
-    // If the runtime closed the descriptor, its number may already name another file of this process (opened
-    // by another thread meanwhile): close it only while it still names the imported dma-buf.
-    struct stat st;
-    const bool mine = m->fd >= 0 && fstat(m->fd, &st) == 0 && (uint64_t)st.st_dev == m->fdDev &&
-                      (uint64_t)st.st_ino == m->fdIno;
-    TRACE("ipc: released mapping (fd %d %s)", m->fd, mine ? "still open: closing it" : "closed by the runtime");
-    if (mine) close(m->fd);
+    const bool closed = closeIfMine(m->fd, m->fdDev, m->fdIno);
+    TRACE("ipc: released mapping (fd %d %s)", m->fd, closed ? "still open: closed it" : "closed by the runtime");
   }
   memset(m, 0, sizeof(*m));
 }

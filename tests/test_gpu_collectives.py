@@ -97,7 +97,9 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (4, {"NCCL_AMD_AG_PULL": "1"}),
             (3, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
             (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}),
-            (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"})]
+            (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"}),
+            # cross-process memory: every dma-buf import refused -> the hipIpc handle fallback (ipc.cc); legacy only
+            (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}), (2, {"NCCL_AMD_IPC": "legacy"})]
 
 
 @pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
