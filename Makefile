@@ -11,8 +11,10 @@ SRCDIR   := nccl_amd/csrc
 
 # -ffp-contract=off: never fuse x*s + acc into one FMA (PreMulSum parity).
 # -fno-gpu-flush-denormals-to-zero: keep fp32 denormals like the reference (no -ftz, common.mk:103).
+# EXTRA: extra defines for A/B builds of variants (e.g. EXTRA=-DNCCL_AMD_COPY_UNROLL=16 BUILD=build_ab LIBDIR=ablib/x)
+EXTRA    ?=
 COMMON   := -O3 -fPIC -std=c++17 -ffp-contract=off -fvisibility=hidden -Wall -Wno-unused-function \
-            -Wno-unused-variable -Wno-unused-but-set-variable -Iinclude
+            -Wno-unused-variable -Wno-unused-but-set-variable -Iinclude $(EXTRA)
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics
 HOSTSRC  := debug.cc bootstrap.cc ipc.cc transport.cc init.cc group.cc enqueue.cc register.cc tuner.cc
 HOSTOBJ  := $(HOSTSRC:%.cc=$(BUILD)/%.o)
@@ -20,7 +22,7 @@ DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf plan-test xgmi-probe
+all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf plan-test xgmi-probe atomicity-probe
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -129,3 +131,11 @@ build/asan/plan_test: tests/native/plan_test.cc $(SRCDIR)/enqueue.cc $(SRCDIR)/d
 	$(SANCXX) $(ASAN) -o $@ tests/native/plan_test.cc $(SRCDIR)/enqueue.cc $(SRCDIR)/debug.cc -lpthread
 
 .PHONY: sanitize
+
+# store-atomicity probe (torn 8/16/64/128-byte lines under concurrent write-through stores; GPU test + bench suite)
+atomicity-probe: tests/native/store_atomicity_probe
+
+tests/native/store_atomicity_probe: tests/native/store_atomicity_probe.hip
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
+
+.PHONY: atomicity-probe

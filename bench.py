@@ -172,13 +172,14 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     top = (16 if quick else 256) * MIB
     buf = torch.empty(top // 2, dtype=torch.float16, device="cuda").uniform_(-1, 1)
     res = torch.empty_like(buf)
-    cols = {"ll": {"NCCL_PROTO": "LL"}, "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
+    cols = {"ll": {"NCCL_PROTO": "LL"}, "ll128": {"NCCL_PROTO": "LL128"},
+            "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
             "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
             "ring": {"NCCL_ALGO": "RING"}, "tree": {"NCCL_ALGO": "TREE"}, "default": {}}
-    limits = {"ll": 512 * 1024, "oneshot": 64 * MIB}
+    limits = {"ll": 512 * 1024, "ll128": 896 * 1024, "oneshot": 64 * MIB}
     rows = {}
     saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION")}
-    for name, env in cols.items():
+    for name, env in cols.items():  # ll128: the LL64-line protocol (64-byte lines)
         for k in saved:
             os.environ.pop(k, None)
         os.environ.update(env)
@@ -346,6 +347,19 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                     {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
             except Exception as e:
                 probe["cu_kernel"] = {"error": repr(e)}
+        # single-copy atomicity over the link: GPU 1 writes LL-style lines into GPU 0's
+        # uncached memory while GPU 0 polls them; torn 8/16/64/128-byte lines are counted (LL needs torn8 == 0,
+        # an LL128-class protocol would need torn64 == torn128 == 0)
+        exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "store_atomicity_probe")
+        if os.path.exists(exe):
+            try:
+                import subprocess
+                r = subprocess.run([exe, "1", "0", "20000", "64", "3000"], capture_output=True, text=True,
+                                   timeout=60)
+                probe["store_atomicity"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 \
+                    else {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
+            except Exception as e:
+                probe["store_atomicity"] = {"error": repr(e)}
         out["xgmi_probe"] = probe
         del src, dsts
     return out

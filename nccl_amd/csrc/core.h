@@ -156,12 +156,15 @@ struct CommTuning {
   int protoFlags;           // NCCL_AMD_PROTO_FLAGS | (NCCL_AMD_P2P_FENCE=0 ? 8 : 0)
   int algo;                 // NCCL_ALGO: TuneAlgoForce (ONESHOT, DIRECT, RING, TREE)
   int llOn, simpleOn;       // NCCL_PROTO
+  int ll128On;              // NCCL_PROTO lists LL128, or NCCL_AMD_LL128=1: the LL64 line protocol (kernels.h)
   int symDisable;           // NCCL_AMD_SYM_DISABLE
   int symOneShot;           // NCCL_AMD_SYM_ONESHOT: caller promises out-of-place window AllReduces
   int noAggregation;        // NCCL_AMD_NO_AGGREGATION
   int64_t oneShotBytes;     // NCCL_AMD_ONESHOT_BYTES
   int64_t llBytes;          // NCCL_AMD_LL_BYTES
   int64_t llChannelBytes;   // NCCL_AMD_LL_CHANNEL_BYTES
+  int64_t ll128Bytes;       // NCCL_AMD_LL128_BYTES (upper end of the LL64 range)
+  int64_t ll128ChannelBytes;  // NCCL_AMD_LL128_CHANNEL_BYTES
   int64_t minChannelBytes;  // NCCL_AMD_MIN_CHANNEL_BYTES
   int64_t oneShotChannelBytes;  // NCCL_AMD_ONESHOT_CHANNEL_BYTES
   int copyVariant;          // NCCL_AMD_COPY_VARIANT (nRanks == 1 copy kernel, diagnostics)
@@ -292,10 +295,10 @@ ncclResult_t collFork(const CollInfo& info);
 bool llPlan(const CollInfo& info, LLOp* op);                  // LL eligibility + plan (enqueue.cc)
 
 // ---------------------------------------------------------------- tuner plugin (reference src/plugin/tuner.cc)
-enum TuneAlgo { TUNE_DEFAULT = 0, TUNE_LL = 1, TUNE_ONESHOT = 2, TUNE_DIRECT = 3 };
+enum TuneAlgo { TUNE_DEFAULT = 0, TUNE_LL = 1, TUNE_ONESHOT = 2, TUNE_DIRECT = 3, TUNE_LL128 = 4 };
 ncclResult_t tunerLoad(ncclComm* comm);
 void tunerUnload(ncclComm* comm);
-void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, bool llOk, int* algo, int* nch);
+void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int* algo, int* nch);
 ncclResult_t collJoin(const CollInfo& info);
 ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
 

@@ -20,6 +20,12 @@
 //     flag32} written by `from` with one write-through store; the flag is the channel's LL epoch, so the
 //     reader needs neither a flag word nor a fence. Parity = epoch & 1 (double buffering).
 //
+//   LL64 lines (the LL128-class protocol, at DevComm::ll64Offset; reference prims_ll128.h): same geometry,
+//     64-byte lines = 4 lanes x 16 bytes = 56 bytes of payload + the 64-bit epoch flag in the last 8 bytes.
+//     64 bytes, not the reference's 128: on MI355X a 128-byte line written by one wave-instruction is
+//     observed torn, 64-byte segments are not (tests/native/store_atomicity_probe).
+//     A separate area, so stale LL64 payload can never alias an LL flag position and vice versa.
+//
 //   counters (plain device memory, local)
 //     uint64 [channel][ctr kind < 5 (sendRS, recvRS, sendAG, recvAG, sym)][peer < NCCL_AMD_MAX_RANKS]
 //     Per-connection step counters (reference: conn->step, src/device/prims_simple.h:100-173),
@@ -66,6 +72,7 @@ struct DevComm {
   uint64_t* counters;                    // local step counters
   uint64_t llOffset;                     // LL line area inside every rank's flag allocation
   uint64_t llBytes;                      // line bytes per (channel, parity, sender)
+  uint64_t ll64Offset;                   // LL64 line area (same geometry as the LL area)
   int llChannels;
   uint32_t* abortFlag;                   // host-pinned; nonzero = abort
   uint32_t* errorWord;                   // host-pinned; first DevError recorded
@@ -104,6 +111,8 @@ struct CollBatchArgs {
 // plan, enqueue.cc:405-470).
 constexpr int kMaxLLBatch = 32;
 enum LLColl { LL_AR = 0, LL_RS = 1, LL_AG = 2, LL_REDUCE = 3 };
+enum LLProto { LLP_LL = 0, LLP_LL64 = 1 };
+constexpr int kLL64Payload = 56;  // payload bytes per 64-byte LL64 line
 struct LLOp {
   const void* send;
   void* recv;
@@ -114,6 +123,7 @@ struct LLOp {
   int chOff;       // first channel (batches spread their ops over the LL channels)
   int coll;        // LLColl
   int root;        // LL_REDUCE: the rank that folds and stores (the others send and poll only)
+  int proto;       // LLProto: LL (part = 8-byte payloads) or LL64 (part = 64-byte lines of 56 payload bytes)
 };
 // The kernel arguments hold room for K ops: a lone op launches with K = 1 (88 bytes of kernel arguments
 // instead of 1.8 KiB; the host issue cost of a launch grows with its argument bytes, about 3 us at 64 B
@@ -147,6 +157,9 @@ __host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int 
 }
 __host__ __device__ inline uint64_t llLineOffset(const DevComm& dc, int c, int parity, int from) {
   return dc.llOffset + (((uint64_t)c * 2 + parity) * dc.nRanks + from) * dc.llBytes;
+}
+__host__ __device__ inline uint64_t ll64LineOffset(const DevComm& dc, int c, int parity, int from) {
+  return dc.ll64Offset + (((uint64_t)c * 2 + parity) * dc.nRanks + from) * dc.llBytes;
 }
 __host__ __device__ inline uint64_t flagIndex(int c, int kind, int from) {
   return ((uint64_t)c * FLG_KINDS + kind) * NCCL_AMD_MAX_RANKS + from;

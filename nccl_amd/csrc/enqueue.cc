@@ -92,9 +92,12 @@ void loadTuning(CommTuning* t) {
     else WARN("NCCL_ALGO=%s: unknown here (ONESHOT, DIRECT, RING, TREE); using the size table", algo);
   }
   t->llOn = t->simpleOn = 1;
+  // LL128 class (LL64 lines, kernels.h ll64ChannelOp): off unless asked for, like the reference on paths
+  // whose 128-byte store atomicity is unproven (tuning.cc:518-536); the 8-GPU suite measures xGMI's
+  t->ll128On = (int)paramInt("NCCL_AMD_LL128", 0);
   if (const char* proto = paramStr("NCCL_PROTO")) {  // reference syntax: "LL,Simple" or "^LL128"
     bool exclude = proto[0] == '^';
-    bool hasLL = false, hasSimple = false;
+    bool hasLL = false, hasSimple = false, hasLL128 = false;
     std::string list(proto + (exclude ? 1 : 0));
     size_t pos = 0;
     while (true) {
@@ -102,12 +105,14 @@ void loadTuning(CommTuning* t) {
       std::string tok = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
       hasLL |= !strcasecmp(tok.c_str(), "LL");
       hasSimple |= !strcasecmp(tok.c_str(), "Simple");
+      hasLL128 |= !strcasecmp(tok.c_str(), "LL128");
       if (comma == std::string::npos) break;
       pos = comma + 1;
     }
     t->llOn = exclude ? !hasLL : hasLL;
     t->simpleOn = exclude ? !hasSimple : hasSimple;
-    if (!t->llOn && !t->simpleOn) {
+    t->ll128On = exclude ? (t->ll128On && !hasLL128) : hasLL128;
+    if (!t->llOn && !t->simpleOn && !t->ll128On) {
       WARN("NCCL_PROTO=%s leaves no protocol enabled; using Simple", proto);
       t->simpleOn = 1;
     }
@@ -119,6 +124,9 @@ void loadTuning(CommTuning* t) {
   t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)
   t->llChannelBytes = paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096);
   if (t->llChannelBytes < 8) t->llChannelBytes = 8;
+  t->ll128Bytes = paramInt("NCCL_AMD_LL128_BYTES", 0);  // 0: size table default (1 MiB / nRanks)
+  t->ll128ChannelBytes = paramInt("NCCL_AMD_LL128_CHANNEL_BYTES", 4096);
+  if (t->ll128ChannelBytes < kLL64Payload) t->ll128ChannelBytes = kLL64Payload;
   t->minChannelBytes = paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
   t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
   t->copyVariant = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
@@ -208,36 +216,52 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   const int ts = typeSize(info.datatype);
   const size_t bytes = info.count * (size_t)ts;  // payload space
   const size_t npk = (bytes + 7) / 8;
+  const size_t nLines = (bytes + kLL64Payload - 1) / kLL64Payload;  // LL64 lines
   const CommTuning& t = comm->tune;
   const bool blocked = info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER;
   const bool shape = !blocked || (bytes & 7) == 0;
   const bool fits = t.llOn && shape && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
+  const bool fits64 = t.ll128On && shape && nLines <= (size_t)comm->llChannels * (comm->llBytes / 64);
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
-  // NCCL_PROTO leaves only LL enabled.
+  // NCCL_PROTO leaves only LL-class protocols enabled.
   // LL lines carry 2x the payload to each of the n-1 peers: its range shrinks with n like the one-shot's
   // (default 256 KiB / n: 128 KiB at n=2, 32 KiB at n=8; for ReduceScatter / AllGather that is per rank
-  // block, i.e. 256 KiB of total data at any n, the same per-rank link bytes)
+  // block, i.e. 256 KiB of total data at any n, the same per-rank link bytes). LL64 lines carry 64/56 of
+  // it, so the LL128 class takes the next range (default up to 1 MiB / n) before one-shot / direct.
   const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : std::max<size_t>(16 << 10, ((size_t)256 << 10) / n);
-  bool useLL = fits && (!t.simpleOn || (t.algo == FORCE_NONE && bytes <= llLim));
+  const size_t ll64Lim = t.ll128Bytes > 0 ? (size_t)t.ll128Bytes : std::max<size_t>(64 << 10, ((size_t)1 << 20) / n);
+  const bool sized = t.algo == FORCE_NONE;
+  int proto = -1;
+  if (!t.simpleOn) {  // only LL-class protocols enabled: the range's protocol, else whichever fits
+    if (fits && (bytes <= llLim || !fits64)) proto = LLP_LL;
+    else if (fits64) proto = LLP_LL64;
+  } else if (fits && sized && bytes <= llLim) {
+    proto = LLP_LL;
+  } else if (fits64 && sized && bytes <= ll64Lim) {
+    proto = LLP_LL64;
+  }
   int tuned = TUNE_DEFAULT, tunedNch = 0;
   if (comm->tunerLoaded) {  // an external tuner plugin may overrule the size table (tuner.cc)
-    tunerPick(comm, info.func, blocked ? bytes * n : bytes, 1, fits, &tuned, &tunedNch);
-    if (tuned != TUNE_DEFAULT) useLL = fits && tuned == TUNE_LL;
+    tunerPick(comm, info.func, blocked ? bytes * n : bytes, 1, (fits ? 1 : 0) | (fits64 ? 2 : 0), &tuned, &tunedNch);
+    if (tuned != TUNE_DEFAULT) proto = (fits && tuned == TUNE_LL) ? LLP_LL : (fits64 && tuned == TUNE_LL128) ? LLP_LL64 : -1;
   }
-  if (!useLL) return false;
-  const uint64_t perCh = (uint64_t)t.llChannelBytes / 8;
-  int nch = (int)((npk + perCh - 1) / perCh);
-  if (tunedNch > 0 && (uint64_t)tunedNch * (comm->llBytes / 16) >= npk) nch = tunedNch;
+  if (proto < 0) return false;
+  // LL: 8-byte payloads, one 16-byte line each; LL64: 56-byte lines of 64 bytes
+  const uint64_t units = proto == LLP_LL ? npk : nLines;
+  const uint64_t unitLine = proto == LLP_LL ? 16 : 64;
+  const uint64_t perCh = proto == LLP_LL ? (uint64_t)t.llChannelBytes / 8 : (uint64_t)t.ll128ChannelBytes / kLL64Payload;
+  int nch = (int)((units + perCh - 1) / perCh);
+  if (tunedNch > 0 && (uint64_t)tunedNch * (comm->llBytes / unitLine) >= units) nch = tunedNch;
   if (nch < 1) nch = 1;
   if (nch > comm->llChannels) nch = comm->llChannels;
   if (nch > comm->chanCap) nch = comm->chanCap;
-  uint64_t part = (npk + nch - 1) / nch;
-  if (part * 16 > comm->llBytes) return false;
+  uint64_t part = (units + nch - 1) / nch;
+  if (part * unitLine > comm->llBytes) return false;
   // every channel of the op must carry at least one payload: an empty channel would advance its epoch
   // without exchanging lines, and the parity double-buffering (kernels.h llChannelOp) relies on each epoch
   // of a channel waiting for every peer's lines of the previous one (a tuner's channel count, or a tiny
   // NCCL_AMD_LL_CHANNEL_BYTES, can leave [lo,hi) empty for the last channels otherwise)
-  nch = (int)((npk + part - 1) / part);
+  nch = (int)((units + part - 1) / part);
   const uint64_t epp = 16 / ts;
   uint64_t blockElems = info.count;
   if (info.func == FUNC_ALLREDUCE) {
@@ -254,6 +278,7 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   op->coll = info.func == FUNC_ALLREDUCE ? LL_AR : info.func == FUNC_REDUCESCATTER ? LL_RS
            : info.func == FUNC_ALLGATHER ? LL_AG : LL_REDUCE;
   op->root = info.root;
+  op->proto = proto;
   return true;
 }
 
@@ -356,8 +381,8 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     p.ll.redArgPtr = p.args.redArgPtr;
     p.ll.nOps = 1;
     p.nChannels = p.ll.ops[0].nch;
-    TRACE("%s: LL count %zu nch %d part %lu payloads", info.opName, count, p.nChannels,
-          (unsigned long)p.ll.ops[0].part);
+    TRACE("%s: %s count %zu nch %d part %lu %s", info.opName, p.ll.ops[0].proto == LLP_LL64 ? "LL128(LL64)" : "LL",
+          count, p.nChannels, (unsigned long)p.ll.ops[0].part, p.ll.ops[0].proto == LLP_LL64 ? "lines" : "payloads");
     return ncclSuccess;
   }
   // The reference's own algorithms, forced with NCCL_ALGO=RING / TREE (pipe.h): the ring for AllReduce,
@@ -401,9 +426,10 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     size_t sb = count * ts, rb = count * ts;
     if (info.func == FUNC_REDUCESCATTER) sb *= n;
     if (info.func == FUNC_ALLGATHER) rb *= n;
-    ncclWindow_vidmem* ws = findSymWindow(comm, info.sendbuff, sb);
-    ncclWindow_vidmem* wr = ws ? findSymWindow(comm, info.recvbuff, rb) : nullptr;
-    if (ws && wr) {
+    // AllGather reads only peers' outputs (symKernel SYM_AG), so its sendbuff needs no window
+    ncclWindow_vidmem* ws = info.func == FUNC_ALLGATHER ? nullptr : findSymWindow(comm, info.sendbuff, sb);
+    ncclWindow_vidmem* wr = (ws || info.func == FUNC_ALLGATHER) ? findSymWindow(comm, info.recvbuff, rb) : nullptr;
+    if (wr && (ws || info.func == FUNC_ALLGATHER)) {
       *kind = PLAN_SYM;
       memset(&sp, 0, sizeof(sp));
       sp.datatype = info.datatype;
@@ -415,13 +441,11 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       sp.args.redArg = p.args.redArg;
       sp.args.redArgPtr = p.args.redArgPtr;
       uintptr_t al = 0;
-      // in-place AllGather: rank r's input is block r of ITS output, not the offset of mine
-      const bool agInPlace = info.func == FUNC_ALLGATHER &&
-                             (const char*)info.sendbuff == (const char*)info.recvbuff + (size_t)comm->rank * count * ts;
       for (int r = 0; r < n; r++) {
-        sp.args.send[r] = ws->peerPtr[r] + ((const char*)info.sendbuff - (const char*)ws->userPtr);
+        // AllGather: only my own input is read (peers' blocks come from their outputs)
+        if (ws) sp.args.send[r] = ws->peerPtr[r] + ((const char*)info.sendbuff - (const char*)ws->userPtr);
+        else sp.args.send[r] = r == comm->rank ? (const char*)info.sendbuff : nullptr;
         sp.args.recv[r] = wr->peerPtr[r] + ((char*)info.recvbuff - (char*)wr->userPtr);
-        if (agInPlace) sp.args.send[r] = sp.args.recv[r] + (size_t)r * count * ts;
         al |= (uintptr_t)sp.args.send[r] | (uintptr_t)sp.args.recv[r];
       }
       bool symAligned = (al & 15) == 0 && !comm->tune.forceElementwise;
@@ -516,7 +540,7 @@ bool batchable(const std::vector<PlannedColl>& run, const PlannedColl& b) {
       a.info.datatype != b.info.datatype || a.info.comm->tune.noAggregation || a.p.algo != b.p.algo)
     return false;
   if (a.p.algo == ALGO_LL) {
-    if (run.size() >= (size_t)kMaxLLBatch) return false;
+    if (run.size() >= (size_t)kMaxLLBatch || a.p.ll.ops[0].proto != b.p.ll.ops[0].proto) return false;
     // AllGather folds nothing: it joins any operator (its own plan carries none)
     if (b.info.func == FUNC_ALLGATHER) return true;
     for (const PlannedColl& x : run)

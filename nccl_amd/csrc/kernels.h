@@ -165,6 +165,11 @@ __device__ void signalAll(uint64_t* const* ptr, const uint64_t* val, int nsig, b
 #define NCCL_AMD_COPY_UNROLL 8
 #endif
 constexpr int kCopyUnroll = NCCL_AMD_COPY_UNROLL;
+// 16-byte packs per batch of the fold (types wider than one byte); each has its successor's loads in flight.
+#ifndef NCCL_AMD_FOLD_UNROLL
+#define NCCL_AMD_FOLD_UNROLL 4
+#endif
+constexpr int kFoldUnroll = NCCL_AMD_FOLD_UNROLL;
 
 // Copy [0,nbytes) from src to dst. Both 16-byte aligned when `aligned`; nbytes multiple of sizeof(T).
 template <typename T, bool REMOTE>
@@ -230,7 +235,7 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
   // separate registers, so they keep one pack per batch to stay within the register budget (kCoResident;
   // two packs spilled up to 55 VGPRs for fp8)
   constexpr bool kSwar = std::is_same<T, uint8_t>::value && Swar8<OP>::ok;
-  constexpr int U = sizeof(T) > 1 ? 4 : kSwar ? 2 : 1;
+  constexpr int U = sizeof(T) > 1 ? kFoldUnroll : kSwar ? 2 : 1;
   uint32_t swarMask = 0;
   if constexpr (kSwar) swarMask = (uint32_t)(uint8_t)fn.arg * 0x01010101u;
   if (aligned) {
@@ -843,11 +848,229 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
   return ok && !abortSh;
 }
 
+// LL64: the LL128-class protocol (reference prims_ll128.h) on the line size MI355X stores atomically. A line
+// is 64 bytes = 4 consecutive lanes x 16 bytes of one wave-instruction: lanes 0-2 carry 16 payload bytes,
+// lane 3 carries 8 payload bytes and the 64-bit epoch flag, so 56 of every 64 bytes on the link are payload
+// (LL: 8 of 16). The reader loads the whole line (4 lanes, one 16-byte system-scope load each) and accepts it
+// once lane 3 sees the flag: that relies on the line arriving as one unit, which the store-atomicity probe
+// measured for 64-byte segments (never torn) and refuted for 128-byte lines (torn in ~1.4 % of racing reads,
+// DESIGN.md §10.1). Payloads, fold order, batching, epochs and parity double-buffering are the LL kernel's;
+// the line area is its own (ll64LineOffset), so neither protocol can mistake the other's payload for a flag.
+__device__ __forceinline__ u32x4 loadLine16(const char* p) { return *(const volatile u32x4*)p; }  // polls
+// Re-reads of lines a poll has already seen complete: uncached memory, so a plain load cannot hit a stale
+// copy; not volatile, so the loads of several peers' lines can be in flight together.
+__device__ __forceinline__ u32x4 loadSeenLine16(const char* p) { return __builtin_nontemporal_load((const u32x4*)p); }
+
+template <typename T, int OP>
+__device__ __forceinline__ bool ll64ChannelOp(const DevComm& dc, const Red<T, OP>& fn, const LLOp& op, int c, int j,
+                                              uint64_t e64, int& abortSh) {
+  const int tid = threadIdx.x, lane = tid & 63, me = dc.rank, n = dc.nRanks;
+  constexpr int EPP = 8 / sizeof(T);
+  const uint32_t flag = (uint32_t)e64 ? (uint32_t)e64 : 1u;
+  const int par = (int)(e64 & 1);
+  // 32-bit indices (an op's payload space fits the line area, < 1 MiB): fewer live registers
+  const uint32_t nbytes = (uint32_t)(op.count * sizeof(T));
+  const uint32_t nLines = (nbytes + kLL64Payload - 1) / kLL64Payload;
+  const uint32_t lo = min((uint32_t)j * (uint32_t)op.part, nLines), hi = min(lo + (uint32_t)op.part, nLines);
+  const int u = tid & 3;  // my 16-byte unit of every line I touch (kThreads is a multiple of 4)
+  const char* send = (const char*)op.send;
+  char* recv = (char*)op.recv;
+  auto payload = [&](const char* base, uint32_t pk) -> uint64_t {  // 8 bytes at any alignment, 0 past the end
+    const char* p = base + pk * 8;
+    const uintptr_t al = (uintptr_t)p;
+    uint64_t v = 0;
+    if (pk * 8 + 8 <= nbytes) {
+      if ((al & 7) == 0) v = *(const uint64_t*)p;
+      else if ((al & 3) == 0) v = ((const uint32_t*)p)[0] | ((uint64_t)((const uint32_t*)p)[1] << 32);
+      else for (int b = 0; b < 8; b++) v |= (uint64_t)(unsigned char)p[b] << (8 * b);
+    } else {
+      for (uint32_t b = pk * 8; b < nbytes; b++) v |= (uint64_t)(unsigned char)base[b] << (8 * (b - pk * 8));
+    }
+    return v;
+  };
+  auto storePayload = [&](char* base, uint32_t pk, uint64_t v) {
+    if (pk * 8 >= nbytes) return;
+    char* p = base + pk * 8;
+    const uintptr_t al = (uintptr_t)p;
+    if (pk * 8 + 8 <= nbytes) {
+      if ((al & 7) == 0) {
+        *(uint64_t*)p = v;
+      } else if ((al & 3) == 0) {
+        ((uint32_t*)p)[0] = (uint32_t)v;
+        ((uint32_t*)p)[1] = (uint32_t)(v >> 32);
+      } else {
+        for (int b = 0; b < 8; b++) p[b] = (char)(v >> (8 * b));
+      }
+    } else {
+      for (uint32_t b = pk * 8; b < nbytes; b++) base[b] = (char)(v >> (8 * (b - pk * 8)));
+    }
+  };
+  const uint64_t flag64 = ((uint64_t)flag << 32) | flag;
+  // payload units of line L: 7L + 2u and 7L + 2u + 1 (u < 3), 7L + 6 (u == 3, beside the flag)
+  constexpr int kUnits = kLL64Payload / 8;
+
+  // send: unit u of lines [lo,hi) to every peer, one 16-byte write-through store per peer
+  for (uint32_t i = lo * 4 + tid; i < hi * 4; i += kThreads) {
+    const uint32_t pk = (i >> 2) * kUnits + 2 * u;
+    const uint32_t off = (i - lo * 4) * 16;
+    uint64_t v0 = 0, v1 = flag64;
+    if (op.coll != LL_RS) {
+      v0 = payload(send, pk);
+      if (u < 3) v1 = payload(send, pk + 1);
+    }
+    for (int k = 1; k < n; k++) {
+      int p = (me + k) % n;
+      if (op.coll == LL_RS) {  // block p goes to its owner
+        v0 = payload(send + (uint64_t)p * nbytes, pk);
+        if (u < 3) v1 = payload(send + (uint64_t)p * nbytes, pk + 1);
+      }
+      char* base = (char*)dc.flags[p] + ll64LineOffset(dc, c, par, me) + off;
+      storeRemote(base, u32x4{(uint32_t)v0, (uint32_t)(v0 >> 32), (uint32_t)v1, (uint32_t)(v1 >> 32)});
+    }
+  }
+  __syncthreads();
+  const uint64_t t0 = clockTicks();
+  bool ok = true;
+  const char* myLL = (const char*)dc.flags[me];
+  const bool folds = op.coll != LL_AG && !(op.coll == LL_REDUCE && me != op.root);
+  const char* mine = op.coll == LL_RS ? send + (uint64_t)me * nbytes : send;
+  // pass 1: wait until every peer's line of every line this thread handles carries this epoch's flag (seen by
+  // the group's lane 3). Lines are whole 4-lane groups and hi * 4 is a multiple of 4, so every lane a group
+  // reads with __shfl is active in the same iteration. All lines are polled before any is folded, so a
+  // thread with several lines waits once.
+  for (uint32_t i = lo * 4 + tid; ok && i < hi * 4; i += kThreads) {
+    const uint32_t off = (i - lo * 4) * 16;
+    uint32_t pending = 0;
+    for (int q = 0; q < n; q++)
+      if (q != me) pending |= 1u << q;
+    uint32_t spins = 0;
+    while (true) {
+      for (int q = 0; q < n; q++) {
+        if (q == me) continue;
+        const bool need = (pending >> q) & 1u;
+        bool mineOk = true;
+        if (need) {
+          const u32x4 v = loadLine16(myLL + ll64LineOffset(dc, c, par, q) + off);
+          mineOk = u != 3 || (v.z == flag && v.w == flag);
+        }
+        const bool lineOk = __shfl((int)mineOk, (lane & ~3) | 3) != 0;
+        if (need && lineOk) pending &= ~(1u << q);
+      }
+      if (!__any(pending != 0)) break;
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 1023) == 0) {
+        if (__hip_atomic_load(dc.abortFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          reportError(dc, DERR_ABORT);
+          abortSh = 1;
+        } else if (__hip_atomic_load(dc.errorWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) ||
+                   clockTicks() - t0 > dc.timeoutTicks) {
+          reportError(dc, DERR_TIMEOUT);
+          abortSh = 1;
+        }
+        if (abortSh) break;
+      }
+    }
+    if (pending) ok = false;
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the re-reads below stay behind the polls
+  // pass 2: re-read the lines (valid until epoch + 2) and place (AllGather) or fold them
+  for (uint32_t i = lo * 4 + tid; ok && i < hi * 4; i += kThreads) {
+    const uint32_t pk = (i >> 2) * kUnits + 2 * u;
+    const uint32_t off = (i - lo * 4) * 16;
+    if (op.coll == LL_AG) {  // place every peer's payload in its block, and my own
+      for (int q = 0; q < n; q++) {
+        char* dst = recv + (uint64_t)q * nbytes;
+        uint64_t v0, v1;
+        if (q == me) {
+          if (dst == send) continue;
+          v0 = payload(send, pk);
+          v1 = u < 3 ? payload(send, pk + 1) : 0;
+        } else {
+          const u32x4 v = loadSeenLine16(myLL + ll64LineOffset(dc, c, par, q) + off);
+          v0 = v.x | ((uint64_t)v.y << 32);
+          v1 = v.z | ((uint64_t)v.w << 32);
+        }
+        storePayload(dst, pk, v0);
+        if (u < 3) storePayload(dst, pk + 1, v1);
+      }
+      continue;
+    }
+    if (!folds) continue;  // Reduce: only the root folds, in its ring order root+1, ..., root
+    // each payload folds in its owner block's ring order; both of my payloads share the owner except at a
+    // block boundary, where the two are folded in separate passes
+    const bool two = u < 3 && (pk + 1) * 8 < nbytes;
+    auto ownerOf = [&](uint32_t q8) -> int {
+      return op.coll == LL_RS ? me : op.coll == LL_REDUCE ? op.root : (int)((q8 * 8 / sizeof(T)) / op.chunk);
+    };
+    const int own0 = ownerOf(pk), own1 = two ? ownerOf(pk + 1) : own0;
+    // source k of the fold order: my own payloads or peer q's line; the next source's load is issued before
+    // the current one is folded
+    auto fetch = [&](int owner, int k) -> u32x4 {
+      const int q = (owner + 1 + k) % n;
+      if (q == me) {
+        const uint64_t a = payload(mine, pk), b = two ? payload(mine, pk + 1) : 0;
+        return u32x4{(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32)};
+      }
+      return loadSeenLine16(myLL + ll64LineOffset(dc, c, par, q) + off);
+    };
+    // fold payload h (0: low 8 bytes of the unit, 1: high 8 bytes) in owner's order
+    auto foldOne = [&](int owner, int h) {
+      union { uint64_t u; T e[EPP]; } acc, x;
+      u32x4 nxt = fetch(owner, 0);
+      for (int k = 0; k < n; k++) {
+        const u32x4 cur = nxt;
+        if (k + 1 < n) nxt = fetch(owner, k + 1);
+        x.u = h ? (cur.z | ((uint64_t)cur.w << 32)) : (cur.x | ((uint64_t)cur.y << 32));
+#pragma unroll
+        for (int e = 0; e < EPP; e++) {
+          T y = fn.pre(x.e[e]);
+          acc.e[e] = k == 0 ? y : fn.red(y, acc.e[e]);
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EPP; e++) acc.e[e] = fn.post(acc.e[e]);
+      storePayload(recv, pk + h, acc.u);
+    };
+    // both payloads of the unit in one pass (same owner: everywhere but at a block boundary); 1-byte types
+    // unpack 8 elements per payload and always fold one payload per pass to stay within the register budget
+    if constexpr (sizeof(T) > 1) {
+      if (two && own0 == own1) {
+        union { uint64_t u; T e[EPP]; } acc0, acc1, x0, x1;
+        u32x4 nxt = fetch(own0, 0);
+        for (int k = 0; k < n; k++) {
+          const u32x4 cur = nxt;
+          if (k + 1 < n) nxt = fetch(own0, k + 1);
+          x0.u = cur.x | ((uint64_t)cur.y << 32);
+          x1.u = cur.z | ((uint64_t)cur.w << 32);
+#pragma unroll
+          for (int e = 0; e < EPP; e++) {
+            T y0 = fn.pre(x0.e[e]), y1 = fn.pre(x1.e[e]);
+            acc0.e[e] = k == 0 ? y0 : fn.red(y0, acc0.e[e]);
+            acc1.e[e] = k == 0 ? y1 : fn.red(y1, acc1.e[e]);
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < EPP; e++) {
+          acc0.e[e] = fn.post(acc0.e[e]);
+          acc1.e[e] = fn.post(acc1.e[e]);
+        }
+        storePayload(recv, pk, acc0.u);
+        storePayload(recv, pk + 1, acc1.u);
+        continue;
+      }
+    }
+    foldOne(own0, 0);
+    if (two) foldOne(own1, 1);
+  }
+  __syncthreads();  // every payload of this op is folded before the next op's lines go out
+  return ok && !abortSh;
+}
+
 // One launch runs a batch of LL ops (a single ReduceScatter / AllGather, or up to 32 AllReduces); op k occupies channels [chOff_k, chOff_k + nch_k) mod
 // llChannels, so the small ops of a batch land on different channels and run in parallel (one
 // round trip for the batch). A channel runs its ops in batch order and its epoch advances once per op
 // it takes part in; all ranks build the same batch, so epochs agree.
-template <typename T, int OP, int K>
+template <typename T, int OP, int K, int P>
 __global__ void __launch_bounds__(kThreads) kCoResident llKernel(LLArgs<K> a) {
   __shared__ int abortSh;
   const DevComm& dc = *a.comm;
@@ -866,7 +1089,10 @@ __global__ void __launch_bounds__(kThreads) kCoResident llKernel(LLArgs<K> a) {
     const int j = (c - a.ops[k].chOff + L) % L;  // op k runs on channels chOff, chOff+1, ... (mod L)
     if (j >= a.ops[k].nch) continue;
     e64++;
-    if (!llChannelOp<T, OP>(dc, fn, a.ops[k], c, j, e64, abortSh)) break;
+    // one protocol per launch (a batch holds ops of one protocol): each kernel keeps its own register budget
+    const bool ok = P == LLP_LL64 ? ll64ChannelOp<T, OP>(dc, fn, a.ops[k], c, j, e64, abortSh)
+                                  : llChannelOp<T, OP>(dc, fn, a.ops[k], c, j, e64, abortSh);
+    if (!ok) break;
   }
   if (threadIdx.x == 0) dc.counters[ctrIndex(c, CTR_LL, 0)] = e64;
 }
@@ -943,7 +1169,17 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     hi = min(lo + a.part, len);
   };
   bool ok;
-  symSignal(dc, sh, c, FLG_SYM_ENTER, e, false);
+  if (COLL == SYM_AG) {
+    // AllGather: my own block goes into my output BEFORE entry (skipped in place), so every peer pulls block
+    // q from rank q's output. No rank needs to know whether a peer runs in place or out of place (ranks may
+    // mix them), and a sendbuff outside any window is fine: only outputs are read remotely.
+    uint64_t lo, hi;
+    partOf(a.chunk, lo, hi);
+    char* dst = a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
+    const char* src = a.send[me] + lo * ts;
+    if (dst != src) copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
+  }
+  symSignal(dc, sh, c, FLG_SYM_ENTER, e, COLL == SYM_AG);  // AG: publishes that block
   ok = symWait(dc, sh, c, FLG_SYM_ENTER, e, true);
   if (ok && COLL == SYM_AR1) {
     // one-shot: fold my channel's portion of the whole buffer from all n inputs, owner block by block
@@ -975,20 +1211,13 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     ok = symWait(dc, sh, c, FLG_SYM_MID, e, true);
   }
   if (ok && (COLL == SYM_AR || COLL == SYM_AG)) {
-    // AG: pull every other rank's block part (AR: its reduced output; AG: its input)
+    // pull every other rank's block part from its output (AR: its reduced block; AG: its input block)
     for (int k = 1; k < n; k++) {
       const int q = (me + n - 1 - (k - 1 + c) % (n - 1)) % n;  // staggered by channel: all links busy
       uint64_t lo, hi;
       partOf(blockLen(q), lo, hi);
-      const char* src = COLL == SYM_AR ? a.recv[q] + ((uint64_t)q * a.chunk + lo) * ts : a.send[q] + lo * ts;
-      copyRange<T, false>(a.recv[me] + ((uint64_t)q * a.chunk + lo) * ts, src, (hi - lo) * ts, aligned);
-    }
-    if (COLL == SYM_AG) {  // my own block (skipped in place)
-      uint64_t lo, hi;
-      partOf(a.chunk, lo, hi);
-      char* dst = a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
-      const char* src = a.send[me] + lo * ts;
-      if (dst != src) copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
+      const uint64_t off = ((uint64_t)q * a.chunk + lo) * ts;
+      copyRange<T, false>(a.recv[me] + off, a.recv[q] + off, (hi - lo) * ts, aligned);
     }
     __syncthreads();
   }
@@ -1057,7 +1286,10 @@ inline void launchLLK(const LaunchPlan& p) {
   a.redArgPtr = p.ll.redArgPtr;
   a.nOps = p.ll.nOps;
   for (int k = 0; k < p.ll.nOps && k < K; k++) a.ops[k] = p.ll.ops[k];
-  hipLaunchKernelGGL((llKernel<T, OP, K>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
+  if (p.ll.ops[0].proto == LLP_LL64)
+    hipLaunchKernelGGL((llKernel<T, OP, K, LLP_LL64>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
+  else
+    hipLaunchKernelGGL((llKernel<T, OP, K, LLP_LL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
 }
 template <typename T, int OP>
 inline void launchLL(const LaunchPlan& p) {

@@ -25,8 +25,10 @@ static size_t flagWordBytes(const ncclComm* c) {
   return (size_t)c->maxChannels * FLG_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
 }
 static size_t llOffset(const ncclComm* c) { return (flagWordBytes(c) + 4095) / 4096 * 4096; }
+// LL area, then the LL64 area of the same geometry (device_abi.h)
+static size_t ll64Offset(const ncclComm* c) { return llOffset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes; }
 static size_t flagsBytes(const ncclComm* c) {
-  return llOffset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes;
+  return ll64Offset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes;
 }
 
 ncclResult_t transportSetup(ncclComm* comm) {
@@ -181,8 +183,9 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
   d.counters = comm->counters;
   // the LL channels of a launch must be co-resident like any channel: never more than chanCap (the line
   // area was sized for the full count; host planning and the kernel's batch modulus use this value)
-  if (comm->llChannels > comm->chanCap && comm->chanCap > 0) comm->llChannels = comm->chanCap;
   d.llOffset = llOffset(comm);
+  d.ll64Offset = ll64Offset(comm);  // both before the cap below: the areas were sized for the full count
+  if (comm->llChannels > comm->chanCap && comm->chanCap > 0) comm->llChannels = comm->chanCap;
   d.llBytes = comm->llBytes;
   d.llChannels = comm->llChannels;
   void* dAbort = nullptr;

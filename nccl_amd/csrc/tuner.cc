@@ -130,8 +130,9 @@ void tunerUnload(ncclComm* comm) {
 }
 
 // Ask the plugin. `algo` (in: the engine's default choice, out: the plugin's) and `nch` (out: channel
-// override or 0). llOk: the LL kernel can take this collective.
-void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, bool llOk, int* algo, int* nch) {
+// override or 0). llMask: 1 = the LL kernel can take this collective, 2 = the LL64 (LL128-class) one can.
+void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int* algo, int* nch) {
+  const bool llOk = (llMask & 1) != 0, ll128Ok = (llMask & 2) != 0;
   *nch = 0;
   if (!comm->tunerLoaded) return;
   const int n = comm->nRanks;
@@ -146,6 +147,8 @@ void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, bool
       table[NCCL_ALGO_RING][NCCL_PROTO_LL] = (float)(4.0 + 2.0 * (n - 1) * bytes * usPerByte);
       table[NCCL_ALGO_TREE][NCCL_PROTO_LL] = table[NCCL_ALGO_RING][NCCL_PROTO_LL];
     }
+    if (ll128Ok)  // 64 link bytes per 56 payload bytes, to every peer
+      table[NCCL_ALGO_RING][NCCL_PROTO_LL128] = (float)(4.5 + (64.0 / 56.0) * (n - 1) * bytes * usPerByte);
     table[NCCL_ALGO_TREE][NCCL_PROTO_SIMPLE] = (float)(7.0 + (n - 1) * bytes * usPerByte);
     table[NCCL_ALGO_RING][NCCL_PROTO_SIMPLE] = (float)(10.0 + 2.0 * (n - 1) / n * bytes * usPerByte);
   } else {
@@ -154,6 +157,9 @@ void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, bool
     if (llOk)  // Reduce's LL lines go to every peer, like AllReduce's
       table[NCCL_ALGO_RING][NCCL_PROTO_LL] =
           (float)(4.0 + (func == FUNC_REDUCE ? 2.0 * (n - 1) : 2.0 * (n - 1.0) / n) * bytes * usPerByte);
+    if (ll128Ok)
+      table[NCCL_ALGO_RING][NCCL_PROTO_LL128] =
+          (float)(4.5 + (64.0 / 56.0) * (func == FUNC_REDUCE ? (n - 1.0) : (n - 1.0) / n) * bytes * usPerByte);
   }
   float before[NCCL_NUM_ALGORITHMS][NCCL_NUM_PROTOCOLS];
   memcpy(before, table, sizeof(table));
@@ -173,6 +179,7 @@ void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, bool
     }
   if (bestA < 0) return;
   if (bestP == NCCL_PROTO_LL) *algo = TUNE_LL;
+  else if (bestP == NCCL_PROTO_LL128) *algo = TUNE_LL128;
   else if (bestA == NCCL_ALGO_TREE) *algo = TUNE_ONESHOT;
   else *algo = TUNE_DIRECT;
   TRACE("tuner: func %d bytes %zu -> algo %d proto %d (%d) nch %d", (int)func, bytes, bestA, bestP, *algo, *nch);

@@ -161,3 +161,45 @@ def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=
                         f"{bad.size} mismatches, first at {bad[:5].tolist()} got {got[bad[:3]].tolist()} "
                         f"want {want[bad[:3]].tolist()}")
     return errs
+
+
+def run_group(comms_and_streams, ops, seed):
+    """Several collectives [(coll, dtype, op, count), ...] issued inside ONE group (so consecutive ops that plan
+    onto the same kernel are batched into one launch), out of place, checked bit-exactly; returns errors."""
+    import torch
+    import nccl_amd
+    n = comms_and_streams[0][0].nranks
+    plan = []
+    for k, (coll, dtype, op, count) in enumerate(ops):
+        inputs = make_inputs(n, dtype, count, seed * 100 + k)
+        exp = expected(coll, inputs, dtype, op, 0)
+        npdt = oracle.NP_STORAGE[dtype]
+        bufs = {}
+        for comm, _ in comms_and_streams:
+            dev = torch.device("cuda", comm.device)
+            b1, sv = to_device(inputs[comm.rank], dev, 0)
+            b2, rv = to_device(np.zeros(out_count(coll, n, count), dtype=npdt), dev, 0)
+            bufs[comm.rank] = (b1, sv, b2, rv)
+        plan.append((coll, dtype, op, count, exp, npdt, bufs))
+    torch.cuda.synchronize()
+    with nccl_amd.group():
+        for coll, dtype, op, count, _, _, bufs in plan:
+            for comm, stream in comms_and_streams:
+                _, sv, _, rv = bufs[comm.rank]
+                launch(comm, coll, sv, rv, count, dtype, op, 0, stream.cuda_stream)
+    errs = []
+    for comm, stream in comms_and_streams:
+        stream.synchronize()
+        if comm.async_error():
+            errs.append(f"rank {comm.rank}: async error {comm.async_error()}")
+    for k, (coll, dtype, op, count, exp, npdt, bufs) in enumerate(plan):
+        for comm, _ in comms_and_streams:
+            if coll == "reduce" and comm.rank != 0:
+                continue
+            got = from_device(bufs[comm.rank][3], npdt)
+            want = exp[0] if coll == "reduce" else exp[comm.rank]
+            if not same_bits(got, want, dtype):
+                bad = np.nonzero(got != want)[0]
+                errs.append(f"group op {k} rank {comm.rank} {coll} dt={dtype} op={op} count={count}: "
+                            f"{bad.size} mismatches, first at {bad[:5].tolist()}")
+    return errs

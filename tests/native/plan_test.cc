@@ -60,7 +60,7 @@ ncclWindow_vidmem* findSymWindow(ncclComm*, const void*, size_t) { return nullpt
 bool groupActive() { return false; }
 ncclResult_t groupDeferColl(const CollInfo&) { return ncclSuccess; }
 void groupRecordError(ncclResult_t) {}
-void tunerPick(ncclComm*, CollFunc, size_t, int, bool, int*, int* nch) { *nch = 0; }
+void tunerPick(ncclComm*, CollFunc, size_t, int, int, int*, int* nch) { *nch = 0; }
 ncclResult_t commCheck(const ncclComm*, const char*, const char*) { return ncclSuccess; }
 }  // namespace ncclamd
 
@@ -154,7 +154,8 @@ int main(int argc, char** argv) {
     return 0;
   }
   if (p.algo == ALGO_LL)
-    printf("algo=ll nch=%d part=%lu slice=0 steps=1 chunk=%lu\n", p.nChannels, (unsigned long)p.ll.ops[0].part,
+    printf("algo=%s nch=%d part=%lu slice=0 steps=1 chunk=%lu\n", p.ll.ops[0].proto == LLP_LL64 ? "ll128" : "ll",
+           p.nChannels, (unsigned long)p.ll.ops[0].part,
            (unsigned long)p.ll.ops[0].chunk);
   else
     printf("algo=%s nch=%d part=%lu slice=%lu steps=%d chunk=%lu\n", names[p.algo], p.nChannels,

@@ -99,7 +99,9 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}),
             (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"}),
             # cross-process memory: every dma-buf import refused -> the hipIpc handle fallback (ipc.cc); legacy only
-            (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}), (2, {"NCCL_AMD_IPC": "legacy"})]
+            (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}), (2, {"NCCL_AMD_IPC": "legacy"}),
+            # the LL128-class protocol (LL64 lines): forced for everything it fits, and in its size-table range
+            (3, {"NCCL_PROTO": "LL128"}), (4, {"NCCL_AMD_LL128": "1"})]
 
 
 @pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
@@ -245,6 +247,71 @@ def test_ll_reducescatter_allgather(built, nranks):
                     i += 1
         if errs:
             break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_ll128_every_collective(built, nranks, monkeypatch):
+    """The LL128-class protocol (kernels.h ll64ChannelOp, NCCL_PROTO=LL128): 64-byte lines of 56 payload bytes.
+    Every collective, type and op, sizes that end mid-line, mid-payload and on channel-part boundaries,
+    in place, unaligned bases; bit-exact vs the oracle (same fold order as every other path)."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    monkeypatch.setenv("NCCL_PROTO", "LL128")
+    monkeypatch.setenv("NCCL_AMD_LL128_CHANNEL_BYTES", "4096")  # many channels even at small sizes
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0] * nranks)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    cs = list(zip(comms, streams))
+    errs = []
+    i = 0
+    for dtype in (7, 9, 6, 2, 3, 4, 0, 1, 5, 8, 10, 11):
+        es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+        for nbytes in (8, 56, 64, 1000, 4096 * 3 + 56 * 5, 100_000):
+            count = max(1, nbytes // es)
+            ops = (0, 1, 2, 3, 4) if nbytes in (1000, 100_000) else (0,)
+            for op in ops:
+                errs += G.run_case(cs, "allreduce", dtype, op, count + (i % 3), 0, seed=1200 + i)
+                errs += G.run_case(cs, "reduce", dtype, op, count, 0, seed=1300 + i, root=i % nranks)
+                blk = max(1, (nbytes // 8) * 8 // es)  # blocked collectives: 8-byte multiple rank blocks
+                errs += G.run_case(cs, "reducescatter", dtype, op, blk * nranks, 0, seed=1400 + i)
+                i += 1
+            errs += G.run_case(cs, "allgather", dtype, 0, max(1, (nbytes // 8) * 8 // es), 0, seed=1500 + i)
+            errs += G.run_case(cs, "allreduce", dtype, 0, count, 0, seed=1600 + i, inplace=True)
+            errs += G.run_case(cs, "allreduce", dtype, 0, count, 1, seed=1700 + i)  # misaligned bases
+        if errs:
+            break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
+def test_ll_and_ll128_share_channels(built, monkeypatch):
+    """LL and LL64 ops interleaved on the same channels (shared epochs, separate line areas): sizes alternating
+    between the LL range and the LL128 range, one op at a time and in group batches, across the 32-bit epoch
+    wrap; every result bit-exact."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    monkeypatch.setenv("NCCL_AMD_LL128", "1")
+    monkeypatch.setenv("NCCL_AMD_LL_EPOCH_BASE", str(2**32 - 7))
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0, 0])
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    cs = list(zip(comms, streams))
+    errs = []
+    for i in range(16):
+        count = 1000 + 13 * i if i % 2 else 60_000 + 101 * i  # 4 KB (LL) / 240 KB (LL128 at n=3)
+        errs += G.run_case(cs, "allreduce", 7, 0, count, 0, seed=2000 + i)
+    # group batches: several LL128 ops in one launch, then an LL batch
+    for k in range(3):
+        errs += G.run_group(cs, [("allreduce", 9, 0, 50_000 + 7 * j) for j in range(5)], seed=2100 + k)
+        errs += G.run_group(cs, [("allreduce", 7, 2, 300 + j) for j in range(6)], seed=2200 + k)
     for c in comms:
         c.destroy()
     assert not errs, "\n".join(errs[:20])

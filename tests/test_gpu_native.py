@@ -43,3 +43,22 @@ def test_xgmi_probe_loopback(built):
     assert out.returncode == 0, out.stdout + out.stderr
     rep = json.loads(out.stdout.strip().splitlines()[-1])
     assert rep["wrong_bytes"] == 0 and rep["write_fanout_GBps"] > 0
+
+
+def test_store_atomicity_probe_one_gpu(built):
+    """the LL protocol relies on 8-byte single-copy atomicity of the halves of a 16-byte
+    write-through store; LL128 would rely on whole 128-byte lines. The probe races a writer (system-scope
+    write-through dwordx4 stores into uncached memory, the LL kernels' store) against system-scope 16-byte
+    readers on other XCDs of the same GPU. torn8 must be 0; the wider classes are reported (bench.py's
+    suite runs the same probe across an xGMI link on multi-GPU nodes)."""
+    import json
+    exe = os.path.join(ROOT, "tests", "native", "store_atomicity_probe")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "atomicity-probe"], cwd=ROOT)
+    out = subprocess.run([exe, "0", "0", "20000", "64", "3000"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stdout + out.stderr
+    rep = json.loads(out.stdout.strip().splitlines()[-1])
+    print("store atomicity (one GPU):", rep)
+    assert rep["reader_waves"] == 64 and rep["line_observations"] > 0
+    assert rep["changed"] > 0, "the readers never raced the writer"
+    assert rep["torn8"] == 0, rep

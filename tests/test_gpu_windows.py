@@ -147,6 +147,61 @@ def test_windows_single_process(built, nranks, oneshot, monkeypatch):
     assert not errs, "\n".join(errs[:20])
 
 
+def test_windows_allgather_mixed_in_place(built):
+    """the symmetric AllGather pulls peers' blocks from their OUTPUTS (each rank places its own block
+    before entry), so ranks may mix in-place and out-of-place calls and a sendbuff need not lie in a window:
+    only the outputs must sit at the same window offset on every rank. (AllReduce / ReduceScatter read
+    peers' INPUTS at the caller's own offsets, so they keep NCCL's rule: both buffers at the same offsets.)"""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    n = 3
+    comms = nccl_amd.Communicator.init_all([0] * n)
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    bufs, wins = _windows(comms)
+    cs = list(zip(comms, streams))
+    errs = []
+    cases = [(7, 30_001, [True, False, True], False), (9, 64_000, [False, True, False], False),
+             (7, 40_003, [False, False, True], True), (2, 70_000, [True, True, False], True)]
+    for i, (dtype, count, mix, outside) in enumerate(cases):
+        es = 2 if dtype == 9 else 4
+        inputs = G.make_inputs(n, dtype, count, 40 + i)
+        want = G.expected("allgather", inputs, dtype, 0, 0)
+        sends, ptrs = [], []
+        for (c, s), b in zip(cs, bufs):
+            r = c.rank
+            raw = b.view(torch.uint8)
+            raw[HALF:HALF + n * count * es].zero_()
+            data = torch.from_numpy(np.ascontiguousarray(inputs[r]).view(np.uint8).copy()).cuda()
+            if mix[r]:    # in place: my input is block r of my output
+                raw[HALF + r * count * es:HALF + (r + 1) * count * es].copy_(data)
+                ptrs.append(b.data_ptr() + HALF + r * count * es)
+            elif outside:  # out of place, sendbuff outside any window
+                sends.append(data)
+                ptrs.append(data.data_ptr())
+            else:          # out of place, sendbuff at offset 0 of the window
+                raw[:data.numel()].copy_(data)
+                ptrs.append(b.data_ptr())
+        torch.cuda.synchronize()
+        with nccl_amd.group():
+            for (c, s), b, sp in zip(cs, bufs, ptrs):
+                c.all_gather_raw(sp, b.data_ptr() + HALF, count, dtype, s.cuda_stream)
+        for (c, s), b in zip(cs, bufs):
+            s.synchronize()
+            got = b.view(torch.uint8)[HALF:HALF + n * count * es].cpu().numpy().view(want[c.rank].dtype)
+            if not G.same_bits(got, want[c.rank], dtype):
+                bad = np.nonzero(got != want[c.rank])[0]
+                errs.append(f"case {i} rank {c.rank} mix {mix} outside {outside}: {bad.size} mismatches, "
+                            f"first {bad[:5].tolist()}")
+    for c, w in zip(comms, wins):
+        c.deregister_window(w)
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
 def test_window_without_symmetric_flag_uses_staged_path(built):
     import torch
     import nccl_amd

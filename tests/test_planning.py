@@ -209,3 +209,31 @@ def test_group_batch_limits_and_opt_out(exe):
     assert [l["ops"] for l in batch(exe, 2, *(["ar:7:100"] * 3), NCCL_AMD_NO_AGGREGATION=1)] == [1, 1, 1]
     # forced ring / chain plans are not batched (their own kernel)
     assert [l["ops"] for l in batch(exe, 4, *(["ar:7:1000000"] * 3), NCCL_ALGO="RING")] == [1, 1, 1]
+
+
+def test_ll128_class_protocol(exe):
+    # LL128 class (LL64 lines of 56 payload bytes): off by default (the reference too, where 128-byte store
+    # atomicity is unproven); NCCL_PROTO=LL128 forces it for everything that fits 32 channels x 512 lines,
+    # NCCL_AMD_LL128=1 gives it the size-table range between LL and one-shot (default up to 1 MiB / n)
+    assert plan(exe, 2, "ar", 7, (512 << 10) // 4)["algo"] == "oneshot"
+    p = plan(exe, 2, "ar", 7, (512 << 10) // 4, NCCL_PROTO="LL128")
+    assert p["algo"] == "ll128" and p["part"] * 64 <= 32 << 10 and p["part"] * p["nch"] * 56 >= 512 << 10
+    cap_lines = 32 * (32 << 10) // 64
+    assert plan(exe, 2, "ar", 9, cap_lines * 56 // 2, NCCL_PROTO="LL128")["algo"] == "ll128"   # exactly full
+    assert plan(exe, 2, "ar", 9, cap_lines * 56 // 2 + 28, NCCL_PROTO="LL128")["algo"] != "ll128"
+    for n in (2, 4, 8):
+        lim = max(64 << 10, (1 << 20) // n)
+        assert plan(exe, n, "ar", 7, (16 << 10) // 4, NCCL_AMD_LL128=1)["algo"] == "ll"      # LL range first
+        assert plan(exe, n, "ar", 7, lim // 4, NCCL_AMD_LL128=1)["algo"] == "ll128"
+        assert plan(exe, n, "ar", 7, lim // 4 + 4, NCCL_AMD_LL128=1)["algo"] in ("oneshot", "direct")
+    assert plan(exe, 2, "ar", 7, 100_000, NCCL_AMD_LL128=1, NCCL_PROTO="^LL128")["algo"] == "oneshot"
+    assert plan(exe, 2, "ar", 7, 100, NCCL_PROTO="LL,LL128")["algo"] == "ll"    # LL range, Simple off
+    assert plan(exe, 2, "ar", 7, 100_000, NCCL_PROTO="LL,LL128")["algo"] == "ll128"
+    for func in ("rs", "ag", "reduce"):
+        assert plan(exe, 4, func, 7, 20_000, NCCL_PROTO="LL128")["algo"] == "ll128"
+    assert plan(exe, 4, "rs", 7, 20_001, NCCL_PROTO="LL128")["algo"] == "direct"  # 8-byte rank blocks only
+    # every channel carries at least one line
+    for count in (1, 14, 15, 1000, 123_457):
+        p = plan(exe, 3, "ar", 7, count, NCCL_PROTO="LL128", NCCL_AMD_LL128_CHANNEL_BYTES=56)
+        lines = -(-count * 4 // 56)
+        assert (p["nch"] - 1) * p["part"] < lines <= p["nch"] * p["part"]
