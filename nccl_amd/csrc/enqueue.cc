@@ -127,7 +127,9 @@ void loadTuning(CommTuning* t) {
   t->ll128Bytes = paramInt("NCCL_AMD_LL128_BYTES", 0);  // 0: size table default (1 MiB / nRanks)
   t->ll128ChannelBytes = paramInt("NCCL_AMD_LL128_CHANNEL_BYTES", 4096);
   if (t->ll128ChannelBytes < kLL64Payload) t->ll128ChannelBytes = kLL64Payload;
-  t->minChannelBytes = paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 64 << 10);
+  // 16 KiB: mid-size direct AllReduces spread over more channels (one-GPU rehearsal, n = 4, 4 MiB: 51 -> 30 us,
+  // profiles/r02_channel_granularity_onegpu.txt); 256 MiB plans are capped at the channel limit either way
+  t->minChannelBytes = paramInt("NCCL_AMD_MIN_CHANNEL_BYTES", 16 << 10);
   t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
   t->copyVariant = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
   t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);

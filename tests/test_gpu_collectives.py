@@ -104,7 +104,12 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (3, {"NCCL_PROTO": "LL128"}), (4, {"NCCL_AMD_LL128": "1"})]
 
 
-@pytest.mark.parametrize("nranks,env", MP_CASES, ids=[f"n{n}-{'-'.join(e.values()) or 'default'}" for n, e in MP_CASES])
+def _mp_id(n, env):
+    return f"n{n}-" + ("-".join(f"{k.replace('NCCL_AMD_', '').replace('NCCL_', '')}={v}" for k, v in env.items())
+                       or "default")
+
+
+@pytest.mark.parametrize("nranks,env", MP_CASES, ids=[_mp_id(n, e) for n, e in MP_CASES])
 def test_multi_process(built, nranks, env):
     _torch()
     import nccl_amd
