@@ -17,13 +17,14 @@ import nccl_amd  # noqa: E402
 from tests import gpu_cases as G  # noqa: E402
 
 KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_AG_PULL",
-         "NCCL_AMD_RS_PULL", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_LL_CHANNEL_BYTES")
+         "NCCL_AMD_RS_PULL", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_LL_CHANNEL_BYTES", "NCCL_AMD_LL128",
+         "NCCL_AMD_LL128_CHANNEL_BYTES")
 
 
 def settings(rng):
     env = {}
     if rng.random() < 0.3:
-        env["NCCL_PROTO"] = rng.choice(["LL", "^LL", "Simple", "LL,Simple"])
+        env["NCCL_PROTO"] = rng.choice(["LL", "^LL", "Simple", "LL,Simple", "LL128", "LL,LL128", "LL128,Simple"])
     if rng.random() < 0.3:
         env["NCCL_ALGO"] = rng.choice(["ONESHOT", "DIRECT", "RING"])
     if rng.random() < 0.4:
@@ -40,6 +41,10 @@ def settings(rng):
         env["NCCL_AMD_MIN_CHANNEL_BYTES"] = str(rng.choice([4096, 16384]))
     if rng.random() < 0.2:
         env["NCCL_AMD_LL_CHANNEL_BYTES"] = str(rng.choice([512, 1024, 8192]))
+    if rng.random() < 0.3:  # the LL128 class (64-byte lines) in its size-table range
+        env["NCCL_AMD_LL128"] = "1"
+    if rng.random() < 0.2:
+        env["NCCL_AMD_LL128_CHANNEL_BYTES"] = str(rng.choice([56, 512, 16384]))
     return env
 
 
