@@ -59,6 +59,26 @@ __device__ __forceinline__ void storeRemote(void* p, u32x4 v) {
 }
 __device__ __forceinline__ void drainStores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// Bulk remote stores (staging slots, AG pushes) as compiler-visible buffer stores with the same cache policy
+// (sc0 sc1: system-scope write-through). The compiler cannot see an inline-asm store, and on gfx9 stores
+// count in vmcnt like loads: a copy loop of asm stores therefore ends every batch with vmcnt(0), i.e. waits
+// for its own stores' completion before the next loads go out. With intrinsic stores the waits cover only
+// the loads. The destination base is wave-uniform (readfirstlane makes that explicit); offsets are 32-bit
+// (a slot or slice is far below 4 GiB).
+#ifndef NCCL_AMD_BUFFER_STORES
+#define NCCL_AMD_BUFFER_STORES 1
+#endif
+constexpr int kSysWriteThrough = 1 | 16;  // buffer cache policy bits: sc0 (bit 0) | sc1 (bit 4)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t remoteRsrc(const void* base) {
+  const uint64_t b = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, -1, 0x00020000);
+}
+__device__ __forceinline__ void storeRemoteAt(__amdgpu_buffer_rsrc_t r, uint32_t byteOff, u32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, byteOff, 0, kSysWriteThrough);
+}
+
 // One element stored system-scope write-through (tails and unaligned ranges of published data).
 template <typename T>
 __device__ __forceinline__ void storeRemoteElt(T* p, T v) {
@@ -180,19 +200,23 @@ __device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t n
     u32x4* d = (u32x4*)dst;
     constexpr int U = kCopyUnroll;
     uint64_t i = threadIdx.x;
+    __amdgpu_buffer_rsrc_t rd;
+    if (REMOTE && NCCL_AMD_BUFFER_STORES) rd = remoteRsrc(dst);
     for (; i + (U - 1) * kThreads < npk; i += U * kThreads) {
       u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s + i + u * kThreads);
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        if (REMOTE) storeRemote(d + i + u * kThreads, v[u]);
+        if (REMOTE && NCCL_AMD_BUFFER_STORES) storeRemoteAt(rd, (uint32_t)((i + u * kThreads) * 16), v[u]);
+        else if (REMOTE) storeRemote(d + i + u * kThreads, v[u]);
         else __builtin_nontemporal_store(v[u], d + i + u * kThreads);
       }
     }
     for (; i < npk; i += kThreads) {
       u32x4 v = __builtin_nontemporal_load(s + i);
-      if (REMOTE) storeRemote(d + i, v);
+      if (REMOTE && NCCL_AMD_BUFFER_STORES) storeRemoteAt(rd, (uint32_t)(i * 16), v);
+      else if (REMOTE) storeRemote(d + i, v);
       else __builtin_nontemporal_store(v, d + i);
     }
     uint64_t done = npk << 4;
@@ -278,7 +302,10 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
 #pragma unroll
         for (int e = 0; e < EPP; e++) acc[u].e[e] = fn.post(acc[u].e[e]);
         if (dstLocal) __builtin_nontemporal_store(acc[u].v, (u32x4*)dstLocal + i);
-        for (int p = 0; p < nPush; p++) storeRemote((u32x4*)dstPush[p] + i, acc[u].v);
+        for (int p = 0; p < nPush; p++) {
+          if (NCCL_AMD_BUFFER_STORES) storeRemoteAt(remoteRsrc(dstPush[p]), (uint32_t)(i * 16), acc[u].v);
+          else storeRemote((u32x4*)dstPush[p] + i, acc[u].v);
+        }
       }
     }
     const uint64_t t = npk * EPP + threadIdx.x;  // < 16-byte tail of the range

@@ -99,7 +99,10 @@ __device__ __forceinline__ void pipeMove(const Red<T, OP>& fn, const char* acc, 
 #pragma unroll
         for (int e = 0; e < EPP; e++) o.e[e] = elem(av[u].e[e], xv[u].e[e]);
       if (dstLocal) __builtin_nontemporal_store(o.v, (u32x4*)dstLocal + i);
-      if (dstPush) storeRemote((u32x4*)dstPush + i, o.v);
+      if (dstPush) {
+        if (NCCL_AMD_BUFFER_STORES) storeRemoteAt(remoteRsrc(dstPush), (uint32_t)(i * 16), o.v);
+        else storeRemote((u32x4*)dstPush + i, o.v);
+      }
     }
   }
   for (uint64_t t = npk * EPP + threadIdx.x; t < nelem; t += kThreads) {  // tail / unaligned
