@@ -176,6 +176,13 @@ ncclResult_t pncclCommInitRankConfig(ncclComm_t* comm, int nranks, ncclUniqueId 
 ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank);
 ncclResult_t pncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank);
 
+/* nccl.h.in:263 — several ids (same number and order on every rank); this single-node star rendezvouses at
+ * commIds[0] and tells the other ids' roots to exit. */
+ncclResult_t ncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
+                                      ncclUniqueId* commIds, ncclConfig_t* config);
+ncclResult_t pncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
+                                       ncclUniqueId* commIds, ncclConfig_t* config);
+
 /* nccl.h.in:195 — single-process clique, one comm per device in devlist (NULL = 0..ndev-1). */
 ncclResult_t ncclCommInitAll(ncclComm_t* comm, int ndev, const int* devlist);
 ncclResult_t pncclCommInitAll(ncclComm_t* comm, int ndev, const int* devlist);
@@ -203,6 +210,16 @@ ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device);
 ncclResult_t pncclCommCuDevice(const ncclComm_t comm, int* device);
 ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank);
 ncclResult_t pncclCommUserRank(const ncclComm_t comm, int* rank);
+
+/* nccl.h.in:333-348 — device memory the communicator holds (all of it persistent: nothing is suspendable). */
+typedef enum {
+  ncclStatGpuMemSuspend = 0,
+  ncclStatGpuMemSuspended = 1,
+  ncclStatGpuMemPersist = 2,
+  ncclStatGpuMemTotal = 3
+} ncclCommMemStat_t;
+ncclResult_t ncclCommMemStats(ncclComm_t comm, ncclCommMemStat_t stat, uint64_t* value);
+ncclResult_t pncclCommMemStats(ncclComm_t comm, ncclCommMemStat_t stat, uint64_t* value);
 
 /* ---- Buffer registration (nccl.h.in:301-307, 350-360) ---- */
 /* nccl.h.in:302 — local (non-collective) registration hint; see DESIGN.md §10. */
@@ -262,6 +279,19 @@ ncclResult_t ncclGroupStart(void);
 ncclResult_t pncclGroupStart(void);
 ncclResult_t ncclGroupEnd(void);
 ncclResult_t pncclGroupEnd(void);
+
+/* nccl.h.in:136-152, 741 — plan the group's collectives without launching them and return the cost model's
+ * estimate (microseconds, like the reference's tuning table) in simInfo->estimatedTime. */
+typedef struct ncclSimInfo_v22200 {
+  size_t size;
+  unsigned int magic;
+  unsigned int version;
+  float estimatedTime;
+} ncclSimInfo_t;
+#define NCCL_SIM_INFO_INITIALIZER \
+  { sizeof(ncclSimInfo_t), 0x74685283, NCCL_VERSION_CODE, NCCL_UNDEF_FLOAT }
+ncclResult_t ncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
+ncclResult_t pncclGroupSimulateEnd(ncclSimInfo_t* simInfo);
 
 #ifdef __cplusplus
 }

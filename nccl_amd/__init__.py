@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import dataclasses
 import enum
 import os
 from typing import Optional, Sequence
@@ -74,6 +75,33 @@ class UniqueId(ctypes.Structure):
     _fields_ = [("internal", ctypes.c_char * 128)]
 
 
+class SimInfo(ctypes.Structure):  # ncclSimInfo_t, nccl.h.in:136-152
+    _fields_ = [("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
+                ("estimatedTime", ctypes.c_float)]
+
+    @classmethod
+    def default(cls) -> "SimInfo":
+        s = cls()
+        s.size = ctypes.sizeof(cls)
+        s.magic = 0x74685283
+        s.version = get_version_code_static()
+        s.estimatedTime = -1.0
+        return s
+
+
+@dataclasses.dataclass(frozen=True)
+class GroupSimInfo:
+    """nccl4py GroupSimInfo (bindings/nccl4py/nccl/core/group.py:28-36)."""
+    estimated_time: float  # seconds
+
+
+class MemStat(enum.IntEnum):  # ncclCommMemStat_t, nccl.h.in:333-338
+    GPU_MEM_SUSPEND = 0
+    GPU_MEM_SUSPENDED = 1
+    GPU_MEM_PERSIST = 2
+    GPU_MEM_TOTAL = 3
+
+
 class Config(ctypes.Structure):  # ncclConfig_t, nccl.h.in:84-108
     _fields_ = [
         ("size", ctypes.c_size_t), ("magic", ctypes.c_uint), ("version", ctypes.c_uint),
@@ -112,7 +140,7 @@ EXPORTED = [
     "ncclCommUserRank", "ncclRedOpCreatePreMulSum", "ncclRedOpDestroy", "ncclReduce", "ncclAllReduce",
     "ncclReduceScatter", "ncclAllGather", "ncclGroupStart", "ncclGroupEnd",
     "ncclCommRegister", "ncclCommDeregister", "ncclCommWindowRegister", "ncclCommWindowDeregister",
-    "ncclWinGetUserPtr",
+    "ncclWinGetUserPtr", "ncclCommInitRankScalable", "ncclCommMemStats", "ncclGroupSimulateEnd",
 ]
 
 
@@ -171,6 +199,9 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
         "ncclCommWindowDeregister": (R, [P, P]),
         "ncclWinGetUserPtr": (R, [P, P, ctypes.POINTER(P)]),
         "ncclMemFree": (R, [P]),
+        "ncclCommInitRankScalable": (R, [ctypes.POINTER(P), I, I, I, ctypes.POINTER(UniqueId), ctypes.POINTER(Config)]),
+        "ncclCommMemStats": (R, [P, I, ctypes.POINTER(U64)]),
+        "ncclGroupSimulateEnd": (R, [ctypes.POINTER(SimInfo)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -207,8 +238,15 @@ def group_start() -> None:
     _check(load().ncclGroupStart(), "ncclGroupStart")
 
 
-def group_end() -> None:
-    _check(load().ncclGroupEnd(), "ncclGroupEnd")
+def group_end(*, simulate: bool = False) -> Optional[GroupSimInfo]:
+    """nccl4py group_end (group.py:54-76): simulate=True plans the group's collectives without launching
+    them (ncclGroupSimulateEnd) and returns the cost model's estimate, in seconds."""
+    if not simulate:
+        _check(load().ncclGroupEnd(), "ncclGroupEnd")
+        return None
+    si = SimInfo.default()
+    _check(load().ncclGroupSimulateEnd(ctypes.byref(si)), "ncclGroupSimulateEnd")
+    return GroupSimInfo(estimated_time=si.estimatedTime * 1e-6)
 
 
 @contextlib.contextmanager
@@ -299,9 +337,19 @@ class Communicator:
 
     # ---- construction (nccl4py Communicator.init / init_all) ----
     @classmethod
-    def init(cls, nranks: int, rank: int, unique_id: bytes, config: Optional[Config] = None) -> "Communicator":
+    def init(cls, nranks: int, rank: int, unique_id, config: Optional[Config] = None) -> "Communicator":
+        """unique_id: one id (bytes), or a sequence of ids for ncclCommInitRankScalable (nccl4py
+        communicator.py:333-334)."""
         lib = load()
         c = ctypes.c_void_p()
+        if not isinstance(unique_id, (bytes, bytearray)):
+            ids = list(unique_id)
+            arr = (UniqueId * len(ids))(*[_uid(b) for b in ids])
+            rc = lib.ncclCommInitRankScalable(ctypes.byref(c), nranks, rank, len(ids), arr,
+                                              ctypes.byref(config) if config is not None else None)
+            if not (rc == Result.InProgress and config is not None and config.blocking == 0):
+                _check(rc, "ncclCommInitRankScalable")
+            return cls(c.value)
         if config is None:
             _check(lib.ncclCommInitRank(ctypes.byref(c), nranks, _uid(unique_id), rank), "ncclCommInitRank")
         else:
@@ -360,6 +408,12 @@ class Communicator:
             _check(load().ncclCommCuDevice(self._comm, ctypes.byref(v)), "ncclCommCuDevice")
             self._device = v.value
         return self._device
+
+    def mem_stats(self, stat: "MemStat" = MemStat.GPU_MEM_TOTAL) -> int:
+        """ncclCommMemStats: device bytes this communicator holds (everything is persistent here)."""
+        v = ctypes.c_uint64()
+        _check(load().ncclCommMemStats(self._comm, int(stat), ctypes.byref(v)), "ncclCommMemStats")
+        return v.value
 
     def async_error(self) -> int:
         v = ctypes.c_int()

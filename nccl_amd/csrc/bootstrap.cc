@@ -79,6 +79,9 @@ static int recvAll(int fd, void* p, size_t n) {
 
 static int64_t bootstrapTimeoutMs() { return paramInt("NCCL_AMD_BOOTSTRAP_TIMEOUT_MS", 600000); }
 
+// Hello.rank of a release message (ncclCommInitRankScalable): the root is not needed, exit.
+static constexpr int32_t kReleaseRank = -1;
+
 // Root service: accept nranks connections, then serve all-gather rounds until every rank hangs up.
 static void rootThread(int listenFd, uint64_t commId) {
   std::vector<int> fds;
@@ -93,7 +96,12 @@ static void rootThread(int listenFd, uint64_t commId) {
     int fd = accept(listenFd, nullptr, nullptr);
     if (fd < 0) continue;
     Hello h;
-    if (recvAll(fd, &h, sizeof(h)) != 1 || h.magic != kIdMagic || h.commId != commId || h.nranks <= 0 ||
+    const bool got = recvAll(fd, &h, sizeof(h)) == 1;
+    if (got && h.magic == kIdMagic && h.commId == commId && h.rank == kReleaseRank && nranks < 0) {
+      close(fd);  // an unused id of ncclCommInitRankScalable: no rank will connect here
+      goto done;
+    }
+    if (!got || h.magic != kIdMagic || h.commId != commId || h.nranks <= 0 ||
         h.rank < 0 || h.rank >= h.nranks || (nranks >= 0 && h.nranks != nranks)) {
       WARN("bootstrap root: rejected connection (bad hello)");
       close(fd);
@@ -204,6 +212,61 @@ ncclResult_t bootstrapInit(const ncclUniqueId* id, int rank, int nranks, Bootstr
   b->rank = rank;
   b->nranks = nranks;
   *out = b;
+  return ncclSuccess;
+}
+
+// ncclCommInitRankScalable hands every rank nId ids (reference bootstrap.cc:59-89 spreads the ranks over
+// nId roots). This engine's star needs one root, so every rank rendezvouses at id 0 and the first rank of
+// each other id's rank group (the reference's block partition, rootIdFromRank) tells that id's root to
+// exit instead of waiting for ranks that never come. Bounded like every bootstrap connect.
+ncclResult_t bootstrapRelease(const ncclUniqueId* id) {
+  IdPayload p;
+  memcpy(&p, id->internal, sizeof(p));
+  if (p.magic != kIdMagic) {
+    WARN("ncclCommInitRankScalable: invalid ncclUniqueId (was it produced by ncclGetUniqueId?)");
+    return ncclInvalidArgument;
+  }
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(bootstrapTimeoutMs());
+  while (true) {
+    int fd = socket(AF_INET, SOCK_STREAM, 0);
+    SYSCHECK(fd >= 0, "socket");
+    if (connect(fd, (struct sockaddr*)&p.addr, sizeof(p.addr)) == 0) {
+      Hello h = {kIdMagic, p.commId, kReleaseRank, 0};
+      bool ok = sendAll(fd, &h, sizeof(h));
+      close(fd);
+      if (ok) return ncclSuccess;
+    } else {
+      close(fd);
+    }
+    if (std::chrono::steady_clock::now() > deadline) {
+      WARN("bootstrap: could not release an unused root");
+      return ncclRemoteError;
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+}
+
+// Root of rank r when nranks ranks are spread over nRoots ids (reference bootstrap.cc:59-69, offset 0).
+static int rootIdFromRank(int r, int nranks, int nRoots) {
+  const int rmr = nranks % nRoots, rpr = nranks / nRoots, D = rmr * (rpr + 1);
+  return r < D ? r / (rpr + 1) : (r - D) / rpr + rmr;
+}
+
+// Each id k >= 1 is released by exactly one rank: the first rank of root k's group, or rank k % nranks
+// for an id no rank maps to (nId > nranks). An id listed twice is one root (still in use if it equals id 0).
+ncclResult_t bootstrapReleaseUnused(const ncclUniqueId* ids, int nId, int rank, int nranks) {
+  for (int k = 1; k < nId; k++) {
+    bool dup = false;
+    for (int j = 0; j < k && !dup; j++) dup = memcmp(&ids[j], &ids[k], sizeof(ncclUniqueId)) == 0;
+    if (dup) continue;
+    int releaser = k % nranks;
+    for (int r = 0; r < nranks; r++)
+      if (rootIdFromRank(r, nranks, nId) == k) {
+        releaser = r;
+        break;
+      }
+    if (releaser == rank) NCCLCHECK(bootstrapRelease(&ids[k]));
+  }
   return ncclSuccess;
 }
 

@@ -79,6 +79,8 @@ struct Bootstrap;
 struct LocalClique;
 ncclResult_t bootstrapGetUniqueId(ncclUniqueId* id);
 ncclResult_t bootstrapInit(const ncclUniqueId* id, int rank, int nranks, Bootstrap** out);
+ncclResult_t bootstrapRelease(const ncclUniqueId* id);  // tell an unused root to exit (InitRankScalable)
+ncclResult_t bootstrapReleaseUnused(const ncclUniqueId* ids, int nId, int rank, int nranks);  // this rank's share
 ncclResult_t bootstrapAllGather(Bootstrap* b, void* data, size_t bytesPerRank);
 ncclResult_t bootstrapBarrier(Bootstrap* b);
 void bootstrapClose(Bootstrap* b);
@@ -250,6 +252,7 @@ ncclResult_t transportConnect(ncclComm* comm);   // map peers after the PeerInfo
 ncclResult_t transportFree(ncclComm* comm);
 ncclResult_t transportDrainCredits(ncclComm* comm);  // wait for acks peers still owe (destroy)
 ncclResult_t commAllocDevState(ncclComm* comm);  // counters, DevComm upload, abort/error words
+size_t commDeviceBytes(const ncclComm* comm);     // device memory held (ncclCommMemStats)
 
 // ---------------------------------------------------------------- enqueue (reference src/enqueue.cc)
 enum CollFunc { FUNC_ALLREDUCE = 0, FUNC_REDUCESCATTER = 1, FUNC_ALLGATHER = 2, FUNC_REDUCE = 3 };
@@ -299,6 +302,13 @@ enum TuneAlgo { TUNE_DEFAULT = 0, TUNE_LL = 1, TUNE_ONESHOT = 2, TUNE_DIRECT = 3
 ncclResult_t tunerLoad(ncclComm* comm);
 void tunerUnload(ncclComm* comm);
 void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int* algo, int* nch);
+// the engine's cost model (tuner.cc): µs of fixed latency + µs of the busiest resource's transfer time
+enum ModelAlgo { MODEL_COPY, MODEL_LL, MODEL_LL128, MODEL_ONESHOT, MODEL_DIRECT, MODEL_SYM, MODEL_RING, MODEL_CHAIN };
+struct ModelCost {
+  double latUs, xferUs;
+  double total() const { return latUs + xferUs; }
+};
+ModelCost modelCost(ModelAlgo a, CollFunc func, int n, size_t bytes);
 ncclResult_t collJoin(const CollInfo& info);
 ncclResult_t launchPlan(const LaunchPlan& plan);  // kernels.hip
 
@@ -335,7 +345,7 @@ int typeSize(ncclDataType_t t);
 
 // ---------------------------------------------------------------- groups (reference src/group.cc)
 ncclResult_t groupStartInternal();
-ncclResult_t groupEndInternal();
+ncclResult_t groupEndInternal(ncclSimInfo_t* simInfo = nullptr);  // simInfo: ncclGroupSimulateEnd
 bool groupActive();
 void groupRecordError(ncclResult_t r);
 ncclResult_t groupDeferColl(const CollInfo& info);

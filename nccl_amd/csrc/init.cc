@@ -303,6 +303,24 @@ NCCL_EXPORT ncclResult_t ncclCommInitRank(ncclComm_t* newcomm, int nranks, ncclU
 }
 NCCL_ALIAS(ncclResult_t, ncclCommInitRank, ncclComm_t*, int, ncclUniqueId, int)
 
+// Several ids (reference init.cc:2695-2728, nccl.h.in:260-264; the number and order of ids are the same on
+// every rank). The reference spreads the bootstrap over nId roots; this single-node star rendezvouses at
+// commIds[0], and each other id's root is told to exit by one rank (bootstrapReleaseUnused).
+NCCL_EXPORT ncclResult_t ncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
+                                                  ncclUniqueId* commIds, ncclConfig_t* config) {
+  logInit();
+  if (nId < 1 || commIds == nullptr) {
+    WARN("ncclCommInitRankScalable : invalid nId %d or commIds NULL", nId);
+    return ncclInvalidArgument;
+  }
+  if (newcomm != nullptr && nranks >= 1 && nranks <= NCCL_AMD_MAX_RANKS && myrank >= 0 && myrank < nranks &&
+      checkConfig(config) == ncclSuccess) {
+    NCCLCHECK(bootstrapReleaseUnused(commIds, nId, myrank, nranks));
+  }
+  return initRankCommon(newcomm, nranks, commIds[0], myrank, config);
+}
+NCCL_ALIAS(ncclResult_t, ncclCommInitRankScalable, ncclComm_t*, int, int, int, ncclUniqueId*, ncclConfig_t*)
+
 // Single-process clique: every comm lives in this process, so peers are connected by raw pointers and
 // no socket rendezvous is needed (reference init.cc:2581-2643 runs the generic path in threads).
 NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
@@ -496,6 +514,25 @@ NCCL_EXPORT ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
   return ncclSuccess;
 }
 NCCL_ALIAS(ncclResult_t, ncclCommUserRank, const ncclComm_t, int*)
+
+// Reference mem_manager.cc:1010-1047. Everything this engine allocates for a communicator (staging slab,
+// flag and LL lines, counters) is persistent — there is no suspend/resume — so Suspend is 0, Suspended
+// is 0 and Total == Persist. A non-blocking communicator still initialising reports ncclInProgress.
+NCCL_EXPORT ncclResult_t ncclCommMemStats(ncclComm_t comm, ncclCommMemStat_t stat, uint64_t* value) {
+  NCCLCHECK(commCheck(comm, "ncclCommMemStats", "comm"));
+  if (value == nullptr) return ncclInvalidArgument;
+  int st = comm->asyncResult.load();
+  if (st == ncclInProgress) return ncclInProgress;
+  if (st != ncclSuccess) return (ncclResult_t)st;
+  switch (stat) {
+    case ncclStatGpuMemTotal:
+    case ncclStatGpuMemPersist: *value = commDeviceBytes(comm); return ncclSuccess;
+    case ncclStatGpuMemSuspend:
+    case ncclStatGpuMemSuspended: *value = 0; return ncclSuccess;
+    default: return ncclInvalidArgument;
+  }
+}
+NCCL_ALIAS(ncclResult_t, ncclCommMemStats, ncclComm_t, ncclCommMemStat_t, uint64_t*)
 
 // ---- custom operators (reference enqueue.cc:2560-2576 user ops, ncclRedOpCreatePreMulSum) ----
 NCCL_EXPORT ncclResult_t ncclRedOpCreatePreMulSum(ncclRedOp_t* op, void* scalar, ncclDataType_t datatype,

@@ -31,6 +31,17 @@ static size_t flagsBytes(const ncclComm* c) {
   return ll64Offset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes;
 }
 
+// Device memory this communicator holds on its GPU (ncclCommMemStats): staging slab, flag/LL lines,
+// step counters and the device copy of DevComm. All of it lives as long as the communicator.
+size_t commDeviceBytes(const ncclComm* c) {
+  size_t b = 0;
+  if (c->staging) b += stagingBytes(c);
+  if (c->flags) b += flagsBytes(c);
+  if (c->counters) b += (size_t)c->maxChannels * CTR_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
+  if (c->devComm) b += sizeof(DevComm);
+  return b;
+}
+
 ncclResult_t transportSetup(ncclComm* comm) {
   HIPCHECK(hipSetDevice(comm->device));
   if (comm->nRanks == 1) return ncclSuccess;  // nranks==1 never touches peers (onerank.cu:49-110)

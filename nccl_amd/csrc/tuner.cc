@@ -16,6 +16,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 
@@ -129,6 +130,56 @@ void tunerUnload(ncclComm* comm) {
   }
 }
 
+// The engine's cost model (µs, the unit of the reference's tuning table, tuning.cc): a fixed launch +
+// handshake latency plus the busiest resource's time — a rank's link bytes over its n-1 xGMI links
+// (≈50 GB/s per link and direction, ring / chain: over ONE link), or its local HBM bytes at ≈6.3 TB/s
+// (MI355X_MICROARCH.md's measured copy rate), whichever is longer. `bytes` is the collective's size as the
+// tuner sees it (AllReduce / Reduce: the buffer; ReduceScatter / AllGather: n × the per-rank block).
+// Used for the plugin's cost table and by ncclGroupSimulateEnd.
+ModelCost modelCost(ModelAlgo a, CollFunc func, int n, size_t bytes) {
+  const double S = (double)bytes, link = 5.0e4 /* B/µs per link */, hbm = 6.3e6 /* B/µs */;
+  if (n <= 1) return {2.0, (a == MODEL_COPY ? 2.0 * S : 0.0) / hbm};  // one rank: a copy or nothing
+  const double nl = n - 1.0;
+  const bool ar = func == FUNC_ALLREDUCE, red = func == FUNC_REDUCE;
+  double lat = 10.0, linkB = 0, hbmB = 0, links = nl;
+  switch (a) {
+    case MODEL_LL:  // 16-byte lines carry 8 payload bytes, to every peer for AllReduce / Reduce
+      lat = 4.0;
+      linkB = (ar || red ? 2.0 * nl : 2.0 * nl / n) * S;
+      break;
+    case MODEL_LL128:  // 64-byte lines carry 56 payload bytes
+      lat = 4.5;
+      linkB = (64.0 / 56.0) * (ar || red ? nl : nl / n) * S;
+      break;
+    case MODEL_ONESHOT:  // every rank publishes its buffer to every peer and folds all n
+      lat = 7.0;
+      linkB = nl * S;
+      hbmB = (n + 1.0) * S;
+      break;
+    case MODEL_DIRECT:  // scatter-reduce-gather: 2(n-1)/n S (AllReduce), (n-1)/n S (RS / AG / Reduce)
+    case MODEL_SYM:
+      lat = a == MODEL_SYM ? 8.0 : 10.0;
+      linkB = (ar ? 2.0 * nl / n : nl / n) * S;
+      hbmB = ar ? (2.0 + 4.0 * nl / n) * S : 2.0 * S;
+      break;
+    case MODEL_RING:  // one link per direction; n-1 (RS / AG) or 2(n-1) (AllReduce) pipelined hops
+      lat = 10.0 + 2.0 * (ar ? 2.0 * nl : nl);
+      linkB = (ar ? 2.0 * nl / n : nl / n) * S;
+      hbmB = ar ? (2.0 + 4.0 * nl / n) * S : 2.0 * S;
+      links = 1.0;
+      break;
+    case MODEL_CHAIN:  // reduce up the chain and broadcast down: S per link and direction, 2(n-1) hops
+      lat = 10.0 + 3.0 * 2.0 * nl;
+      linkB = S;
+      hbmB = 4.0 * S;
+      links = 1.0;
+      break;
+    case MODEL_COPY: break;
+  }
+  const double t = std::max(linkB / (links * link), hbmB / hbm);
+  return {lat, t};
+}
+
 // Ask the plugin. `algo` (in: the engine's default choice, out: the plugin's) and `nch` (out: channel
 // override or 0). llMask: 1 = the LL kernel can take this collective, 2 = the LL64 (LL128-class) one can.
 void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int* algo, int* nch) {
@@ -136,30 +187,24 @@ void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int 
   *nch = 0;
   if (!comm->tunerLoaded) return;
   const int n = comm->nRanks;
-  const double linkGBps = 50.0 * (n - 1);  // per-rank aggregate xGMI estimate (us per byte = 1e-3/GBps)
-  const double usPerByte = 1e-3 / linkGBps;
+  auto us = [&](ModelAlgo a) { return (float)modelCost(a, func, n, bytes).total(); };
   float table[NCCL_NUM_ALGORITHMS][NCCL_NUM_PROTOCOLS];
   for (int a = 0; a < NCCL_NUM_ALGORITHMS; a++)
     for (int p = 0; p < NCCL_NUM_PROTOCOLS; p++) table[a][p] = (float)NCCL_ALGO_PROTO_IGNORE;
   ncclFunc_t f = ncclFuncAllReduce;
   if (func == FUNC_ALLREDUCE) {
     if (llOk) {
-      table[NCCL_ALGO_RING][NCCL_PROTO_LL] = (float)(4.0 + 2.0 * (n - 1) * bytes * usPerByte);
+      table[NCCL_ALGO_RING][NCCL_PROTO_LL] = us(MODEL_LL);
       table[NCCL_ALGO_TREE][NCCL_PROTO_LL] = table[NCCL_ALGO_RING][NCCL_PROTO_LL];
     }
-    if (ll128Ok)  // 64 link bytes per 56 payload bytes, to every peer
-      table[NCCL_ALGO_RING][NCCL_PROTO_LL128] = (float)(4.5 + (64.0 / 56.0) * (n - 1) * bytes * usPerByte);
-    table[NCCL_ALGO_TREE][NCCL_PROTO_SIMPLE] = (float)(7.0 + (n - 1) * bytes * usPerByte);
-    table[NCCL_ALGO_RING][NCCL_PROTO_SIMPLE] = (float)(10.0 + 2.0 * (n - 1) / n * bytes * usPerByte);
+    if (ll128Ok) table[NCCL_ALGO_RING][NCCL_PROTO_LL128] = us(MODEL_LL128);
+    table[NCCL_ALGO_TREE][NCCL_PROTO_SIMPLE] = us(MODEL_ONESHOT);
+    table[NCCL_ALGO_RING][NCCL_PROTO_SIMPLE] = us(MODEL_DIRECT);
   } else {
     f = func == FUNC_REDUCESCATTER ? ncclFuncReduceScatter : func == FUNC_ALLGATHER ? ncclFuncAllGather : ncclFuncReduce;
-    table[NCCL_ALGO_RING][NCCL_PROTO_SIMPLE] = (float)(10.0 + (n - 1.0) / n * bytes * usPerByte);
-    if (llOk)  // Reduce's LL lines go to every peer, like AllReduce's
-      table[NCCL_ALGO_RING][NCCL_PROTO_LL] =
-          (float)(4.0 + (func == FUNC_REDUCE ? 2.0 * (n - 1) : 2.0 * (n - 1.0) / n) * bytes * usPerByte);
-    if (ll128Ok)
-      table[NCCL_ALGO_RING][NCCL_PROTO_LL128] =
-          (float)(4.5 + (64.0 / 56.0) * (func == FUNC_REDUCE ? (n - 1.0) : (n - 1.0) / n) * bytes * usPerByte);
+    table[NCCL_ALGO_RING][NCCL_PROTO_SIMPLE] = us(MODEL_DIRECT);
+    if (llOk) table[NCCL_ALGO_RING][NCCL_PROTO_LL] = us(MODEL_LL);
+    if (ll128Ok) table[NCCL_ALGO_RING][NCCL_PROTO_LL128] = us(MODEL_LL128);
   }
   float before[NCCL_NUM_ALGORITHMS][NCCL_NUM_PROTOCOLS];
   memcpy(before, table, sizeof(table));

@@ -526,3 +526,60 @@ def test_communicator_churn_releases_resources(built):
     free1, _ = torch.cuda.mem_get_info()
     # each communicator holds > 1 GiB of staging: a leak of even one would show
     assert free0 - free1 < (256 << 20), f"device memory not released: {(free0 - free1) >> 20} MiB lost"
+
+
+def test_init_rank_scalable_and_mem_stats(built):
+    """ncclCommInitRankScalable (reference init.cc:2695-2728) with three ids, two ranks created from one
+    thread (non-blocking config), then an AllReduce bit-exact vs the oracle; ncclCommMemStats (reference
+    mem_manager.cc:1010-1047): everything the communicator holds is persistent, > 1 GiB of staging."""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    uids = [nccl_amd.get_unique_id() for _ in range(3)]
+    cfg = nccl_amd.Config.default(blocking=0)
+    comms = [nccl_amd.Communicator.init(2, r, uids, cfg) for r in range(2)]
+    for c in comms:
+        c.wait_ready(120)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    errs = G.run_case(list(zip(comms, streams)), "allreduce", 7, 0, 123_457, 0, seed=21)
+    stats = [{s.name: c.mem_stats(s) for s in nccl_amd.MemStat} for c in comms]
+    for c in comms:
+        c.destroy()
+    assert not errs, errs
+    for st in stats:
+        assert st["GPU_MEM_TOTAL"] == st["GPU_MEM_PERSIST"] > (1 << 30), st
+        assert st["GPU_MEM_SUSPEND"] == 0 and st["GPU_MEM_SUSPENDED"] == 0, st
+
+
+def test_group_simulate_end_launches_nothing(two_comms):
+    """ncclGroupSimulateEnd (reference group.cc:116-123): the group's ops are planned, not launched, and the
+    cost model's estimate comes back (µs in the C struct, seconds through the nccl4py mirror); the comms keep
+    working afterwards (planning a simulated group changes no device-visible state)."""
+    import torch
+    import nccl_amd
+    import oracle
+    comms, streams = two_comms
+    est = {}
+    for count in (1024, 1 << 16, 1 << 24):
+        ins = _inputs(2, count, seed=count % 97)
+        sends = [torch.from_numpy(x).cuda() for x in ins]
+        recvs = [torch.zeros(count, device="cuda") for _ in range(2)]
+        torch.cuda.synchronize()
+        nccl_amd.group_start()
+        for c, s, x, y in zip(comms, streams, sends, recvs):
+            c.allreduce(x, y, nccl_amd.SUM, stream=s)
+        sim = nccl_amd.group_end(simulate=True)
+        torch.cuda.synchronize()
+        assert not recvs[0].any() and not recvs[1].any(), "a simulated group launched work"
+        est[count] = sim.estimated_time
+        with nccl_amd.group():
+            for c, s, x, y in zip(comms, streams, sends, recvs):
+                c.allreduce(x, y, nccl_amd.SUM, stream=s)
+        torch.cuda.synchronize()
+        want = oracle.all_reduce(ins, 7, 0)
+        for y in recvs:
+            assert np.array_equal(y.cpu().numpy(), want)
+    assert 0 < est[1024] <= est[1 << 16] < est[1 << 24], est
+    assert est[1024] < 20e-6 and est[1 << 24] > 100e-6, est  # LL latency vs 64 MiB over one xGMI link

@@ -90,6 +90,37 @@ def test_bootstrap_across_processes(built, n):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+@pytest.mark.parametrize("n,nid", [(4, 2), (5, 3), (2, 5), (8, 8)])
+def test_bootstrap_scalable_ids(built, n, nid):
+    """ncclCommInitRankScalable's rendezvous (reference init.cc:2695-2728): the ranks meet at id 0, the
+    other ids' roots are released by exactly one rank each (the reference's rank-to-root partition,
+    bootstrap.cc:59-69) and stop listening; nid > n included."""
+    subprocess.check_call(["make", "-s", "bootstrap-test"], cwd=ROOT)
+    exe = os.path.join(ROOT, "build", "bootstrap_test")
+    env = dict(os.environ, NCCL_AMD_BOOTSTRAP_TIMEOUT_MS="20000")
+    r = subprocess.run([exe, str(n), "2", "scalable", str(nid)], env=env, capture_output=True, text=True,
+                       timeout=60)
+    assert r.returncode == 0 and "roots_left=0" in r.stdout, r.stdout + r.stderr
+
+
+def test_new_api_argument_checks_without_gpu(built):
+    """ncclCommInitRankScalable / ncclCommMemStats / ncclGroupSimulateEnd argument checks (no GPU)."""
+    lib = nccl_amd.load()
+    P = ctypes.c_void_p
+    c = P()
+    assert lib.ncclCommInitRankScalable(ctypes.byref(c), 2, 0, 0, None, None) == 4   # nId < 1
+    v = ctypes.c_uint64()
+    assert lib.ncclCommMemStats(None, 3, ctypes.byref(v)) == 4                      # NULL comm
+    si = nccl_amd.SimInfo.default()
+    assert lib.ncclGroupSimulateEnd(ctypes.byref(si)) == 5                          # not in a group
+    bad = nccl_amd.SimInfo.default()
+    bad.magic = 0
+    assert lib.ncclGroupStart() == 0
+    assert lib.ncclGroupSimulateEnd(ctypes.byref(bad)) == 4                         # uninitialised struct
+    assert lib.ncclGroupStart() == 0                                                # empty group: 0 us
+    assert lib.ncclGroupSimulateEnd(ctypes.byref(si)) == 0 and si.estimatedTime == 0.0
+
+
 def test_registration_argument_checks_without_gpu(built):
     lib = nccl_amd.load()
     P = ctypes.c_void_p

@@ -32,9 +32,10 @@ def _run(path, *args, **env):
 
 
 @pytest.mark.parametrize("san,args", [("asan", ("5", "4")), ("asan", ("5", "4", "threads")),
-                                      ("tsan", ("6", "4", "threads"))])
+                                      ("tsan", ("6", "4", "threads")), ("asan", ("5", "2", "scalable", "3"))])
 def test_bootstrap_sanitized(sanitized, san, args):
-    assert "failures=0" in _run(os.path.join(sanitized, san, "bootstrap_test"), *args)
+    out = _run(os.path.join(sanitized, san, "bootstrap_test"), *args)
+    assert "failures=0" in out and "roots_left=0" in out if "scalable" in args else "failures=0" in out
 
 
 @pytest.mark.parametrize("san,args", [("asan", ()), ("tsan", ("nofork",))])
