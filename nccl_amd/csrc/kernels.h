@@ -79,6 +79,25 @@ __device__ __forceinline__ void storeRemoteAt(__amdgpu_buffer_rsrc_t r, uint32_t
   __builtin_amdgcn_raw_buffer_store_b128(v, r, byteOff, 0, kSysWriteThrough);
 }
 
+// This rank's own outputs (phase B's fold result, phase C's gathered blocks, the symmetric kernels' results):
+// NCCL_AMD_LOCAL_WT=1 writes them with the same system-scope write-through buffer stores as the remote ones
+// instead of global nontemporal stores (A/B knob; the nRanks==1 copy measured the difference).
+// `base` is the batch's wave-uniform first pack, so offsets stay small at any buffer size.
+#ifndef NCCL_AMD_LOCAL_WT
+#define NCCL_AMD_LOCAL_WT 0
+#endif
+struct LocalStore {
+  __amdgpu_buffer_rsrc_t r;
+  u32x4* d;
+  __device__ __forceinline__ LocalStore(void* dst, uint64_t base) : d((u32x4*)dst + base) {
+    if (NCCL_AMD_LOCAL_WT) r = remoteRsrc(d);
+  }
+  __device__ __forceinline__ void put(uint32_t k, u32x4 v) {  // pack base + k
+    if (NCCL_AMD_LOCAL_WT) __builtin_amdgcn_raw_buffer_store_b128(v, r, k * 16u, 0, kSysWriteThrough);
+    else __builtin_nontemporal_store(v, d + k);
+  }
+};
+
 // One element stored system-scope write-through (tails and unaligned ranges of published data).
 template <typename T>
 __device__ __forceinline__ void storeRemoteElt(T* p, T v) {
@@ -206,11 +225,12 @@ __device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t n
       u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s + i + u * kThreads);
+      LocalStore ls(dst, i - threadIdx.x);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         if (REMOTE && NCCL_AMD_BUFFER_STORES) storeRemoteAt(rd, (uint32_t)((i + u * kThreads) * 16), v[u]);
         else if (REMOTE) storeRemote(d + i + u * kThreads, v[u]);
-        else __builtin_nontemporal_store(v[u], d + i + u * kThreads);
+        else ls.put(threadIdx.x + u * kThreads, v[u]);
       }
     }
     for (; i < npk; i += kThreads) {
@@ -295,13 +315,14 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
           cur[u] = nxt[u];
         }
       }
+      LocalStore ls(dstLocal, base - threadIdx.x);
 #pragma unroll
       for (int u = 0; u < U; u++) {
         uint64_t i = base + (uint64_t)u * kThreads;
         if (i >= npk) continue;
 #pragma unroll
         for (int e = 0; e < EPP; e++) acc[u].e[e] = fn.post(acc[u].e[e]);
-        if (dstLocal) __builtin_nontemporal_store(acc[u].v, (u32x4*)dstLocal + i);
+        if (dstLocal) ls.put(threadIdx.x + u * kThreads, acc[u].v);
         for (int p = 0; p < nPush; p++) {
           if (NCCL_AMD_BUFFER_STORES) storeRemoteAt(remoteRsrc(dstPush[p]), (uint32_t)(i * 16), acc[u].v);
           else storeRemote((u32x4*)dstPush[p] + i, acc[u].v);

@@ -49,20 +49,26 @@ ncclResult_t warmKernels() {
 
 // Streaming copy (reference onerank.cu:52-56 uses cudaMemcpyAsync; this is the hand-written
 // replacement): 16 B per lane, U packs in flight per lane, grid-stride over 256*U*16-byte tiles.
-// NTL/NTS select nontemporal loads/stores (measured variants).
-template <int U, bool NTL, bool NTS>
+// NTL selects nontemporal loads; SPOL the store: -2 plain, -1 global nontemporal, >= 0 a buffer store with
+// that cache policy (sc0 = 1, nt = 2, sc1 = 16; offsets from the tile's own base, so 32 bits suffice)
+// (measured variants).
+template <int U, bool NTL, int SPOL>
 __global__ void __launch_bounds__(256) copyKernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
                                                   uint64_t npk) {
   uint64_t stride = (uint64_t)gridDim.x * 256 * U;
-  for (uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; base < npk; base += stride) {
+  for (uint64_t t0 = (uint64_t)blockIdx.x * 256 * U; t0 < npk; t0 += stride) {
+    const uint64_t base = t0 + threadIdx.x;
     u32x4 v[U];
 #pragma unroll
     for (int u = 0; u < U; u++)
       if (base + u * 256 < npk) v[u] = NTL ? __builtin_nontemporal_load(src + base + u * 256) : src[base + u * 256];
+    __amdgpu_buffer_rsrc_t rd;
+    if constexpr (SPOL >= 0) rd = remoteRsrc(dst + t0);
 #pragma unroll
     for (int u = 0; u < U; u++)
       if (base + u * 256 < npk) {
-        if (NTS) __builtin_nontemporal_store(v[u], dst + base + u * 256);
+        if constexpr (SPOL >= 0) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (uint32_t)((threadIdx.x + u * 256) * 16), 0, SPOL);
+        else if constexpr (SPOL == -1) __builtin_nontemporal_store(v[u], dst + base + u * 256);
         else dst[base + u * 256] = v[u];
       }
   }
@@ -78,7 +84,10 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
   if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
     uint64_t npk = bytes >> 4;
     if (npk) {
-      // variant (NCCL_AMD_COPY_VARIANT): 0 nt/nt U4 (default), 1 plain/plain U4, 2 plain/nt U4, 3 nt/nt U8
+      // variant (NCCL_AMD_COPY_VARIANT): 0 (default) nt loads + system-scope write-through buffer stores
+      // (sc0|sc1) U4; 1 plain/plain U4, 2 plain/global-nt U4, 3 nt/global-nt U8, 9 nt/global-nt U4 (the
+      // round-1/2 default); nt loads with buffer stores under cache policy 4 sc0|sc1, 5 sc1, 6 sc1|nt, 7 nt,
+      // 8 none (scripts/copy_policy_probe.hip)
       int U = var == 3 ? 8 : 4;
       uint64_t tiles = (npk + 256 * U - 1) / (256 * U);
       // one 16 KiB tile per workgroup by default: measured best on 256 MiB with buffers rotated past the
@@ -87,10 +96,15 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
       u32x4* d = (u32x4*)dst;
       const u32x4* s = (const u32x4*)src;
       switch (var) {
-        case 1: hipLaunchKernelGGL((copyKernel<4, false, false>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 2: hipLaunchKernelGGL((copyKernel<4, false, true>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 3: hipLaunchKernelGGL((copyKernel<8, true, true>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        default: hipLaunchKernelGGL((copyKernel<4, true, true>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 1: hipLaunchKernelGGL((copyKernel<4, false, -2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 2: hipLaunchKernelGGL((copyKernel<4, false, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 3: hipLaunchKernelGGL((copyKernel<8, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 5: hipLaunchKernelGGL((copyKernel<4, true, 16>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 6: hipLaunchKernelGGL((copyKernel<4, true, 18>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 7: hipLaunchKernelGGL((copyKernel<4, true, 2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 8: hipLaunchKernelGGL((copyKernel<4, true, 0>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 9: hipLaunchKernelGGL((copyKernel<4, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        default: hipLaunchKernelGGL((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
       }
       HIPCHECK(hipGetLastError());
     }
