@@ -66,7 +66,8 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   c->nRanks = nranks;
   c->device = dev;
   c->blocking = true;
-  c->minCTAs = 1;
+  // reference env names (env.rst :884/:901): NCCL_MIN/MAX_CTAS, or the older NCCL_MIN/MAX_NCHANNELS
+  c->minCTAs = (int)paramInt("NCCL_MIN_CTAS", paramInt("NCCL_MIN_NCHANNELS", 1));
   c->maxCTAs = (int)paramInt("NCCL_MAX_CTAS", paramInt("NCCL_MAX_NCHANNELS", 256));
   if (cfg) {
     if (cfg->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = cfg->blocking != 0;
@@ -84,11 +85,13 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   if (c->nSlots < 1) c->nSlots = 1;
   // Slot size: the staging slab (maxChannels x 2 kinds x nSlots x nRanks x slot) is sized to a fixed
   // HBM budget (NCCL_AMD_STAGING_MIB, default 1 GiB of the 288 GB), so fewer ranks get bigger slots
-  // (fewer handshakes per byte). NCCL_AMD_SLOT_BYTES overrides.
+  // (fewer handshakes per byte). NCCL_AMD_SLOT_BYTES overrides; so does the reference's NCCL_BUFFSIZE (bytes
+  // of one channel's buffer towards one peer, env.rst :857), which here is split into the nSlots slots.
   int64_t budget = paramInt("NCCL_AMD_STAGING_MIB", 1024) << 20;
   int64_t sb = budget / ((int64_t)c->maxChannels * 2 * c->nSlots * (nranks > 1 ? nranks : 2));
   if (sb > (1 << 20)) sb = 1 << 20;
   if (sb < (16 << 10)) sb = 16 << 10;
+  if (int64_t buff = paramInt("NCCL_BUFFSIZE", 0)) sb = buff / c->nSlots;
   sb = paramInt("NCCL_AMD_SLOT_BYTES", sb);
   sb = (sb + 4095) / 4096 * 4096;
   if (sb < 4096) sb = 4096;

@@ -583,3 +583,31 @@ def test_group_simulate_end_launches_nothing(two_comms):
             assert np.array_equal(y.cpu().numpy(), want)
     assert 0 < est[1024] <= est[1 << 16] < est[1 << 24], est
     assert est[1024] < 20e-6 and est[1 << 24] > 100e-6, est  # LL latency vs 64 MiB over one xGMI link
+
+
+def test_reference_buffer_and_channel_knobs(built):
+    """NCCL_BUFFSIZE (reference env.rst :857: one channel's buffer towards one peer) sets the staging slot
+    size, visible in ncclCommMemStats; NCCL_MAX_NCHANNELS caps the channels; results stay bit-exact."""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    old = {k: os.environ.get(k) for k in ("NCCL_BUFFSIZE", "NCCL_MAX_NCHANNELS", "NCCL_MIN_NCHANNELS")}
+    os.environ.update(NCCL_BUFFSIZE=str(256 << 10), NCCL_MAX_NCHANNELS="16", NCCL_MIN_NCHANNELS="4")
+    try:
+        comms = nccl_amd.Communicator.init_all([0, 0])
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    errs = G.run_case(list(zip(comms, streams)), "allreduce", 7, 0, 3_000_017, 0, seed=23)
+    total = comms[0].mem_stats()
+    for c in comms:
+        c.destroy()
+    assert not errs, errs
+    slab = 16 * 2 * 2 * 2 * (128 << 10)  # channels x kinds x slots x ranks x (BUFFSIZE / 2 slots)
+    assert slab <= total < slab + (64 << 20), (total, slab)
