@@ -20,32 +20,32 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
 }
 
 // WT: destination stores are system-scope write-through buffer stores (the library's remote-store flavour)
-template <int U, bool WT>
-__global__ void __launch_bounds__(512) copyK(u32x4* __restrict__ d, const u32x4* __restrict__ s, uint64_t npk) {
-  const uint64_t stride = (uint64_t)gridDim.x * 512 * U;
+template <int U, bool WT, int BS = 512>
+__global__ void __launch_bounds__(BS) copyK(u32x4* __restrict__ d, const u32x4* __restrict__ s, uint64_t npk) {
+  const uint64_t stride = (uint64_t)gridDim.x * BS * U;
   // 32-bit buffer offsets cover 4 GiB; the probe's buffers are 256 MiB
   __amdgpu_buffer_rsrc_t rd = rsrc(d);
-  for (uint64_t i = (uint64_t)blockIdx.x * 512 * U + threadIdx.x; i + (U - 1) * 512 < npk; i += stride) {
+  for (uint64_t i = (uint64_t)blockIdx.x * BS * U + threadIdx.x; i + (U - 1) * BS < npk; i += stride) {
     u32x4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s + i + u * 512);
+    for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s + i + u * BS);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      if (WT) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (uint32_t)((i + u * 512) * 16), 0, 1 | 16);
-      else __builtin_nontemporal_store(v[u], d + i + u * 512);
+      if (WT) __builtin_amdgcn_raw_buffer_store_b128(v[u], rd, (uint32_t)((i + u * BS) * 16), 0, 1 | 16);
+      else __builtin_nontemporal_store(v[u], d + i + u * BS);
     }
   }
 }
 
-template <int U, bool WT>
+template <int U, bool WT, int BS = 512>
 static double timeIt(u32x4* d, const u32x4* s, uint64_t npk, int grid) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int i = 0; i < 3; i++) hipLaunchKernelGGL((copyK<U, WT>), dim3(grid), dim3(512), 0, 0, d, s, npk);
+  for (int i = 0; i < 3; i++) hipLaunchKernelGGL((copyK<U, WT, BS>), dim3(grid), dim3(BS), 0, 0, d, s, npk);
   const int iters = 10;
   CK(hipEventRecord(a));
-  for (int i = 0; i < iters; i++) hipLaunchKernelGGL((copyK<U, WT>), dim3(grid), dim3(512), 0, 0, d, s, npk);
+  for (int i = 0; i < iters; i++) hipLaunchKernelGGL((copyK<U, WT, BS>), dim3(grid), dim3(BS), 0, 0, d, s, npk);
   CK(hipEventRecord(b));
   CK(hipEventSynchronize(b));
   float ms = 0;
@@ -81,6 +81,17 @@ int main() {
         printf("%-18s %5d %3d %10.1f %10.1f %12.2f\n", m.name, g, u, ms * 1e3, gbs, gbs / g);
         fflush(stdout);
       }
+  // workgroup size at low workgroup counts (plain -> UC write-through, U = 8): is the ~50 GB/s ceiling per
+  // workgroup (waves) or per CU?
+  printf("# workgroup size: plain->UC(wt), U=8\n");
+  for (int g : {32, 64, 128}) {
+    double a = timeIt<8, true, 256>(uD, nS, npk, g), b = timeIt<8, true, 512>(uD, nS, npk, g),
+           c = timeIt<8, true, 1024>(uD, nS, npk, g);
+    double ga = 2.0 * bytes / (a * 1e-3) / 1e9, gb = 2.0 * bytes / (b * 1e-3) / 1e9, gc = 2.0 * bytes / (c * 1e-3) / 1e9;
+    printf("grid %4d  256 thr %8.1f GB/s (%6.2f/WG)  512 thr %8.1f (%6.2f/WG)  1024 thr %8.1f (%6.2f/WG)\n", g, ga,
+           ga / g, gb, gb / g, gc, gc / g);
+    fflush(stdout);
+  }
   CK(hipFree(nS));
   CK(hipFree(nD));
   CK(hipFree(uS));
