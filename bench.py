@@ -549,7 +549,7 @@ def main(argv=None):
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
             "traffic_source": "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)"
             if traffic else None,
-            "kernel": "copyKernel<4,true,17>" if n == 1 else "collKernel<float,0,0> (AllReduce, direct)",
+            "kernel": "copyKernel<2,true,17>" if n == 1 else "collKernel<float,0,0> (AllReduce, direct)",
             "algorithmic_bytes_per_launch": hbm_bytes, "kernel_avg_ms": round(gpu_ms, 5)}
     if n > 1:
         spec_peak = (n - 1) * XGMI_LINK_GBPS_DIR

@@ -85,10 +85,10 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
     uint64_t npk = bytes >> 4;
     if (npk) {
       // variant (NCCL_AMD_COPY_VARIANT): 0 (default) nt loads + system-scope write-through buffer stores
-      // (sc0|sc1) U4; 1 plain/plain U4, 2 plain/global-nt U4, 3 nt/global-nt U8, 9 nt/global-nt U4 (the
-      // round-1/2 default); nt loads with buffer stores under cache policy 4 sc0|sc1, 5 sc1, 6 sc1|nt, 7 nt,
-      // 8 none (scripts/copy_policy_probe.hip)
-      int U = var == 3 ? 8 : 4;
+      // (sc0|sc1), 2 packs per thread (8 KiB tiles); 1 plain/plain U4, 2 plain/global-nt U4, 3 nt/global-nt U8,
+      // 9 nt/global-nt U4 (the round-1/2 default); nt loads with U4 buffer stores under cache policy 4 sc0|sc1,
+      // 5 sc1, 6 sc1|nt, 7 nt, 8 none (scripts/copy_policy_probe.hip, copy_shape_probe.hip)
+      int U = var == 3 ? 8 : (var == 0 || var > 9) ? 2 : 4;
       uint64_t tiles = (npk + 256 * U - 1) / (256 * U);
       // one 16 KiB tile per workgroup by default: measured best on 256 MiB with buffers rotated past the
       // 256 MiB Infinity Cache (6.48 TB/s vs 6.26 for a 2048-block grid-stride; scripts/copy_variants.hip)
@@ -104,7 +104,8 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
         case 7: hipLaunchKernelGGL((copyKernel<4, true, 2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
         case 8: hipLaunchKernelGGL((copyKernel<4, true, 0>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
         case 9: hipLaunchKernelGGL((copyKernel<4, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        default: hipLaunchKernelGGL((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 4: hipLaunchKernelGGL((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        default: hipLaunchKernelGGL((copyKernel<2, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
       }
       HIPCHECK(hipGetLastError());
     }
