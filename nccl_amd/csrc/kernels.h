@@ -1309,17 +1309,37 @@ inline ncclResult_t launchSymIntOp(const SymPlan& p) {
 
 // ------------------------------------------------------------------------------------ nRanks == 1
 
-// PreMulSum on one rank (reference onerank.cu:14-47): out = post(pre(in)).
+// PreMulSum on one rank (reference onerank.cu:14-47): out = post(pre(in)). Like the nRanks == 1 copy (kernels.hip):
+// 16-byte packs, 2 per thread, one 8 KiB tile per 256-thread workgroup (grid-stride past the grid), nontemporal
+// loads and system-scope write-through buffer stores; element-wise for unaligned buffers and the
+// < 16-byte tail.
 template <typename T, int OP>
 __global__ void __launch_bounds__(256) oneRankKernel(T* dst, const T* src, uint64_t n, uint64_t arg,
-                                                     const void* argPtr) {
+                                                     const void* argPtr, int aligned) {
   uint64_t a = arg;
   if (argPtr) {
     a = 0;
     __builtin_memcpy(&a, argPtr, sizeof(T));
   }
   const Red<T, OP> fn(a);
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+  constexpr int EPP = 16 / sizeof(T), U = 2;
+  const uint64_t npk = aligned ? n / EPP : 0;
+  const u32x4* s = (const u32x4*)src;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * 256 * U; t0 < npk; t0 += (uint64_t)gridDim.x * 256 * U) {
+    PackU<T> v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (t0 + threadIdx.x + u * 256 < npk) v[u].v = __builtin_nontemporal_load(s + t0 + threadIdx.x + u * 256);
+    const __amdgpu_buffer_rsrc_t rd = remoteRsrc((u32x4*)dst + t0);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (t0 + threadIdx.x + u * 256 < npk) {
+#pragma unroll
+        for (int e = 0; e < EPP; e++) v[u].e[e] = fn.post(fn.pre(v[u].e[e]));
+        __builtin_amdgcn_raw_buffer_store_b128(v[u].v, rd, (threadIdx.x + u * 256) * 16u, 0, kSysWriteThrough);
+      }
+  }
+  for (uint64_t i = npk * EPP + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     dst[i] = fn.post(fn.pre(src[i]));
 }
 
@@ -1358,10 +1378,13 @@ inline void launchColl(const LaunchPlan& p) {
 template <typename T, int OP>
 inline ncclResult_t launchTyped(const LaunchPlan& p) {
   if (p.algo == ALGO_ONERANK) {
-    int grid = (int)std::min<uint64_t>(1024, (p.args.count + 255) / 256);
+    const int aligned = (((uintptr_t)p.args.recvbuff | (uintptr_t)p.args.sendbuff) & 15) == 0;
+    constexpr uint64_t kTile = 256 * 2 * (16 / sizeof(T));  // elements per 8 KiB tile
+    const uint64_t units = aligned ? (p.args.count + kTile - 1) / kTile : (p.args.count + 255) / 256;
+    int grid = (int)std::min<uint64_t>(aligned ? (1u << 20) : 1024, units);
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL((oneRankKernel<T, OP>), dim3(grid), dim3(256), 0, p.stream, (T*)p.args.recvbuff,
-                       (const T*)p.args.sendbuff, p.args.count, p.args.redArg, p.args.redArgPtr);
+                       (const T*)p.args.sendbuff, p.args.count, p.args.redArg, p.args.redArgPtr, aligned);
     HIPCHECK(hipGetLastError());
     return ncclSuccess;
   }
