@@ -339,3 +339,80 @@ def test_two_gib_window_multi_process(built):
     assert len(results) == 2, f"only {len(results)} of 2 ranks reported"
     bad = [e for r in sorted(results) for e in results[r]]
     assert not bad, "\n".join(bad)
+
+
+def _example_worker(rank, nranks, uid, mode, q):
+    """The reference's docs/examples/05_symmetric_memory/01_allreduce/c/main.cc:75-170 (mode "window") and
+    04_user_buffer_registration/01_allreduce/c/main.cc:75-166 (mode "register") as written: 1M floats in
+    ncclMemAlloc'd buffers, every element = rank, ncclAllReduce sum; every element must be n(n-1)/2."""
+    try:
+        import ctypes
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        lib = nccl_amd.load()
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        count = 1024 * 1024
+        size = count * 4
+        send, recv = ctypes.c_void_p(), ctypes.c_void_p()
+        assert lib.ncclMemAlloc(ctypes.byref(send), size) == 0 and lib.ncclMemAlloc(ctypes.byref(recv), size) == 0
+        handles = []
+        if mode == "window":
+            handles = [comm.register_window(send.value, size), comm.register_window(recv.value, size)]
+        else:
+            handles = [comm.register_buffer(send.value, size), comm.register_buffer(recv.value, size)]
+        host = torch.full((count,), float(rank), dtype=torch.float32)
+        torch.cuda.synchronize()
+        rt = ctypes.CDLL("libamdhip64.so")  # the HIP runtime torch already loaded (matched by soname)
+        assert rt.hipMemcpy(send, ctypes.c_void_p(host.data_ptr()), ctypes.c_size_t(size), 1) == 0  # H2D
+        s = torch.cuda.Stream()
+        comm.all_reduce_raw(send.value, recv.value, count, 7, 0, s.cuda_stream)
+        s.synchronize()
+        out = torch.empty(count, dtype=torch.float32)
+        assert rt.hipMemcpy(ctypes.c_void_p(out.data_ptr()), recv, ctypes.c_size_t(size), 2) == 0  # D2H
+        want = float(nranks * (nranks - 1) // 2)
+        errs = [] if bool((out == want).all()) else [f"rank {rank} ({mode}): {int((out != want).sum())} elements "
+                                                     f"differ from {want}, e.g. {out[:4].tolist()}"]
+        for h in handles:
+            if mode == "window":
+                comm.deregister_window(h)
+            else:
+                comm.deregister_buffer(h)
+        lib.ncclMemFree(send)
+        lib.ncclMemFree(recv)
+        comm.destroy()
+        q.put((rank, errs))
+    except Exception as e:
+        q.put((rank, [f"rank {rank} exception: {e!r}"]))
+
+
+@pytest.mark.parametrize("mode,nranks", [("window", 2), ("window", 4), ("register", 3)])
+def test_reference_examples_symmetric_and_registered(built, mode, nranks):
+    """Known-answer examples of the reference, one process per rank (the MPI examples' layout): the result is
+    exact (small integers in fp32) under any fold order, so it pins the windows / registration paths to
+    the reference's own expected value, not to the oracle."""
+    import queue
+    import time
+    import nccl_amd
+    uid = nccl_amd.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_example_worker, args=(r, nranks, uid, mode, q)) for r in range(nranks)]
+    for p in ps:
+        p.start()
+    results = {}
+    t0 = time.time()
+    while len(results) < nranks and time.time() - t0 < 240:
+        try:
+            r, errs = q.get(timeout=20)
+            results[r] = errs
+        except queue.Empty:
+            if not any(p.is_alive() for p in ps):
+                break
+    for p in ps:
+        if p.is_alive() and len(results) < nranks:
+            p.kill()
+        p.join(timeout=60)
+    assert len(results) == nranks, f"only {len(results)} of {nranks} ranks reported"
+    bad = [e for r in sorted(results) for e in results[r]]
+    assert not bad, "\n".join(bad)

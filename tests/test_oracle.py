@@ -13,7 +13,9 @@ GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 @pytest.mark.parametrize("n", [1, 2, 3, 4, 8])
 def test_kat_allreduce_rank_values(built, n):
-    # docs/examples/03_collectives/01_allreduce/c/main.cc:112-168 and python/allreduce.py:97-116:
+    # docs/examples/03_collectives/01_allreduce/c/main.cc:112-168 and python/allreduce.py:97-116 (also
+    # 04_user_buffer_registration/01_allreduce/c/main.cc:112-166 and 05_symmetric_memory/01_allreduce/c/
+    # main.cc:112-170 with 1M floats; GPU: test_gpu_windows.py::test_reference_examples_symmetric_and_registered):
     # every rank fills its buffer with its rank id; every element of the result is n(n-1)/2.
     count = 32 * 1024
     ins = [np.full(count, float(r), dtype=np.float32) for r in range(n)]
