@@ -554,8 +554,15 @@ def main(argv=None):
     if n > 1:
         spec_peak = (n - 1) * XGMI_LINK_GBPS_DIR
         meas = None
-        if rank == 0 and torch.cuda.device_count() >= n:  # ranks on separate GPUs: a real xGMI measurement
+        # ranks on separate GPUs: a real xGMI measurement, taken while every rank waits at a host barrier
+        # (no peer kernel spinning on its GPU or moving bytes over the links during the probe)
+        probe = torch.cuda.device_count() >= n
+        if probe:
+            barrier()
+        if rank == 0 and probe:
             meas = xgmi_denominator(n)
+        if probe:
+            barrier()
         xg = {"busbw": round(busbw, 1), "unit": "GB/s", "spec_peak": round(spec_peak, 1),
               "spec_frac": round(busbw / spec_peak, 4),
               "spec_basis": f"{n - 1} links x {XGMI_LINK_GBPS_DIR} GB/s per direction (153.6 GB/s spec / 2)"}
