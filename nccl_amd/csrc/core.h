@@ -351,4 +351,15 @@ void groupRecordError(ncclResult_t r);
 ncclResult_t groupDeferColl(const CollInfo& info);
 ncclResult_t groupDeferInit(std::function<ncclResult_t()> job);
 
+// Restores the caller's current device when an API call that switched to its comm's device returns (the
+// reference saves and restores around every launch and registration: enqueue.cc:3137-3162, group.cc:860-863).
+struct DeviceRestore {
+  int dev = -1;
+  DeviceRestore() { (void)hipGetDevice(&dev); }
+  ~DeviceRestore() {
+    int cur = -1;
+    if (dev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != dev) (void)hipSetDevice(dev);
+  }
+};
+
 }  // namespace ncclamd

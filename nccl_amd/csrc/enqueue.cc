@@ -647,6 +647,9 @@ ncclResult_t enqueueCheck(CollInfo* info) {
        (int)info->datatype, (int)info->op, info->root, (void*)info->comm, info->comm->nRanks, (void*)info->stream);
   if (info->count == 0) return ncclSuccess;  // reference enqueue.cc:3024
   if (groupActive()) return groupDeferColl(*info);
+  // the caller's current device survives the call, as in the reference (an eager call is a one-op group
+  // whose launch saves and restores the device: enqueue.cc:3137-3162, group.cc:860-863)
+  DeviceRestore restore;
   return launchColl(*info);
 }
 

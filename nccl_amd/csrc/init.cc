@@ -405,6 +405,7 @@ static void pollAsync(ncclComm* comm) {
 NCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
   NCCLCHECK(commCheck(comm, "ncclCommFinalize", "comm"));
   if (comm->finalized) return ncclInvalidUsage;
+  DeviceRestore restore;
   HIPCHECK(hipSetDevice(comm->device));
   HIPCHECK(hipDeviceSynchronize());
   if (comm->bootstrap) NCCLCHECK(bootstrapBarrier(comm->bootstrap));
@@ -453,6 +454,7 @@ NCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
   if (comm->initThread.joinable()) comm->initThread.join();
   // Kernels poll the abort word inside every bounded spin (reference primitives.h:154-164).
   if (comm->hostAbort) __atomic_store_n(comm->hostAbort, 1u, __ATOMIC_RELEASE);
+  DeviceRestore restore;
   (void)hipSetDevice(comm->device);
   (void)hipDeviceSynchronize();
   commFree(comm);

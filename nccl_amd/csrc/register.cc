@@ -223,6 +223,7 @@ NCCL_EXPORT ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, siz
   // a group task in the reference (dev_runtime.cc:1350-1366): inside a group every rank's registration
   // runs concurrently at ncclGroupEnd, so one thread may register the windows of all its ranks
   if (groupActive()) return groupDeferInit([=]() { return windowRegister(comm, buff, size, win, winFlags); });
+  DeviceRestore restore;
   return windowRegister(comm, buff, size, win, winFlags);
 }
 NCCL_ALIAS(ncclResult_t, ncclCommWindowRegister, ncclComm_t, void*, size_t, ncclWindow_t*, int)
@@ -236,6 +237,7 @@ NCCL_EXPORT ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t 
     return ncclInvalidArgument;
   }
   // collectives enqueued on this window may still run: wait for the device before unmapping peers
+  DeviceRestore restore;
   HIPCHECK(hipSetDevice(comm->device));
   HIPCHECK(hipDeviceSynchronize());
   comm->windows.erase(it);
