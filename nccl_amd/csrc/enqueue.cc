@@ -120,7 +120,7 @@ void loadTuning(CommTuning* t) {
   t->symDisable = (int)paramInt("NCCL_AMD_SYM_DISABLE", 0);
   t->symOneShot = (int)paramInt("NCCL_AMD_SYM_ONESHOT", 0);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
-  t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks)
+  t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks; 2 MiB at 2 ranks)
   t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)
   t->llChannelBytes = paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096);
   if (t->llChannelBytes < 8) t->llChannelBytes = 8;
@@ -360,9 +360,14 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   bool oneShot = false;
   if (info.func == FUNC_ALLREDUCE) {
     // one-shot moves (n-1)S link bytes per rank vs 2(n-1)S/n for the direct path, but saves two
-    // handshakes: the crossover shrinks with n (default 2 MiB / n: 1 MiB at n=2, 256 KiB at n=8)
+    // handshakes: the crossover shrinks with n (default 2 MiB / n: 512 KiB at n=4, 256 KiB at n=8). At n = 2
+    // both move S over the one link and 4S of HBM per rank, so only one-shot's 32-channel cap ends its range:
+    // 2 MiB there (one-GPU rehearsal, fp16: 2 MiB one-shot 14.1 us vs direct 16.0, 4 MiB 23.1 vs 17.7;
+    // profiles/r02_scale_rehearsal_n2_onegpu.json)
     size_t bytes = count * (size_t)ts;
-    size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes : ((size_t)2 << 20) / n;
+    size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes
+                 : n == 2                    ? ((size_t)2 << 20)
+                                             : ((size_t)2 << 20) / n;
     oneShot = comm->tune.algo == FORCE_ONESHOT || (comm->tune.algo == FORCE_NONE && bytes <= lim);
   }
   int tunedNch = 0;

@@ -32,7 +32,7 @@ def plan(exe, n, func, dtype, count, offset=0, chancap=256, **env):
 
 @pytest.mark.parametrize("n,nbytes,algo", [
     (1, 4096, "copy"), (1, 256 << 20, "copy"),
-    (2, 8, "ll"), (2, 64 << 10, "ll"), (2, 128 << 10, "ll"), (2, 256 << 10, "oneshot"), (2, 1 << 20, "oneshot"),
+    (2, 8, "ll"), (2, 64 << 10, "ll"), (2, 128 << 10, "ll"), (2, 256 << 10, "oneshot"), (2, 1 << 20, "oneshot"), (2, 2 << 20, "oneshot"),
     (2, 4 << 20, "direct"), (2, 256 << 20, "direct"),
     (4, 64 << 10, "ll"), (4, 128 << 10, "oneshot"), (4, 512 << 10, "oneshot"), (4, 1 << 20, "direct"),
     (8, 16 << 10, "ll"), (8, 32 << 10, "ll"), (8, 64 << 10, "oneshot"), (8, 256 << 10, "oneshot"),
