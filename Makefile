@@ -22,7 +22,7 @@ DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf plan-test xgmi-probe atomicity-probe
+all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test xgmi-probe atomicity-probe
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -88,6 +88,14 @@ tests/native/nccl_perf: tests/native/nccl_perf.cc include/nccl.h $(LIBDIR)/libnc
 	$(HIPCC) -O2 --offload-arch=$(ARCH) -Iinclude -o $@ $< -L$(LIBDIR) -lnccl -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
 
 .PHONY: nccl-perf
+
+# the reference's communicator-creation examples (pthread per rank, ncclCommInitAll) + a known-answer AllReduce
+comm-examples: tests/native/comm_examples
+
+tests/native/comm_examples: tests/native/comm_examples.cc include/nccl.h $(LIBDIR)/libnccl.so
+	$(HIPCC) -O2 --offload-arch=$(ARCH) -Iinclude -o $@ $< -L$(LIBDIR) -lnccl -lpthread -Wl,-rpath,'$$ORIGIN/../../$(LIBDIR)'
+
+.PHONY: comm-examples
 
 # CU-driven peer bandwidth probe (run by bench.py's suite on multi-GPU nodes)
 xgmi-probe: tests/native/xgmi_probe

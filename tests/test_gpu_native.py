@@ -62,3 +62,18 @@ def test_store_atomicity_probe_one_gpu(built):
     assert rep["reader_waves"] == 64 and rep["line_observations"] > 0
     assert rep["changed"] > 0, "the readers never raced the writer"
     assert rep["torn8"] == 0, rep
+
+
+@pytest.mark.parametrize("mode,n", [("pthread", 2), ("pthread", 4), ("initall", 2), ("initall", 4)])
+def test_reference_communicator_examples(built, mode, n):
+    """The reference's communicator-creation examples as a C program against nccl.h
+    (tests/native/comm_examples.cc: docs/examples/01_communicators/02_one_device_per_pthread and
+    01_multiple_devices_single_process): per-thread ncclCommInitRank on one unique id, or ncclCommInitAll
+    from one thread; rank / count / device queries; a 1M-float AllReduce whose every element must be
+    n(n-1)/2; the caller's current device unchanged by every call; Finalize + Destroy. All ranks on the one GPU."""
+    exe = os.path.join(ROOT, "tests", "native", "comm_examples")
+    if not os.path.exists(exe):
+        subprocess.check_call(["make", "comm-examples"], cwd=ROOT)
+    env = dict(os.environ, NCCL_MULTI_RANK_GPU_ENABLE="1", NCCL_AMD_SPIN_TIMEOUT_MS="20000")
+    out = subprocess.run([exe, mode, str(n)], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.startswith("OK"), out.stdout + out.stderr
