@@ -133,11 +133,15 @@ void tunerUnload(ncclComm* comm) {
 // The engine's cost model (µs, the unit of the reference's tuning table, tuning.cc): a fixed launch +
 // handshake latency plus the busiest resource's time — a rank's link bytes over its n-1 xGMI links
 // (≈50 GB/s per link and direction, ring / chain: over ONE link), or its local HBM bytes at ≈6.3 TB/s
-// (MI355X_MICROARCH.md's measured copy rate), whichever is longer. `bytes` is the collective's size as the
+// (MI355X_MICROARCH.md's measured copy rate), whichever is longer; one-shot runs on at most 32 channels and
+// one channel's workgroup moves ≈50 GB/s (scripts/wg_rate_probe.hip), so its HBM rate is capped
+// at 1.6 TB/s — which puts its n = 2 crossover with direct at ≈2.4 MB, where the one-GPU rehearsal has it
+// (2 MiB one-shot 14.1 µs vs direct 16.0, 4 MiB 23.1 vs 17.7). `bytes` is the collective's size as the
 // tuner sees it (AllReduce / Reduce: the buffer; ReduceScatter / AllGather: n × the per-rank block).
 // Used for the plugin's cost table and by ncclGroupSimulateEnd.
 ModelCost modelCost(ModelAlgo a, CollFunc func, int n, size_t bytes) {
   const double S = (double)bytes, link = 5.0e4 /* B/µs per link */, hbm = 6.3e6 /* B/µs */;
+  const double oneShotHbm = std::min(hbm, 32 * 5.0e4);  // 32 channels x ≈50 GB/s per workgroup
   if (n <= 1) return {2.0, (a == MODEL_COPY ? 2.0 * S : 0.0) / hbm};  // one rank: a copy or nothing
   const double nl = n - 1.0;
   const bool ar = func == FUNC_ALLREDUCE, red = func == FUNC_REDUCE;
@@ -176,7 +180,7 @@ ModelCost modelCost(ModelAlgo a, CollFunc func, int n, size_t bytes) {
       break;
     case MODEL_COPY: break;
   }
-  const double t = std::max(linkB / (links * link), hbmB / hbm);
+  const double t = std::max(linkB / (links * link), hbmB / (a == MODEL_ONESHOT ? oneShotHbm : hbm));
   return {lat, t};
 }
 
