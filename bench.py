@@ -298,7 +298,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     #  default 128 KiB slots at n = 8, 256 KiB with 128 channels)
     for env in ({}, {"NCCL_AMD_SLOT_BYTES": "32768"}, {"NCCL_AMD_SLOT_BYTES": "65536"},
                 {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_AMD_NSLOTS": "4"}, {"NCCL_MAX_CTAS": "128"},
-                {"NCCL_MAX_CTAS": "64"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}, {"NCCL_AMD_AG_PULL": "1"},
+                {"NCCL_MAX_CTAS": "64"}, {"NCCL_MAX_CTAS": "32"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}, {"NCCL_AMD_AG_PULL": "1"},
                 {"NCCL_AMD_RS_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}):
         for k in knobs:
             os.environ.pop(k, None)
