@@ -161,6 +161,7 @@ struct CommTuning {
   int ll128On;              // NCCL_PROTO lists LL128, or NCCL_AMD_LL128=1: the LL64 line protocol (kernels.h)
   int symDisable;           // NCCL_AMD_SYM_DISABLE
   int symOneShot;           // NCCL_AMD_SYM_ONESHOT: caller promises out-of-place window AllReduces
+  int symWtPublish;         // NCCL_AMD_SYM_WT: symmetric kernels publish with write-through stores, no L2 write-back
   int noAggregation;        // NCCL_AMD_NO_AGGREGATION
   int64_t oneShotBytes;     // NCCL_AMD_ONESHOT_BYTES
   int64_t llBytes;          // NCCL_AMD_LL_BYTES

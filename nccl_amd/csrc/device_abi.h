@@ -150,6 +150,7 @@ struct SymArgs {
   uint64_t redArg;
   const void* redArgPtr;
   int aligned;
+  int wtPublish;       // bytes peers read (AR fold result, AG own block) stored write-through: no L2 write-back
 };
 
 __host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int kind, int slot, int from) {

@@ -119,6 +119,7 @@ void loadTuning(CommTuning* t) {
   }
   t->symDisable = (int)paramInt("NCCL_AMD_SYM_DISABLE", 0);
   t->symOneShot = (int)paramInt("NCCL_AMD_SYM_ONESHOT", 0);
+  t->symWtPublish = (int)paramInt("NCCL_AMD_SYM_WT", 0);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
   t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks; 2 MiB at 2 ranks)
   t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)
@@ -458,6 +459,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       bool symAligned = (al & 15) == 0 && !comm->tune.forceElementwise;
       if (info.func != FUNC_ALLREDUCE) symAligned = symAligned && ((count * ts) & 15) == 0;
       sp.args.aligned = symAligned ? 1 : 0;
+      sp.args.wtPublish = comm->tune.symWtPublish;
       size_t spanBytes = blockElems * ts;  // what one channel plan divides
       size_t minPart = (size_t)comm->tune.minChannelBytes;
       int maxCh = comm->chanCap;

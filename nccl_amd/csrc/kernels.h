@@ -1170,6 +1170,7 @@ struct SymShared {
   uint64_t want[NCCL_AMD_MAX_RANKS];
   uint64_t* sigPtr[NCCL_AMD_MAX_RANKS];
   uint64_t sigVal[NCCL_AMD_MAX_RANKS];
+  char* pushPtr[1];
 };
 
 // Every lane i < n (i != me) stores `e` into peer i's flag word [c][kind][me]; REL publishes my prior stores.
@@ -1207,6 +1208,10 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
   }
   const Red<T, OP> fn(opArg);
   const bool aligned = a.aligned != 0;
+  // wtPublish: what peers read from my output (AR: my reduced part; AG: my own block) is stored system-scope
+  // write-through, so nothing of it sits dirty in this XCD's L2 and the signal that publishes it needs no
+  // L2 write-back (buffer_wbl2), only the store drain — as the staged path's pushes
+  const bool wt = a.wtPublish != 0;
   auto blockLen = [&](int q) -> uint64_t {
     if (COLL == SYM_RS || COLL == SYM_AG) return a.chunk;
     uint64_t b = (uint64_t)q * a.chunk;
@@ -1225,9 +1230,12 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     partOf(a.chunk, lo, hi);
     char* dst = a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
     const char* src = a.send[me] + lo * ts;
-    if (dst != src) copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
+    if (dst != src) {
+      if (wt) copyRange<T, true>(dst, src, (hi - lo) * ts, aligned);
+      else copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
+    }
   }
-  symSignal(dc, sh, c, FLG_SYM_ENTER, e, COLL == SYM_AG);  // AG: publishes that block
+  symSignal(dc, sh, c, FLG_SYM_ENTER, e, COLL == SYM_AG && !wt);  // AG: publishes that block
   ok = symWait(dc, sh, c, FLG_SYM_ENTER, e, true);
   if (ok && COLL == SYM_AR1) {
     // one-shot: fold my channel's portion of the whole buffer from all n inputs, owner block by block
@@ -1251,11 +1259,14 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
       for (int k = 0; k < n; k++) sh.srcPtr[k] = a.send[(me + 1 + k) % n] + ((uint64_t)me * a.chunk + lo) * ts;
     __syncthreads();
     char* dst = COLL == SYM_RS ? a.recv[me] + lo * ts : a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
-    foldRange<T, OP>(fn, n, sh.srcPtr, hi - lo, dst, nullptr, 0, aligned);
+    const bool push = COLL == SYM_AR && wt;  // peers read it in the pull phase
+    if (tid == 0) sh.pushPtr[0] = dst;
+    __syncthreads();
+    foldRange<T, OP>(fn, n, sh.srcPtr, hi - lo, push ? nullptr : dst, sh.pushPtr, push ? 1 : 0, aligned);
     __syncthreads();
   }
   if (ok && COLL == SYM_AR) {
-    symSignal(dc, sh, c, FLG_SYM_MID, e, true);  // my reduced part is in my output: publish it
+    symSignal(dc, sh, c, FLG_SYM_MID, e, !wt);  // my reduced part is in my output: publish it
     ok = symWait(dc, sh, c, FLG_SYM_MID, e, true);
   }
   if (ok && (COLL == SYM_AR || COLL == SYM_AG)) {
