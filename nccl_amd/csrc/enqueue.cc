@@ -119,7 +119,9 @@ void loadTuning(CommTuning* t) {
   }
   t->symDisable = (int)paramInt("NCCL_AMD_SYM_DISABLE", 0);
   t->symOneShot = (int)paramInt("NCCL_AMD_SYM_ONESHOT", 0);
-  t->symWtPublish = (int)paramInt("NCCL_AMD_SYM_WT", 0);
+  // write-through publish in the symmetric kernels: n = 2 one-GPU rehearsal 0.291-0.295 -> 0.234-0.241 ms at
+  // 256 MiB fp32 (no per-channel L2 write-back; profiles/r02_sym_wt_ab_onegpu.txt)
+  t->symWtPublish = (int)paramInt("NCCL_AMD_SYM_WT", 1);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
   t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks; 2 MiB at 2 ranks)
   t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)

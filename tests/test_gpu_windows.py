@@ -120,13 +120,16 @@ def _windows(comms, streams_dev=0):
     return bufs, wins
 
 
-@pytest.mark.parametrize("nranks,oneshot", [(2, False), (3, False), (2, True)])
-def test_windows_single_process(built, nranks, oneshot, monkeypatch):
+@pytest.mark.parametrize("nranks,oneshot,wt", [(2, False, 1), (3, False, 1), (2, True, 1), (2, False, 0), (3, False, 0)])
+def test_windows_single_process(built, nranks, oneshot, wt, monkeypatch):
     import torch
     import nccl_amd
     os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
     if oneshot:  # the one-shot window kernel: a rank-uniform promise that every AllReduce is out of place
         monkeypatch.setenv("NCCL_AMD_SYM_ONESHOT", "1")
+    # wt=0: the nontemporal-store publish with an L2 write-back release (NCCL_AMD_SYM_WT=0) instead of the
+    # default write-through publish
+    monkeypatch.setenv("NCCL_AMD_SYM_WT", str(wt))
     torch.cuda.set_device(0)
     comms = nccl_amd.Communicator.init_all([0] * nranks)
     streams = [torch.cuda.Stream() for _ in range(nranks)]
