@@ -1222,6 +1222,7 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     hi = min(lo + a.part, len);
   };
   bool ok;
+  bool agRel = false;  // AG: publish my block with an L2 write-back (no write-through copy of it was made)
   if (COLL == SYM_AG) {
     // AllGather: my own block goes into my output BEFORE entry (skipped in place), so every peer pulls block
     // q from rank q's output. No rank needs to know whether a peer runs in place or out of place (ranks may
@@ -1234,8 +1235,10 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
       if (wt) copyRange<T, true>(dst, src, (hi - lo) * ts, aligned);
       else copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
     }
+    // in place, the block was written by the caller's earlier kernels: keep the write-back release for it
+    agRel = !wt || dst == src;
   }
-  symSignal(dc, sh, c, FLG_SYM_ENTER, e, COLL == SYM_AG && !wt);  // AG: publishes that block
+  symSignal(dc, sh, c, FLG_SYM_ENTER, e, agRel);  // AG: publishes that block
   ok = symWait(dc, sh, c, FLG_SYM_ENTER, e, true);
   if (ok && COLL == SYM_AR1) {
     // one-shot: fold my channel's portion of the whole buffer from all n inputs, owner block by block
