@@ -18,7 +18,7 @@ from tests import gpu_cases as G  # noqa: E402
 
 KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_AG_PULL",
          "NCCL_AMD_RS_PULL", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_LL_CHANNEL_BYTES", "NCCL_AMD_LL128",
-         "NCCL_AMD_LL128_CHANNEL_BYTES")
+         "NCCL_AMD_LL128_CHANNEL_BYTES", "NCCL_AMD_SYM_WT")
 
 
 def settings(rng):
@@ -45,7 +45,43 @@ def settings(rng):
         env["NCCL_AMD_LL128"] = "1"
     if rng.random() < 0.2:
         env["NCCL_AMD_LL128_CHANNEL_BYTES"] = str(rng.choice([56, 512, 16384]))
+    if rng.random() < 0.3:
+        env["NCCL_AMD_SYM_WT"] = "0"  # the symmetric kernels' write-back publish instead of write-through
     return env
+
+
+def run_window_cases(cs, rng, k):
+    """k random cases with every buffer inside NCCL_WIN_COLL_SYMMETRIC windows at the same offsets on every
+    rank (the symmetric kernels; Reduce and LL-sized ops take their usual paths), checked bit-exact."""
+    import numpy as np
+    import oracle
+    from tests import test_gpu_windows as W
+    n = len(cs)
+    bufs, wins = W._windows([c for c, _ in cs])
+    bases = [(b, b.data_ptr()) for b in bufs]
+    errs, done = [], 0
+    for _ in range(k):
+        coll = rng.choice(["allreduce", "allreduce", "reducescatter", "allgather", "reduce"])
+        dt = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+        op = 0 if coll == "allgather" else rng.choice([0, 1, 2, 3, 4])
+        es = np.dtype(oracle.NP_STORAGE[dt]).itemsize
+        off = rng.choice([0, 0, 0, 1, 3])
+        inplace = off == 0 and rng.random() < 0.3
+        span = (W.HALF - 64) // es  # elements one half of the window holds past the offset
+        count = rng.choice([1, 7, 16, 1000, 4099, 65_536, 100_003, 300_001])
+        if coll in ("reducescatter", "allgather"):
+            count = min(count, span // n)
+            count = max(1, count // n) * n if coll == "reducescatter" else max(1, count)
+        count = min(count, span)
+        root = rng.randrange(n)
+        e = W._run(cs, bases, coll, dt, op, count, off, inplace, seed=rng.randrange(1 << 30), root=root)
+        done += 1
+        if e:
+            errs.append(f"window {coll} dt={dt} op={op} count={count} off={off} inplace={inplace} root={root}: {e[:3]}")
+            break
+    for (c, _), w in zip(cs, wins):
+        c.deregister_window(w)
+    return errs, done
 
 
 def run_group(cs, ops, rng):
@@ -107,7 +143,13 @@ def main():
         streams = [torch.cuda.Stream() for _ in range(n)]
         cs = list(zip(comms, streams))
         done = 0
-        for _ in range(rng.randint(4, 12)):
+        if rng.random() < 0.25:  # symmetric windows for this communicator
+            errs, k = run_window_cases(cs, rng, rng.randint(4, 12))
+            total += k
+            done += k
+            if errs:
+                failures.append(f"n={n} env={env} {errs[0]}")
+        for _ in range(0 if failures else rng.randint(4, 12)):
             if rng.random() < 0.2:  # a group of several ops: LL batches between other collectives
                 dt = rng.choice([2, 6, 7, 9])
                 op = rng.choice([0, 2, 3])
