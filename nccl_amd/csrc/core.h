@@ -118,6 +118,12 @@ ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d);  // se
 ncclResult_t ipcFetchFd(const IpcDesc& d, int* fd);  // an exporter's fd for d, over its fd server (bounded)
 ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out);
 void ipcRelease(IpcImport* m);
+// Registered buffers (register.cc): ask the fd server `server` (a peer's) to map the dma-buf `fd` (sent along,
+// the caller keeps its copy) on its device on behalf of `rank`, remembered under `tag`; *addr = where it
+// landed in the peer's process. Release drops that mapping (best effort: a peer already gone released it).
+ncclResult_t ipcRemoteImport(const char* server, int rank, uint64_t tag, int fd, uint64_t size, uint64_t* addr);
+void ipcRemoteRelease(const char* server, int rank, uint64_t tag);
+uint64_t ipcNewTag();
 
 struct PeerInfo {  // exchanged once at init (reference: struct ncclPeerInfo, src/init.cc:1035-1037)
   int rank;
@@ -149,19 +155,41 @@ struct IpcMapping {
   int refs;
 };
 
+// One registered allocation (reference struct ncclReg, src/include/register.h; src/register/register.cc): the
+// whole allocation holding a registered buffer, mapped once into every peer's process (a peer's fd server
+// imports it on request, ipc.cc) and refcounted by the ncclCommRegister handles (local) and the stream-capture
+// auto-registrations (graph, NCCL_GRAPH_REGISTER) that lie in it.
+struct RegAlloc {
+  uint64_t base, size;
+  uint64_t bufferId;   // the runtime's allocation id: a freed and re-allocated range is detected, never reused
+  uint64_t tag;        // name of this registration at the peers' fd servers
+  uint64_t rmt[NCCL_AMD_MAX_RANKS];  // the allocation's base as mapped in rank r's process (mine: base)
+  bool imported[NCCL_AMD_MAX_RANKS]; // mapped by rank r's fd server (released by an RPC at deregistration)
+  bool usable;         // every peer maps it: collectives on it may run zero-copy
+  int localRefs, graphRefs;
+};
+struct RegHandle {  // what ncclCommRegister returns
+  void* buff;
+  size_t size;
+  RegAlloc* ra;  // nullptr when registration is disabled (NCCL_LOCAL_REGISTER=0)
+};
+
 // Hot-path tuning knobs, read ONCE at communicator init (reference NCCL_PARAM caches its env reads,
 // include/param.h:21-31) and agreed across ranks (rank 0's values win), so every rank takes the same
 // algorithm/protocol decision and no getenv() runs per collective.
 struct CommTuning {
   int checkPointers;        // NCCL_CHECK_POINTERS
   int forceElementwise;     // NCCL_AMD_FORCE_ELEMENTWISE (diagnostics)
-  int protoFlags;           // NCCL_AMD_PROTO_FLAGS | (NCCL_AMD_P2P_FENCE=0 ? 8 : 0)
+  int protoFlags;           // NCCL_AMD_PROTO_FLAGS | (no release fence before data flags ? 8 : 0) | pulls
+  int p2pFence;             // NCCL_AMD_P2P_FENCE: 1 fence, 0 none, -1 unset (none iff all ranks share one GPU)
   int algo;                 // NCCL_ALGO: TuneAlgoForce (ONESHOT, DIRECT, RING, TREE)
   int llOn, simpleOn;       // NCCL_PROTO
   int ll128On;              // NCCL_PROTO lists LL128, or NCCL_AMD_LL128=1: the LL64 line protocol (kernels.h)
   int symDisable;           // NCCL_AMD_SYM_DISABLE
   int symOneShot;           // NCCL_AMD_SYM_ONESHOT: caller promises out-of-place window AllReduces
   int symWtPublish;         // NCCL_AMD_SYM_WT: symmetric kernels publish with write-through stores, no L2 write-back
+  int localRegister;        // NCCL_LOCAL_REGISTER: ncclCommRegister maps buffers into peers (zero-copy collectives)
+  int graphRegister;        // NCCL_GRAPH_REGISTER: buffers of captured collectives are registered automatically
   int noAggregation;        // NCCL_AMD_NO_AGGREGATION
   int64_t oneShotBytes;     // NCCL_AMD_ONESHOT_BYTES
   int64_t llBytes;          // NCCL_AMD_LL_BYTES
@@ -174,6 +202,7 @@ struct CommTuning {
   int64_t copyGrid;         // NCCL_AMD_COPY_GRID (cap on its workgroups; default: one per 16 KiB tile)
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
+void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known
 
 struct ncclCommImpl;
 }  // namespace ncclamd
@@ -233,7 +262,8 @@ struct ncclComm {
   std::shared_ptr<ncclamd::LocalClique> clique;  // ncclCommInitAll comms: in-process all-gather
   std::vector<ncclWindow_vidmem*> windows;        // registered windows (register.cc)
   std::vector<ncclamd::IpcMapping> ipcMaps;
-  std::vector<void*> regHandles;                   // ncclCommRegister handles
+  std::vector<ncclamd::RegHandle*> regHandles;     // ncclCommRegister handles
+  std::vector<ncclamd::RegAlloc*> regs;            // registered allocations (register.cc)
 
   std::vector<ncclamd::UserRedOp> userOps;
   std::atomic<int> asyncResult{ncclSuccess};
@@ -337,6 +367,12 @@ bool batchable(const std::vector<PlannedColl>& run, const PlannedColl& b);  // c
 ncclResult_t launchBatch(std::vector<PlannedColl>& run);  // one launch for a run of batchable ops
 // window lookup: the window holding [p, p+bytes) with NCCL_WIN_COLL_SYMMETRIC, or nullptr (register.cc)
 ncclWindow_vidmem* findSymWindow(ncclComm* comm, const void* p, size_t bytes);
+// Registered buffers of one collective (register.cc): true when [send, +sendBytes) (skipped when send is
+// nullptr) and [recv, +recvBytes) lie in allocations every peer maps — registered with ncclCommRegister, or,
+// under stream capture with NCCL_GRAPH_REGISTER=1, registered here on the fly. rmtSend[r] / rmtRecv[r] = the
+// buffers as mapped in rank r's process (mine: the buffers themselves).
+bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
+               size_t recvBytes, const char** rmtSend, char** rmtRecv);
 void windowsFree(ncclComm* comm);  // release every window and IPC mapping (destroy/abort)
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
 ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);

@@ -13,6 +13,8 @@
 //       AG_READY / AG_ACK  = the same for the all-gather direction
 //       SYM_ENTER / SYM_MID / SYM_DONE[c][from] = epoch of the last symmetric (window) collective in
 //                          which `from` entered / published its reduced block / finished reading peers
+//       REG_SEND / REG_RECV[c][from] = `from`'s registered send / recv buffer as mapped in MY address space,
+//                          stored before its SYM_ENTER (zero-copy collectives on ncclCommRegister buffers)
 //     A word is written by exactly one remote rank and polled only by its owner.
 //
 //   LL lines (same uncached allocation as the flags, at DevComm::llOffset; reference prims_ll.h:108-158)
@@ -42,9 +44,13 @@ enum StagingKind { STG_RS = 0, STG_AG = 1, STG_KINDS = 2 };
 // FLG_PULL_READY / FLG_PULL_ACK and CTR_PULL_PUB / CTR_PULL_GOT: the AG-pull gather (kernels.h
 // Channel::agPull) publishes ONE copy per step that every peer reads, so it keeps its own sequence (the
 // per-pair AG counters diverge once a Reduce has pushed to its root only).
+// FLG_REG_SEND / FLG_REG_RECV: the device-side pointer exchange of registered (ncclCommRegister) buffers —
+// before its ENTER signal, rank `from` stores its send / recv buffer AS MAPPED IN THIS PROCESS into these
+// words of the same channel (reference: the ptrExchange slots of prims_simple.h:748-846).
 enum FlagKind {
   FLG_RS_READY = 0, FLG_RS_ACK = 1, FLG_AG_READY = 2, FLG_AG_ACK = 3,
-  FLG_SYM_ENTER = 4, FLG_SYM_MID = 5, FLG_SYM_DONE = 6, FLG_PULL_READY = 7, FLG_PULL_ACK = 8, FLG_KINDS = 9
+  FLG_SYM_ENTER = 4, FLG_SYM_MID = 5, FLG_SYM_DONE = 6, FLG_PULL_READY = 7, FLG_PULL_ACK = 8,
+  FLG_REG_SEND = 9, FLG_REG_RECV = 10, FLG_KINDS = 11
 };
 enum CtrKind {
   CTR_SEND_RS = 0, CTR_RECV_RS = 1, CTR_SEND_AG = 2, CTR_RECV_AG = 3, CTR_SYM = 4, CTR_LL = 5,
@@ -140,10 +146,16 @@ using LLBatchArgs = LLArgs<kMaxLLBatch>;
 
 // Symmetric (window) collective arguments: every rank's buffers as mapped in this process (reference
 // ncclSymPtr::peerPtr, src/device/symmetric/kernel.cuh), so peers are read and written directly.
+// regMode (buffers registered with ncclCommRegister, reference src/register/coll_reg.cc:326-395): the host
+// knows only where ITS OWN buffers are mapped in every peer, so send[r] / recv[r] (r != rank) hold MY buffers
+// as mapped in rank r; the kernel hands them to rank r through r's FLG_REG_SEND / FLG_REG_RECV words and reads
+// the peers' buffers from its own words after the ENTER handshake (the reference's ptrExchange,
+// prims_simple.h:748-846). `aligned` then carries only the count condition: pointer alignment of every
+// rank's buffers is decided in the kernel, from the exchanged pointers, identically on every rank.
 struct SymArgs {
   const DevComm* comm;
-  const char* send[NCCL_AMD_MAX_RANKS];  // rank r's sendbuff
-  char* recv[NCCL_AMD_MAX_RANKS];        // rank r's recvbuff
+  const char* send[NCCL_AMD_MAX_RANKS];  // rank r's sendbuff (regMode: my sendbuff as mapped in rank r)
+  char* recv[NCCL_AMD_MAX_RANKS];        // rank r's recvbuff (regMode: my recvbuff as mapped in rank r)
   uint64_t count;      // AR: elements; RS: recvcount; AG: sendcount
   uint64_t chunk;      // elements per rank block
   uint64_t part;       // elements per channel (AR two-shot / RS / AG: within a block; one-shot: of the buffer)
@@ -151,6 +163,8 @@ struct SymArgs {
   const void* redArgPtr;
   int aligned;
   int wtPublish;       // bytes peers read (AR fold result, AG own block) stored write-through: no L2 write-back
+  int regMode;         // buffers registered with ncclCommRegister: device-side pointer exchange (above)
+  int relFence;        // publish with a system release fence even after write-through stores (across devices)
 };
 
 __host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int kind, int slot, int from) {

@@ -80,9 +80,13 @@ void loadTuning(CommTuning* t) {
   memset(t, 0, sizeof(*t));
   t->checkPointers = (int)paramInt("NCCL_CHECK_POINTERS", 0);
   t->forceElementwise = (int)paramInt("NCCL_AMD_FORCE_ELEMENTWISE", 0);
-  // no release fence before data flags by default: every byte a peer reads from this rank's writes is a
-  // write-through system-scope store, drained before the flag store
-  t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (paramInt("NCCL_AMD_P2P_FENCE", 0) ? 0 : 8) |
+  // Release fence (buffer_wbl2) before data flags: NCCL_AMD_P2P_FENCE=1 keeps it, =0 drops it (every byte a
+  // peer reads from this rank's writes is a write-through system-scope store, drained before the flag store,
+  // DESIGN.md §4). Unset (-1): dropped only when every rank shares one GPU, where that ordering has been
+  // tested; kept across devices until a multi-GPU run shows the drain suffices over xGMI.
+  // Resolved by resolveFence() once the peer table is known.
+  t->p2pFence = (int)paramInt("NCCL_AMD_P2P_FENCE", -1);
+  t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (t->p2pFence == 0 ? 8 : 0) |
                   (paramInt("NCCL_AMD_AG_PULL", 0) ? 16 : 0) | (paramInt("NCCL_AMD_RS_PULL", 0) ? 32 : 0);
   if (const char* algo = paramStr("NCCL_ALGO")) {
     if (!strcasecmp(algo, "ONESHOT")) t->algo = FORCE_ONESHOT;
@@ -122,6 +126,10 @@ void loadTuning(CommTuning* t) {
   // write-through publish in the symmetric kernels: n = 2 one-GPU rehearsal 0.291-0.295 -> 0.234-0.241 ms at
   // 256 MiB fp32 (no per-channel L2 write-back; profiles/r02_sym_wt_ab_onegpu.txt)
   t->symWtPublish = (int)paramInt("NCCL_AMD_SYM_WT", 1);
+  // reference register.cc:16 / enqueue.cc:283 (both default on): ncclCommRegister'd buffers and, under stream
+  // capture, the captured collectives' buffers run the zero-copy kernel (register.cc)
+  t->localRegister = (int)paramInt("NCCL_LOCAL_REGISTER", 1);
+  t->graphRegister = (int)paramInt("NCCL_GRAPH_REGISTER", 1);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
   t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks; 2 MiB at 2 ranks)
   t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)
@@ -136,6 +144,11 @@ void loadTuning(CommTuning* t) {
   t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
   t->copyVariant = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
   t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);
+}
+
+// The fence default once the ranks' devices are known (all ranks see the same peer table and rank 0's knobs).
+void resolveFence(CommTuning* t, bool oneDevice) {
+  if (t->p2pFence < 0 && oneDevice) t->protoFlags |= 8;
 }
 
 // Pointer check (reference argcheck.cc:12-28), active with NCCL_CHECK_POINTERS=1.
@@ -354,12 +367,13 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   if (info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER) aligned = aligned && ((count * ts) & 15) == 0;
   if (comm->tune.forceElementwise) aligned = false;  // diagnostics: T-sized accesses only
   p.args.aligned = aligned ? 1 : 0;
-  // NCCL_AMD_P2P_FENCE=1 puts a system release fence (buffer_wbl2) back before data flags; the default
-  // omits it: all published bytes are already stored write-through at system scope and drained (§4).
+  // protoFlags bit 8 = no system release fence (buffer_wbl2) before data flags: all published bytes are
+  // stored write-through at system scope and drained (§4); set when every rank shares one GPU or with
+  // NCCL_AMD_P2P_FENCE=0 (resolveFence).
   p.args.protoFlags = comm->tune.protoFlags;
   // Algorithm choice (reference: NCCL_ALGO / tuning.cc cost model): one-shot for small AllReduce
-  // (latency: one handshake), direct scatter-reduce-gather otherwise (bandwidth). NCCL_ALGO may force
-  // either: ONESHOT or DIRECT (the reference's RING/TREE names map to DIRECT).
+  // (latency: one handshake), direct scatter-reduce-gather otherwise (bandwidth). NCCL_ALGO=ONESHOT or
+  // DIRECT forces either; the reference's RING and TREE run their own kernels (pipe.h, below).
   bool oneShot = false;
   if (info.func == FUNC_ALLREDUCE) {
     // one-shot moves (n-1)S link bytes per rank vs 2(n-1)S/n for the direct path, but saves two
@@ -430,16 +444,34 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       return ncclSuccess;
     }
   }
-  // Symmetric windows (reference: symmetric kernels for buffers in NCCL_WIN_COLL_SYMMETRIC windows,
-  // src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*): zero-copy pull kernels.
+  // Zero-copy kernels (kernels.h symKernel): buffers in NCCL_WIN_COLL_SYMMETRIC windows (reference: symmetric
+  // kernels, src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*), or registered with ncclCommRegister /
+  // auto-registered under stream capture (reference: IPC-registered ring buffers, src/register/coll_reg.cc:
+  // 326-395). Reduce keeps the staged path.
   if (info.func != FUNC_REDUCE && !comm->tune.symDisable) {
     size_t sb = count * ts, rb = count * ts;
     if (info.func == FUNC_REDUCESCATTER) sb *= n;
     if (info.func == FUNC_ALLGATHER) rb *= n;
+    const char* sendPtr[NCCL_AMD_MAX_RANKS] = {};
+    char* recvPtr[NCCL_AMD_MAX_RANKS] = {};
+    int regMode = -1;
     // AllGather reads only peers' outputs (symKernel SYM_AG), so its sendbuff needs no window
     ncclWindow_vidmem* ws = info.func == FUNC_ALLGATHER ? nullptr : findSymWindow(comm, info.sendbuff, sb);
     ncclWindow_vidmem* wr = (ws || info.func == FUNC_ALLGATHER) ? findSymWindow(comm, info.recvbuff, rb) : nullptr;
     if (wr && (ws || info.func == FUNC_ALLGATHER)) {
+      regMode = 0;
+      for (int r = 0; r < n; r++) {
+        // AllGather: only my own input is read (peers' blocks come from their outputs)
+        if (ws) sendPtr[r] = ws->peerPtr[r] + ((const char*)info.sendbuff - (const char*)ws->userPtr);
+        else sendPtr[r] = r == comm->rank ? (const char*)info.sendbuff : nullptr;
+        recvPtr[r] = wr->peerPtr[r] + ((char*)info.recvbuff - (char*)wr->userPtr);
+      }
+    } else if (regLookup(comm, info.stream, info.func == FUNC_ALLGATHER ? nullptr : info.sendbuff, sb,
+                         info.recvbuff, rb, sendPtr, recvPtr)) {
+      regMode = 1;  // my buffers as mapped in each peer; the kernel exchanges them at entry
+      if (info.func == FUNC_ALLGATHER) sendPtr[comm->rank] = (const char*)info.sendbuff;
+    }
+    if (regMode >= 0) {
       *kind = PLAN_SYM;
       memset(&sp, 0, sizeof(sp));
       sp.datatype = info.datatype;
@@ -450,18 +482,19 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       sp.args.chunk = blockElems;
       sp.args.redArg = p.args.redArg;
       sp.args.redArgPtr = p.args.redArgPtr;
+      sp.args.regMode = regMode;
       uintptr_t al = 0;
       for (int r = 0; r < n; r++) {
-        // AllGather: only my own input is read (peers' blocks come from their outputs)
-        if (ws) sp.args.send[r] = ws->peerPtr[r] + ((const char*)info.sendbuff - (const char*)ws->userPtr);
-        else sp.args.send[r] = r == comm->rank ? (const char*)info.sendbuff : nullptr;
-        sp.args.recv[r] = wr->peerPtr[r] + ((char*)info.recvbuff - (char*)wr->userPtr);
-        al |= (uintptr_t)sp.args.send[r] | (uintptr_t)sp.args.recv[r];
+        sp.args.send[r] = sendPtr[r];
+        sp.args.recv[r] = recvPtr[r];
+        al |= (uintptr_t)sendPtr[r] | (uintptr_t)recvPtr[r];
       }
-      bool symAligned = (al & 15) == 0 && !comm->tune.forceElementwise;
+      // registered buffers: peers' pointers are known only in the kernel, which adds their alignment
+      bool symAligned = (regMode || (al & 15) == 0) && !comm->tune.forceElementwise;
       if (info.func != FUNC_ALLREDUCE) symAligned = symAligned && ((count * ts) & 15) == 0;
       sp.args.aligned = symAligned ? 1 : 0;
       sp.args.wtPublish = comm->tune.symWtPublish;
+      sp.args.relFence = (comm->tune.protoFlags & 8) == 0;  // across devices: release fence kept (resolveFence)
       size_t spanBytes = blockElems * ts;  // what one channel plan divides
       size_t minPart = (size_t)comm->tune.minChannelBytes;
       int maxCh = comm->chanCap;
@@ -495,8 +528,8 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       sp.args.part = part;
       sp.nChannels = nch;
       sp.stream = info.stream;
-      TRACE("%s: symmetric coll %d nch %d part %lu aligned %d", info.opName, sp.coll, nch, (unsigned long)part,
-            sp.args.aligned);
+      TRACE("%s: %s coll %d nch %d part %lu aligned %d", info.opName, regMode ? "registered zero-copy" : "symmetric",
+            sp.coll, nch, (unsigned long)part, sp.args.aligned);
       return ncclSuccess;
     }
   }

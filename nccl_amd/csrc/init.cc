@@ -148,6 +148,9 @@ static void computeChannelCap(ncclComm* c) {
   int cap = 2 * minCU / maxPer;
   if (cap < 1) cap = 1;
   c->chanCap = cap < c->maxChannels ? cap : c->maxChannels;
+  bool oneDevice = true;
+  for (size_t i = 1; i < c->peers.size(); i++) oneDevice = oneDevice && !strcmp(c->peers[i].busId, c->peers[0].busId);
+  resolveFence(&c->tune, oneDevice);
 }
 
 // Shape parameters every rank must agree on (exchanged with the PeerInfo block).

@@ -43,12 +43,44 @@ struct FdServer {
   std::mutex mu;
   std::map<uint64_t, int> table;  // key -> exported dma-buf fd
   char name[40] = {};  // fits IpcDesc::server
+  int device = 0;      // the communicator's GPU: peers' registered buffers are mapped onto it
+  // Peers' registered buffers mapped in this process on their behalf (IMPORT requests; reference: the peer's
+  // proxy thread maps a registered buffer for ncclIpcLocalRegisterBuffer, src/transport/p2p.cc ipcRegister):
+  // (registering rank, its registration tag) -> mapping. Touched only by the server thread.
+  std::map<std::pair<int, uint64_t>, IpcImport> imports;
+};
+
+// Requests on the fd server's socket (one per connection). FETCH: hand over the fd published under `key`.
+// IMPORT: map the dma-buf fd attached to the request (SCM_RIGHTS) on this comm's device on behalf of rank
+// `from`, remember it under (from, key) and answer the address it got here. RELEASE: drop that mapping.
+enum IpcOp : uint32_t { IPC_FETCH = 1, IPC_IMPORT = 2, IPC_RELEASE = 3 };
+struct IpcRequest {
+  uint32_t op;
+  int32_t from;
+  uint64_t key;
+  uint64_t size;
+};
+struct IpcReply {
+  int32_t status;  // 0 = ok
+  int32_t pad;
+  uint64_t value;  // IMPORT: the mapped address in the server's process
 };
 
 static std::atomic<uint64_t> gServerSerial{0};
 static std::atomic<uint64_t> gKeySerial{1};
 
 static int64_t ipcTimeoutMs() { return paramInt("NCCL_AMD_IPC_TIMEOUT_MS", 60000); }
+
+static uint32_t randomNonce() {
+  uint32_t v = 0;
+  int fd = open("/dev/urandom", O_RDONLY | O_CLOEXEC);
+  if (fd >= 0) {
+    if (read(fd, &v, sizeof(v)) != (ssize_t)sizeof(v)) v = 0;
+    close(fd);
+  }
+  if (v == 0) v = (uint32_t)std::chrono::steady_clock::now().time_since_epoch().count() ^ (uint32_t)getpid() * 2654435761u;
+  return v;
+}
 
 bool ipcLegacy() {
   const char* m = paramStr("NCCL_AMD_IPC");
@@ -70,26 +102,26 @@ static void setTimeouts(int fd) {
   setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof(tv));
 }
 
-// One request per connection: the client sends an 8-byte key; the server answers {status, 0} with the
-// fd attached (SCM_RIGHTS) when the key is published and the client runs under our uid.
-static void serveOne(FdServer* s, int c) {
-  setTimeouts(c);
-  struct ucred cred;
-  socklen_t cl = sizeof(cred);
-  uint64_t key = 0;
-  int32_t reply[2] = {-1, 0};
-  int fd = -1;
-  if (getsockopt(c, SOL_SOCKET, SO_PEERCRED, &cred, &cl) == 0 && cred.uid == getuid() &&
-      recv(c, &key, sizeof(key), MSG_WAITALL) == (ssize_t)sizeof(key)) {
-    std::lock_guard<std::mutex> g(s->mu);
-    auto it = s->table.find(key);
-    if (it != s->table.end()) {
-      fd = it->second;
-      reply[0] = 0;
-    }
-  }
+static ncclResult_t importFd(int fd, uint64_t size, IpcImport* out);
+
+static int recvWithFd(int c, void* buf, size_t len, int* fd) {
   struct msghdr m = {};
-  struct iovec io = {reply, sizeof(reply)};
+  struct iovec io = {buf, len};
+  m.msg_iov = &io;
+  m.msg_iovlen = 1;
+  char ctl[CMSG_SPACE(sizeof(int))] = {};
+  m.msg_control = ctl;
+  m.msg_controllen = sizeof(ctl);
+  *fd = -1;
+  ssize_t got = recvmsg(c, &m, MSG_WAITALL | MSG_CMSG_CLOEXEC);
+  for (struct cmsghdr* h = CMSG_FIRSTHDR(&m); h; h = CMSG_NXTHDR(&m, h))
+    if (h->cmsg_level == SOL_SOCKET && h->cmsg_type == SCM_RIGHTS) memcpy(fd, CMSG_DATA(h), sizeof(int));
+  return got == (ssize_t)len ? 0 : -1;
+}
+
+static int sendWithFd(int c, const void* buf, size_t len, int fd) {
+  struct msghdr m = {};
+  struct iovec io = {const_cast<void*>(buf), len};
   m.msg_iov = &io;
   m.msg_iovlen = 1;
   char ctl[CMSG_SPACE(sizeof(int))] = {};
@@ -102,11 +134,63 @@ static void serveOne(FdServer* s, int c) {
     h->cmsg_len = CMSG_LEN(sizeof(int));
     memcpy(CMSG_DATA(h), &fd, sizeof(int));
   }
-  (void)sendmsg(c, &m, MSG_NOSIGNAL);
+  return sendmsg(c, &m, MSG_NOSIGNAL) == (ssize_t)len ? 0 : -1;
+}
+
+// One request per connection, from a process of our uid only (SO_PEERCRED).
+static void serveOne(FdServer* s, int c) {
+  setTimeouts(c);
+  struct ucred cred;
+  socklen_t cl = sizeof(cred);
+  IpcRequest q = {};
+  IpcReply reply = {-1, 0, 0};
+  int inFd = -1, outFd = -1;
+  if (getsockopt(c, SOL_SOCKET, SO_PEERCRED, &cred, &cl) != 0 || cred.uid != getuid() ||
+      recvWithFd(c, &q, sizeof(q), &inFd) != 0) {
+    if (inFd >= 0) close(inFd);
+    close(c);
+    return;
+  }
+  if (q.op == IPC_FETCH) {
+    std::lock_guard<std::mutex> g(s->mu);
+    auto it = s->table.find(q.key);
+    if (it != s->table.end()) {
+      outFd = it->second;
+      reply.status = 0;
+    }
+  } else if (q.op == IPC_IMPORT && inFd >= 0) {
+    IpcImport m;
+    if (hipSetDevice(s->device) == hipSuccess && importFd(inFd, q.size, &m) == ncclSuccess) {
+      inFd = -1;  // owned by the mapping now
+      auto key = std::make_pair((int)q.from, q.key);
+      auto old = s->imports.find(key);
+      if (old != s->imports.end()) ipcRelease(&old->second);  // a re-registration replaces its mapping
+      s->imports[key] = m;
+      reply.status = 0;
+      reply.value = (uint64_t)m.ptr;
+    } else {
+      (void)hipGetLastError();
+    }
+  } else if (q.op == IPC_RELEASE) {
+    auto it = s->imports.find(std::make_pair((int)q.from, q.key));
+    if (it != s->imports.end()) {
+      (void)hipSetDevice(s->device);
+      ipcRelease(&it->second);
+      s->imports.erase(it);
+    }
+    reply.status = 0;
+  }
+  if (inFd >= 0) close(inFd);
+  (void)sendWithFd(c, &reply, sizeof(reply), outFd);
   close(c);
 }
 
 static void serverLoop(FdServer* s) {
+  // The server maps peers' registered buffers while this process may be capturing a graph on another thread
+  // (NCCL_GRAPH_REGISTER: every rank registers inside its capture): relaxed capture mode keeps this thread's
+  // runtime calls out of such a global-mode capture (the reference's proxy thread does the same)
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
   while (true) {
     struct pollfd p[2] = {{s->listenFd, POLLIN, 0}, {s->wakePipe[0], POLLIN, 0}};
     int r = poll(p, 2, -1);
@@ -122,7 +206,11 @@ static void serverLoop(FdServer* s) {
 ncclResult_t ipcServerStart(ncclComm* comm) {
   if (comm->fdServer || ipcLegacy()) return ncclSuccess;
   FdServer* s = new FdServer();
-  snprintf(s->name, sizeof(s->name), "ncclamd.%d.%llu", (int)getpid(), (unsigned long long)gServerSerial++);
+  s->device = comm->device;
+  // pid + a per-process serial + a random nonce: processes of other PID namespaces sharing this network
+  // namespace (containers with host networking) may reuse our pid, and the abstract namespace is per netns
+  snprintf(s->name, sizeof(s->name), "ncclamd.%d.%llu.%08x", (int)getpid(), (unsigned long long)gServerSerial++,
+           (unsigned)randomNonce());
   s->listenFd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
   struct sockaddr_un a;
   socklen_t al = abstractAddr(s->name, &a);
@@ -145,6 +233,8 @@ void ipcServerStop(ncclComm* comm) {
   if (s->wakePipe[1] >= 0) (void)!write(s->wakePipe[1], "x", 1);
   if (s->thread.joinable()) s->thread.join();
   for (auto& kv : s->table) close(kv.second);
+  if (!s->imports.empty()) (void)hipSetDevice(comm->device);
+  for (auto& kv : s->imports) ipcRelease(&kv.second);  // peers' registrations still mapped here
   close(s->listenFd);
   close(s->wakePipe[0]);
   close(s->wakePipe[1]);
@@ -220,47 +310,77 @@ void ipcUnexport(ncclComm* comm, const IpcDesc& d) {
   s->table.erase(it);
 }
 
-ncclResult_t ipcFetchFd(const IpcDesc& d, int* out) {
+// Connect to the fd server named `server` (retrying until the IPC timeout: the peer may still be starting).
+static ncclResult_t connectServer(const char* server, int* out, bool retry) {
   struct sockaddr_un a;
-  socklen_t al = abstractAddr(d.server, &a);
+  socklen_t al = abstractAddr(server, &a);
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ipcTimeoutMs());
-  int c = -1;
   while (true) {
-    c = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
+    int c = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
     SYSCHECK(c >= 0, "socket");
-    if (connect(c, (struct sockaddr*)&a, al) == 0) break;
+    if (connect(c, (struct sockaddr*)&a, al) == 0) {
+      setTimeouts(c);
+      *out = c;
+      return ncclSuccess;
+    }
     int err = errno;
     close(c);
-    if (std::chrono::steady_clock::now() > deadline) {
-      WARN("ipc: connect to %s failed: %s", d.server, strerror(err));
+    if (!retry || std::chrono::steady_clock::now() > deadline) {
+      if (retry) WARN("ipc: connect to %s failed: %s", server, strerror(err));
       return ncclRemoteError;
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(5));
   }
-  setTimeouts(c);
-  int32_t reply[2] = {-1, 0};
-  struct msghdr m = {};
-  struct iovec io = {reply, sizeof(reply)};
-  m.msg_iov = &io;
-  m.msg_iovlen = 1;
-  char ctl[CMSG_SPACE(sizeof(int))] = {};
-  m.msg_control = ctl;
-  m.msg_controllen = sizeof(ctl);
+}
+
+// One request / reply round trip (fd attached to the request and / or received with the reply).
+static ncclResult_t ipcCall(const char* server, const IpcRequest& q, int sendFd, IpcReply* r, int* recvFd, bool retry) {
+  int c = -1;
+  NCCLCHECK(connectServer(server, &c, retry));
   int fd = -1;
-  if (send(c, &d.key, sizeof(d.key), MSG_NOSIGNAL) == (ssize_t)sizeof(d.key) &&
-      recvmsg(c, &m, MSG_WAITALL | MSG_CMSG_CLOEXEC) == (ssize_t)sizeof(reply) && reply[0] == 0) {
-    for (struct cmsghdr* h = CMSG_FIRSTHDR(&m); h; h = CMSG_NXTHDR(&m, h))
-      if (h->cmsg_level == SOL_SOCKET && h->cmsg_type == SCM_RIGHTS) memcpy(&fd, CMSG_DATA(h), sizeof(int));
-  }
+  r->status = -1;
+  bool ok = sendWithFd(c, &q, sizeof(q), sendFd) == 0 && recvWithFd(c, r, sizeof(*r), &fd) == 0;
   close(c);
-  if (fd < 0) {
+  if (recvFd) *recvFd = fd;
+  else if (fd >= 0) close(fd);
+  return ok ? ncclSuccess : ncclRemoteError;
+}
+
+ncclResult_t ipcFetchFd(const IpcDesc& d, int* out) {
+  IpcRequest q = {IPC_FETCH, -1, d.key, 0};
+  IpcReply r;
+  int fd = -1;
+  ncclResult_t res = ipcCall(d.server, q, -1, &r, &fd, true);
+  if (res != ncclSuccess && res != ncclRemoteError) return res;
+  if (fd < 0 || r.status != 0) {
+    if (fd >= 0) close(fd);
     WARN("ipc: %s did not hand over export %llu (%s)", d.server, (unsigned long long)d.key,
-         reply[0] == 0 ? "no descriptor attached" : "unknown key, timeout or peer gone");
+         r.status == 0 ? "no descriptor attached" : "unknown key, timeout or peer gone");
     return ncclRemoteError;
   }
   *out = fd;
   return ncclSuccess;
 }
+
+ncclResult_t ipcRemoteImport(const char* server, int rank, uint64_t tag, int fd, uint64_t size, uint64_t* addr) {
+  IpcRequest q = {IPC_IMPORT, rank, tag, size};
+  IpcReply r;
+  NCCLCHECK(ipcCall(server, q, fd, &r, nullptr, true));
+  if (r.status != 0) {
+    WARN("ipc: %s could not map a registered buffer of %zu MiB", server, (size_t)(size >> 20));
+    return ncclRemoteError;
+  }
+  *addr = r.value;
+  return ncclSuccess;
+}
+
+void ipcRemoteRelease(const char* server, int rank, uint64_t tag) {
+  IpcRequest q = {IPC_RELEASE, rank, tag, 0};
+  IpcReply r;
+  (void)ipcCall(server, q, -1, &r, nullptr, false);  // a peer already gone has released everything itself
+}
+
+uint64_t ipcNewTag() { return gKeySerial++; }
 
 // Close an imported descriptor unless the runtime already did: its number may by then name another file of
 // this process (opened by another thread meanwhile), so only while it still names the imported dma-buf.
@@ -277,29 +397,25 @@ static ncclResult_t importLegacy(const IpcDesc& d, IpcImport* out) {
   return ncclSuccess;
 }
 
-static ncclResult_t importDmaBuf(const IpcDesc& d, IpcImport* out) {
-  int fd = -1;
-  NCCLCHECK(ipcFetchFd(d, &fd));
-  if (paramInt("NCCL_AMD_IPC_FAIL_DMABUF", 0)) {  // tests: exercise the fallback on a box where dma-buf works
-    close(fd);
-    WARN("ipc: NCCL_AMD_IPC_FAIL_DMABUF=1: refusing the dma-buf import");
-    return ncclUnhandledCudaError;
-  }
+// Map a dma-buf fd (owned from here on: kept by the mapping, or closed on failure).
+static ncclResult_t importFd(int fd, uint64_t size, IpcImport* out) {
+  memset(out, 0, sizeof(*out));
+  out->fd = -1;
   hipExternalMemoryHandleDesc hd;
   memset(&hd, 0, sizeof(hd));
   hd.type = hipExternalMemoryHandleTypeOpaqueFd;
   hd.handle.fd = fd;
-  hd.size = d.size;
+  hd.size = size;
   hipExternalMemory_t em = nullptr;
   hipError_t e = hipImportExternalMemory(&em, &hd);
   if (e != hipSuccess) {
     close(fd);
-    WARN("ipc: hipImportExternalMemory(%zu MiB): %s", (size_t)(d.size >> 20), hipGetErrorString(e));
+    WARN("ipc: hipImportExternalMemory(%zu MiB): %s", (size_t)(size >> 20), hipGetErrorString(e));
     return ncclUnhandledCudaError;
   }
   // Descriptor ownership: kept until the mapping is released (ipcRelease), then closed if the runtime has
   // not closed it itself (the runtime's behaviour is logged at TRACE level)
-  TRACE("ipc: imported %zu MiB from %s (fd %d %s after import)", (size_t)(d.size >> 20), d.server, fd,
+  TRACE("ipc: imported %zu MiB (fd %d %s after import)", (size_t)(size >> 20), fd,
         fcntl(fd, F_GETFD) != -1 ? "open" : "closed by the runtime");
   out->fd = fd;
   struct stat st;
@@ -310,7 +426,7 @@ static ncclResult_t importDmaBuf(const IpcDesc& d, IpcImport* out) {
   hipExternalMemoryBufferDesc bd;
   memset(&bd, 0, sizeof(bd));
   bd.offset = 0;
-  bd.size = d.size;
+  bd.size = size;
   void* p = nullptr;
   e = hipExternalMemoryGetMappedBuffer(&p, em, &bd);
   if (e != hipSuccess) {
@@ -323,6 +439,17 @@ static ncclResult_t importDmaBuf(const IpcDesc& d, IpcImport* out) {
   out->ptr = p;
   out->ext = em;
   return ncclSuccess;
+}
+
+static ncclResult_t importDmaBuf(const IpcDesc& d, IpcImport* out) {
+  int fd = -1;
+  NCCLCHECK(ipcFetchFd(d, &fd));
+  if (paramInt("NCCL_AMD_IPC_FAIL_DMABUF", 0)) {  // tests: exercise the fallback on a box where dma-buf works
+    close(fd);
+    WARN("ipc: NCCL_AMD_IPC_FAIL_DMABUF=1: refusing the dma-buf import");
+    return ncclUnhandledCudaError;
+  }
+  return importFd(fd, d.size, out);
 }
 
 ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {

@@ -219,23 +219,26 @@ __device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t n
     u32x4* d = (u32x4*)dst;
     constexpr int U = kCopyUnroll;
     uint64_t i = threadIdx.x;
-    __amdgpu_buffer_rsrc_t rd;
-    if (REMOTE && NCCL_AMD_BUFFER_STORES) rd = remoteRsrc(dst);
     for (; i + (U - 1) * kThreads < npk; i += U * kThreads) {
       u32x4 v[U];
 #pragma unroll
       for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s + i + u * kThreads);
       LocalStore ls(dst, i - threadIdx.x);
+      // the buffer resource is rebased on every batch (its wave-uniform first pack), so the 32-bit store
+      // offsets stay below U * kThreads * 16 bytes whatever the range's size (a symmetric-window part can
+      // exceed 4 GiB with a low channel cap)
+      __amdgpu_buffer_rsrc_t rd;
+      if (REMOTE && NCCL_AMD_BUFFER_STORES) rd = remoteRsrc(d + (i - threadIdx.x));
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        if (REMOTE && NCCL_AMD_BUFFER_STORES) storeRemoteAt(rd, (uint32_t)((i + u * kThreads) * 16), v[u]);
+        if (REMOTE && NCCL_AMD_BUFFER_STORES) storeRemoteAt(rd, (uint32_t)((threadIdx.x + u * kThreads) * 16), v[u]);
         else if (REMOTE) storeRemote(d + i + u * kThreads, v[u]);
         else ls.put(threadIdx.x + u * kThreads, v[u]);
       }
     }
     for (; i < npk; i += kThreads) {
       u32x4 v = __builtin_nontemporal_load(s + i);
-      if (REMOTE && NCCL_AMD_BUFFER_STORES) storeRemoteAt(rd, (uint32_t)(i * 16), v);
+      if (REMOTE && NCCL_AMD_BUFFER_STORES) storeRemoteAt(remoteRsrc(d + (i - threadIdx.x)), threadIdx.x * 16u, v);
       else if (REMOTE) storeRemote(d + i, v);
       else __builtin_nontemporal_store(v, d + i);
     }
@@ -324,7 +327,9 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
         for (int e = 0; e < EPP; e++) acc[u].e[e] = fn.post(acc[u].e[e]);
         if (dstLocal) ls.put(threadIdx.x + u * kThreads, acc[u].v);
         for (int p = 0; p < nPush; p++) {
-          if (NCCL_AMD_BUFFER_STORES) storeRemoteAt(remoteRsrc(dstPush[p]), (uint32_t)(i * 16), acc[u].v);
+          // resource rebased on the batch's first pack: 32-bit offsets at any range size
+          if (NCCL_AMD_BUFFER_STORES)
+            storeRemoteAt(remoteRsrc((u32x4*)dstPush[p] + (base - threadIdx.x)), (threadIdx.x + u * kThreads) * 16u, acc[u].v);
           else storeRemote((u32x4*)dstPush[p] + i, acc[u].v);
         }
       }
@@ -1171,6 +1176,9 @@ struct SymShared {
   uint64_t* sigPtr[NCCL_AMD_MAX_RANKS];
   uint64_t sigVal[NCCL_AMD_MAX_RANKS];
   char* pushPtr[1];
+  const char* send[NCCL_AMD_MAX_RANKS];  // every rank's buffers as mapped here (windows: from the arguments;
+  char* recv[NCCL_AMD_MAX_RANKS];        // registered buffers: exchanged at entry)
+  int aligned;
 };
 
 // Every lane i < n (i != me) stores `e` into peer i's flag word [c][kind][me]; REL publishes my prior stores.
@@ -1207,7 +1215,17 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
   }
   const Red<T, OP> fn(opArg);
-  const bool aligned = a.aligned != 0;
+  if (tid < NCCL_AMD_MAX_RANKS) {
+    sh.send[tid] = a.send[tid];
+    sh.recv[tid] = a.recv[tid];
+    // registered buffers: hand rank tid MY buffers as mapped in its address space (its REG words of this
+    // channel; read by it after my ENTER below, which signalAll orders behind these stores' completion)
+    if (a.regMode && tid < n && tid != me) {
+      storeFlag(dc.flags[tid] + flagIndex(c, FLG_REG_SEND, me), (uint64_t)a.send[tid]);
+      storeFlag(dc.flags[tid] + flagIndex(c, FLG_REG_RECV, me), (uint64_t)a.recv[tid]);
+    }
+  }
+  bool aligned = a.aligned != 0;
   // wtPublish: what peers read from my output (AR: my reduced part; AG: my own block) is stored system-scope
   // write-through, so nothing of it sits dirty in this XCD's L2 and the signal that publishes it needs no
   // L2 write-back (buffer_wbl2), only the store drain — as the staged path's pushes
@@ -1231,15 +1249,33 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     partOf(a.chunk, lo, hi);
     char* dst = a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
     const char* src = a.send[me] + lo * ts;
+    // registered buffers: only my own pointers are known here, alignment of the copy is decided by them
+    if (a.regMode) aligned = aligned && (((uintptr_t)a.recv[me] | (uintptr_t)a.send[me]) & 15) == 0;
     if (dst != src) {
       if (wt) copyRange<T, true>(dst, src, (hi - lo) * ts, aligned);
       else copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
     }
     // in place, the block was written by the caller's earlier kernels: keep the write-back release for it
-    agRel = !wt || dst == src;
+    agRel = !wt || dst == src || a.relFence;
   }
   symSignal(dc, sh, c, FLG_SYM_ENTER, e, agRel);  // AG: publishes that block
   ok = symWait(dc, sh, c, FLG_SYM_ENTER, e, true);
+  if (a.regMode) {
+    // every peer stored its buffers (as mapped here) before its ENTER: read them, then decide the access
+    // width from ALL ranks' pointers — the same set on every rank, so every rank takes the same path
+    if (tid < n && tid != me) {
+      sh.send[tid] = (const char*)loadFlag(dc.flags[me] + flagIndex(c, FLG_REG_SEND, tid));
+      sh.recv[tid] = (char*)loadFlag(dc.flags[me] + flagIndex(c, FLG_REG_RECV, tid));
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uintptr_t al = 0;
+      for (int r = 0; r < n; r++) al |= (uintptr_t)sh.recv[r] | (COLL == SYM_AG ? 0 : (uintptr_t)sh.send[r]);
+      sh.aligned = a.aligned != 0 && (al & 15) == 0;
+    }
+    __syncthreads();
+    aligned = sh.aligned != 0;
+  }
   if (ok && COLL == SYM_AR1) {
     // one-shot: fold my channel's portion of the whole buffer from all n inputs, owner block by block
     uint64_t lo, hi;
@@ -1248,9 +1284,9 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
       const int owner = (int)(x / a.chunk);
       const uint64_t end = min(hi, (uint64_t)(owner + 1) * a.chunk);
       if (tid == 0)
-        for (int k = 0; k < n; k++) sh.srcPtr[k] = a.send[(owner + 1 + k) % n] + x * ts;
+        for (int k = 0; k < n; k++) sh.srcPtr[k] = sh.send[(owner + 1 + k) % n] + x * ts;
       __syncthreads();
-      foldRange<T, OP>(fn, n, sh.srcPtr, end - x, a.recv[me] + x * ts, nullptr, 0, aligned);
+      foldRange<T, OP>(fn, n, sh.srcPtr, end - x, sh.recv[me] + x * ts, nullptr, 0, aligned);
       __syncthreads();
       x = end;
     }
@@ -1259,9 +1295,9 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     uint64_t lo, hi;
     partOf(blockLen(me), lo, hi);
     if (tid == 0)
-      for (int k = 0; k < n; k++) sh.srcPtr[k] = a.send[(me + 1 + k) % n] + ((uint64_t)me * a.chunk + lo) * ts;
+      for (int k = 0; k < n; k++) sh.srcPtr[k] = sh.send[(me + 1 + k) % n] + ((uint64_t)me * a.chunk + lo) * ts;
     __syncthreads();
-    char* dst = COLL == SYM_RS ? a.recv[me] + lo * ts : a.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
+    char* dst = COLL == SYM_RS ? sh.recv[me] + lo * ts : sh.recv[me] + ((uint64_t)me * a.chunk + lo) * ts;
     const bool push = COLL == SYM_AR && wt;  // peers read it in the pull phase
     if (tid == 0) sh.pushPtr[0] = dst;
     __syncthreads();
@@ -1269,7 +1305,7 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     __syncthreads();
   }
   if (ok && COLL == SYM_AR) {
-    symSignal(dc, sh, c, FLG_SYM_MID, e, !wt);  // my reduced part is in my output: publish it
+    symSignal(dc, sh, c, FLG_SYM_MID, e, !wt || a.relFence);  // my reduced part is in my output: publish it
     ok = symWait(dc, sh, c, FLG_SYM_MID, e, true);
   }
   if (ok && (COLL == SYM_AR || COLL == SYM_AG)) {
@@ -1279,7 +1315,7 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
       uint64_t lo, hi;
       partOf(blockLen(q), lo, hi);
       const uint64_t off = ((uint64_t)q * a.chunk + lo) * ts;
-      copyRange<T, false>(a.recv[me] + off, a.recv[q] + off, (hi - lo) * ts, aligned);
+      copyRange<T, false>(sh.recv[me] + off, sh.recv[q] + off, (hi - lo) * ts, aligned);
     }
     __syncthreads();
   }

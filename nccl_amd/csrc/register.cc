@@ -1,17 +1,21 @@
 // register.cc — buffer registration and symmetric windows.
 //
 // Reference: src/register/register.cc:154-200 (ncclCommRegister / ncclCommDeregister: local, refcounted
-// registration used by the reference's SIMPLE-protocol zero-copy paths), src/dev_runtime.cc:1331-1400,
-// 1592-1610 (ncclCommWindowRegister as a group task: every rank maps every peer's window;
-// ncclCommWindowDeregister; ncclWinGetUserPtr), src/device/symmetric/* (the kernels that use them).
+// registration), src/register/coll_reg.cc:326-395 (a ring collective on registered buffers: the buffer is
+// IPC-registered with every peer, src/transport/p2p.cc ipcRegisterBuffer, and the kernels exchange the peers'
+// addresses of it at run time, src/device/prims_simple.h:748-846 ptrExchange), src/enqueue.cc:283
+// (NCCL_GRAPH_REGISTER: buffers of captured collectives are registered automatically),
+// src/dev_runtime.cc:1331-1400, 1592-1610 (ncclCommWindowRegister as a group task: every rank maps every
+// peer's window; ncclCommWindowDeregister; ncclWinGetUserPtr), src/device/symmetric/* (the window kernels).
 //
-// ncclCommRegister: this engine's staged path only ever reads and writes user buffers locally (peers
-// exchange data through the comm's own uncached staging), so there is nothing to map: the call
-// validates and records the buffer and returns a handle, like the reference does when local
-// registration is disabled (register.cc:156-159). Zero-copy is what windows are for:
-// ncclCommWindowRegister maps every peer's buffer into this process (a dma-buf fd across processes, ipc.cc;
-// the raw pointer inside one process) and collectives whose buffers lie in NCCL_WIN_COLL_SYMMETRIC windows
-// run the symmetric kernels (kernels.h symKernel), which read peers' windows directly.
+// ncclCommRegister stays a LOCAL call, as in the reference: the allocation holding the buffer is exported as a
+// dma-buf and each peer process maps it through its fd server (ipc.cc IMPORT request — the reference's proxy
+// thread does the same for ipcRegisterBuffer), which answers where it landed. A collective whose buffers are
+// registered then runs the zero-copy symmetric kernel in "registered" mode (kernels.h symKernel, regMode): each
+// rank hands every peer its buffers as mapped in that peer through the flag block before its ENTER signal, so
+// ranks need not agree on offsets, and nothing is staged. As in the reference, every rank registers the
+// buffers it passes to such a collective (docs/userguide/source/usage/bufferreg.rst:55-56); windows
+// (ncclCommWindowRegister) remain the collective, symmetric form.
 #include <string.h>
 #include <unistd.h>
 
@@ -96,6 +100,7 @@ static ncclResult_t windowRegister(ncclComm* comm, void* buff, size_t size, nccl
   }
 
   ncclWindow_vidmem* w = new ncclWindow_vidmem();
+  ncclResult_t mapRes = ncclSuccess;
   w->comm = comm;
   w->userPtr = buff;
   w->size = size;
@@ -114,23 +119,30 @@ static ncclResult_t windowRegister(ncclComm* comm, void* buff, size_t size, nccl
     }
     ncclResult_t res = ipcMap(comm, r, p, &w->peerPtr[r]);
     if (res != ncclSuccess) {
-      for (int q = 0; q < r; q++)
-        if (w->peerBase[q]) ipcUnmap(comm, q, w->peerBase[q]);
-      if (needIpc) ipcUnexport(comm, me.desc);
-      delete w;
-      return res;
+      mapRes = res;
+      break;
     }
     w->peerBase[r] = p.base;
   }
   if (needIpc) {
-    // every peer has mapped my allocation (its mapping keeps it referenced): stop serving the descriptor
-    std::vector<char> sync(comm->nRanks);
+    // Every rank joins this all-gather whatever its own imports gave: a rank that failed to map
+    // a peer must not leave the others waiting in it. It carries each rank's outcome, so all ranks release
+    // their mappings and return the same error together; on success every peer has mapped my allocation
+    // (its mapping keeps it referenced) and the descriptor is no longer served.
+    std::vector<char> sync(comm->nRanks, 0);
+    sync[comm->rank] = mapRes == ncclSuccess ? 1 : 0;
     ncclResult_t bres = commAllGather(comm, sync.data(), 1);
     ipcUnexport(comm, me.desc);
+    for (int r = 0; r < comm->nRanks && bres == ncclSuccess; r++)
+      if (!sync[r]) bres = mapRes != ncclSuccess ? mapRes : ncclRemoteError;
     if (bres != ncclSuccess) {
+      if (mapRes == ncclSuccess) WARN("ncclCommWindowRegister: a peer could not map its windows; releasing");
       windowRelease(comm, w);
       return bres;
     }
+  } else if (mapRes != ncclSuccess) {
+    windowRelease(comm, w);
+    return mapRes;
   }
   comm->windows.push_back(w);
   *win = w;
@@ -153,14 +165,177 @@ ncclWindow_vidmem* findSymWindow(ncclComm* comm, const void* p, size_t bytes) {
   return nullptr;
 }
 
+// ---- registered buffers (ncclCommRegister, NCCL_GRAPH_REGISTER) ----
+
+static uint64_t bufferIdOf(const void* p) {
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (uint64_t)id;
+}
+
+// Drop the peers' mappings of an allocation (the caller made sure no kernel of this rank still uses it; a
+// peer's kernels stop reading it before this rank's kernel passes its DONE handshake).
+static void regRelease(ncclComm* comm, RegAlloc* ra) {
+  for (int r = 0; r < comm->nRanks; r++)
+    if (ra->imported[r]) ipcRemoteRelease(comm->peers[r].stagingDesc.server, comm->rank, ra->tag);
+  delete ra;
+}
+
+// Map the allocation [base, +size) into every peer process (same process: its own pointer).
+static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint64_t id, RegAlloc** out) {
+  RegAlloc* ra = new RegAlloc();
+  memset(ra, 0, sizeof(*ra));
+  ra->base = base;
+  ra->size = size;
+  ra->bufferId = id;
+  ra->tag = ipcNewTag();
+  ra->usable = true;
+  const int me = comm->rank, pid = getpid();
+  int fd = -1;
+  ncclResult_t res = ncclSuccess;
+  for (int r = 0; r < comm->nRanks && res == ncclSuccess; r++) {
+    if (r == me || comm->peers[r].pid == pid) {  // one address space (peer access enabled at init)
+      ra->rmt[r] = base;
+      continue;
+    }
+    if (comm->peers[r].stagingDesc.server[0] == 0) {  // NCCL_AMD_IPC=legacy: no fd server to map through
+      INFO("rank %d: registered buffer %lx stays local (no fd server on rank %d)", me, (unsigned long)base, r);
+      ra->usable = false;
+      break;
+    }
+    if (fd < 0) {
+      hipError_t e = hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        WARN("ncclCommRegister: allocation %lx (+%zu) cannot be exported: %s", (unsigned long)base, (size_t)size,
+             hipGetErrorString(e));
+        res = ncclUnhandledCudaError;
+        break;
+      }
+    }
+    res = ipcRemoteImport(comm->peers[r].stagingDesc.server, me, ra->tag, fd, size, &ra->rmt[r]);
+    if (res == ncclSuccess) ra->imported[r] = true;
+  }
+  if (fd >= 0) close(fd);
+  if (res != ncclSuccess) {
+    regRelease(comm, ra);
+    return res;
+  }
+  TRACE("rank %d: registered allocation %lx +%zu MiB (tag %lu, %s)", me, (unsigned long)base, (size_t)(size >> 20),
+        (unsigned long)ra->tag, ra->usable ? "mapped by every peer" : "local only");
+  *out = ra;
+  return ncclSuccess;
+}
+
+// Find or create the registration of the allocation holding [buff, +size) and take a reference on it.
+static ncclResult_t regAcquire(ncclComm* comm, const void* buff, size_t size, bool graph, RegAlloc** out) {
+  hipDeviceptr_t base = nullptr;
+  size_t allocSize = 0;
+  HIPCHECK(hipMemGetAddressRange(&base, &allocSize, (hipDeviceptr_t)buff));
+  if ((uint64_t)buff + size > (uint64_t)base + allocSize) {
+    WARN("ncclCommRegister: [%p, +%zu) is not inside one allocation", buff, size);
+    return ncclInvalidArgument;
+  }
+  const uint64_t id = bufferIdOf(buff);
+  RegAlloc* ra = nullptr;
+  for (RegAlloc* x : comm->regs)
+    if (x->base == (uint64_t)base && x->size == allocSize && x->bufferId == id) ra = x;
+  if (!ra) {
+    NCCLCHECK(regCreate(comm, (uint64_t)base, allocSize, id, &ra));
+    comm->regs.push_back(ra);
+  }
+  if (graph) ra->graphRefs++;
+  else ra->localRefs++;
+  *out = ra;
+  return ncclSuccess;
+}
+
+static void regPut(ncclComm* comm, RegAlloc* ra, bool graph) {
+  if (graph) ra->graphRefs--;
+  else ra->localRefs--;
+  if (ra->localRefs > 0 || ra->graphRefs > 0) return;
+  comm->regs.erase(std::find(comm->regs.begin(), comm->regs.end(), ra));
+  regRelease(comm, ra);
+}
+
+// The usable registration holding [p, +bytes), or nullptr. A registration whose allocation was freed and its
+// range handed out again (another buffer id) is never used; an automatic (graph) one is dropped then.
+static RegAlloc* regFind(ncclComm* comm, const void* p, size_t bytes, bool capturing) {
+  const uint64_t a = (uint64_t)p;
+  uint64_t id = 0;
+  bool haveId = false;
+  for (size_t i = 0; i < comm->regs.size(); i++) {
+    RegAlloc* ra = comm->regs[i];
+    if (a < ra->base || a + bytes > ra->base + ra->size) continue;
+    if (!haveId) {
+      id = bufferIdOf(p);
+      haveId = true;
+    }
+    if (id != ra->bufferId) {  // stale: the registered allocation is gone
+      if (ra->localRefs == 0) {
+        INFO("rank %d: allocation %lx was freed and re-allocated since a captured collective registered it",
+             comm->rank, (unsigned long)ra->base);
+        ra->graphRefs = 1;
+        regPut(comm, ra, true);
+        i--;
+      }
+      continue;
+    }
+    if (!ra->usable || (ra->localRefs == 0 && !capturing)) return nullptr;  // automatic ones: captures only
+    return ra;
+  }
+  return nullptr;
+}
+
+bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
+               size_t recvBytes, const char** rmtSend, char** rmtRecv) {
+  if (comm->nRanks == 1) return false;
+  bool capturing = false;
+  if (comm->tune.graphRegister) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    capturing = hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+    (void)hipGetLastError();
+  }
+  if (comm->regs.empty() && !capturing) return false;
+  RegAlloc* rs = send ? regFind(comm, send, sendBytes, capturing) : nullptr;
+  RegAlloc* rr = regFind(comm, recv, recvBytes, capturing);
+  if (capturing) {
+    // NCCL_GRAPH_REGISTER (reference enqueue.cc:283, coll_reg.cc:383-387): a captured collective registers its
+    // buffers itself; the registrations live until the communicator is destroyed (or their range is freed and
+    // re-allocated, regFind)
+    // (relaxed capture mode around the export: the capture of this thread stays valid whatever the runtime
+    // deems unsafe among the calls below)
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    RegAlloc* x = nullptr;
+    if (send && !rs && regAcquire(comm, send, sendBytes, true, &x) == ncclSuccess) rs = x->usable ? x : nullptr;
+    if (!rr && regAcquire(comm, recv, recvBytes, true, &x) == ncclSuccess) rr = x->usable ? x : nullptr;
+    (void)hipThreadExchangeStreamCaptureMode(&mode);
+    (void)hipGetLastError();
+  }
+  if (!rr || (send && !rs)) return false;
+  for (int r = 0; r < comm->nRanks; r++) {
+    rmtSend[r] = send ? (const char*)(rs->rmt[r] + ((uint64_t)send - rs->base)) : nullptr;
+    rmtRecv[r] = (char*)(rr->rmt[r] + ((uint64_t)recv - rr->base));
+  }
+  return true;
+}
+
 void windowsFree(ncclComm* comm) {
   (void)hipSetDevice(comm->device);
   for (ncclWindow_vidmem* w : comm->windows) windowRelease(comm, w);
   comm->windows.clear();
   for (IpcMapping& m : comm->ipcMaps) ipcRelease(&m.map);
   comm->ipcMaps.clear();
-  for (void* h : comm->regHandles) free(h);
+  for (RegHandle* h : comm->regHandles) delete h;
   comm->regHandles.clear();
+  // No release requests at destroy: peers may be tearing down at the same moment, and every peer's fd server
+  // drops the mappings it holds for this communicator when it stops (ipcServerStop)
+  for (RegAlloc* ra : comm->regs) delete ra;
+  comm->regs.clear();
 }
 
 }  // namespace ncclamd
@@ -168,11 +343,6 @@ void windowsFree(ncclComm* comm) {
 using namespace ncclamd;
 
 #define NCCL_ALIAS(ret, name, ...) extern "C" __attribute__((visibility("default"), alias(#name))) ret p##name(__VA_ARGS__);
-
-struct RegHandle {
-  void* buff;
-  size_t size;
-};
 
 NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle) {
   NCCLCHECK(commCheck(comm, "ncclCommRegister", "comm"));
@@ -185,9 +355,20 @@ NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, siz
     WARN("ncclCommRegister : invalid buffer %p / size %zu", buff, size);
     return ncclInvalidArgument;
   }
-  RegHandle* h = (RegHandle*)malloc(sizeof(RegHandle));
-  h->buff = buff;
-  h->size = size;
+  int st = comm->asyncResult.load();
+  if (st != ncclSuccess) return st == ncclInProgress ? ncclInProgress : ncclInvalidUsage;
+  RegHandle* h = new RegHandle{buff, size, nullptr};
+  // NCCL_LOCAL_REGISTER=0: the handle only records the buffer (reference register.cc:156-159 returns NULL;
+  // a handle is kept here so that ncclCommDeregister of it stays valid)
+  if (comm->tune.localRegister && comm->nRanks > 1) {
+    DeviceRestore restore;
+    HIPCHECK(hipSetDevice(comm->device));
+    ncclResult_t res = regAcquire(comm, buff, size, false, &h->ra);
+    if (res != ncclSuccess) {
+      delete h;
+      return res;
+    }
+  }
   comm->regHandles.push_back(h);
   *handle = h;
   return ncclSuccess;
@@ -197,13 +378,21 @@ NCCL_ALIAS(ncclResult_t, ncclCommRegister, const ncclComm_t, void*, size_t, void
 NCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle) {
   NCCLCHECK(commCheck(comm, "ncclCommDeregister", "comm"));
   if (handle == nullptr) return ncclSuccess;  // reference commDeregister: NULL reg is a no-op
-  auto it = std::find(comm->regHandles.begin(), comm->regHandles.end(), handle);
+  auto it = std::find(comm->regHandles.begin(), comm->regHandles.end(), (RegHandle*)handle);
   if (it == comm->regHandles.end()) {
     WARN("Deregister: Could not find handle");
     return ncclInvalidUsage;
   }
+  RegHandle* h = *it;
   comm->regHandles.erase(it);
-  free(handle);
+  if (h->ra) {
+    // collectives enqueued on the buffer may still run: wait for them before the peers unmap it
+    DeviceRestore restore;
+    HIPCHECK(hipSetDevice(comm->device));
+    if (h->ra->localRefs == 1 && h->ra->graphRefs == 0) HIPCHECK(hipDeviceSynchronize());
+    regPut(comm, h->ra, false);
+  }
+  delete h;
   return ncclSuccess;
 }
 NCCL_ALIAS(ncclResult_t, ncclCommDeregister, const ncclComm_t, void*)

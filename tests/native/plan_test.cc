@@ -58,6 +58,7 @@ ncclResult_t launchSymPlan(const SymPlan& p) {
   return ncclSuccess;
 }
 ncclWindow_vidmem* findSymWindow(ncclComm*, const void*, size_t) { return nullptr; }
+bool regLookup(ncclComm*, hipStream_t, const void*, size_t, const void*, size_t, const char**, char**) { return false; }
 bool groupActive() { return false; }
 ncclResult_t groupDeferColl(const CollInfo&) { return ncclSuccess; }
 void groupRecordError(ncclResult_t) {}

@@ -72,6 +72,44 @@ def _dev(torch, arr):
     return torch.from_numpy(np.ascontiguousarray(arr).view(np.uint8)).cuda()
 
 
+def test_c1_allreduce_fp32_64MiB_n1(built):
+    """C1: ncclAllReduce sum fp32, 64 MiB, world_size 1 (reference taskAppend -> ncclLaunchOneRank,
+    src/enqueue.cc:3039-3041; src/device/onerank.cu:49-110): out of place the output is the input bit for bit
+    (oracle.all_reduce of one rank), in place the call moves nothing and leaves the buffer untouched. Also the
+    avg (PreMulSum by 1/1 = identity) at the same size, which takes the one-rank kernel instead of the copy."""
+    import oracle
+    import torch
+    import nccl_amd
+    torch.cuda.set_device(0)
+    comm = nccl_amd.Communicator.init_all([0])[0]
+    try:
+        count = 64 * MIB // 4
+        src = oracle.fill(7, _seed(0), count)
+        want = oracle.all_reduce([src], 7, 0)
+        assert want.view(np.uint32).tobytes() == src.view(np.uint32).tobytes()
+        send = _dev(torch, src)
+        recv = torch.full_like(send, 0xA5)
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        comm.all_reduce_raw(send.data_ptr(), recv.data_ptr(), count, 7, 0, s.cuda_stream)
+        s.synchronize()
+        assert comm.async_error() == 0
+        assert not _cmp("C1 out of place", recv.cpu().numpy().view(np.float32), want, 7)
+        assert not _cmp("C1 sendbuff", send.cpu().numpy().view(np.float32), src, 7)  # input not written
+        # in place: no bytes move (reference onerank.cu:52-56 skips the copy), the buffer is unchanged
+        comm.all_reduce_raw(send.data_ptr(), send.data_ptr(), count, 7, 0, s.cuda_stream)
+        s.synchronize()
+        assert not _cmp("C1 in place", send.cpu().numpy().view(np.float32), src, 7)
+        # avg on one rank: PreMulSum by fp32(1/1) = x * 1.0, bit-exact identity (oracle restates it)
+        recv.fill_(0)
+        torch.cuda.synchronize()
+        comm.all_reduce_raw(send.data_ptr(), recv.data_ptr(), count, 7, 4, s.cuda_stream)
+        s.synchronize()
+        assert not _cmp("C1 avg", recv.cpu().numpy().view(np.float32), oracle.all_reduce([src], 7, 4), 7)
+    finally:
+        comm.destroy()
+
+
 def _c2_worker(rank, nranks, uid, q):
     try:
         import oracle

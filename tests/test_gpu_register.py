@@ -1,0 +1,247 @@
+"""GPU parity tests of zero-copy collectives on buffers registered with ncclCommRegister (reference
+src/register/register.cc:154-200, src/register/coll_reg.cc:326-395; docs/userguide/source/usage/bufferreg.rst:
+every rank registers the buffers it passes). Registration is local: the allocation is mapped into every peer
+process by that peer's fd server (ipc.cc IMPORT), and the collective runs the symmetric kernel in registered
+mode — the peers' buffer addresses are exchanged by the kernels at entry (kernels.h symKernel regMode, the
+reference's ptrExchange, prims_simple.h:748-846), so ranks need not use the same offsets. Results must be
+bit-identical to the oracle for AllReduce, ReduceScatter and AllGather; Reduce keeps the staged path. Also:
+buffers of captured collectives are registered automatically (NCCL_GRAPH_REGISTER, reference enqueue.cc:283).
+All ranks share the box's one GPU (single process: raw pointers; multi-process: dma-buf IPC)."""
+import multiprocessing as mp
+import os
+import queue
+import re
+import time
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_windows import HALF, WIN_BYTES, _cases, _run
+
+os.environ.setdefault("NCCL_AMD_SPIN_TIMEOUT_MS", "30000")
+pytestmark = pytest.mark.gpu
+
+
+def _spawn(target, nranks, args=(), limit_s=600):
+    import nccl_amd
+    uid = nccl_amd.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=target, args=(r, nranks, uid, q) + tuple(args)) for r in range(nranks)]
+    for p in ps:
+        p.start()
+    results, t0 = {}, time.time()
+    while len(results) < nranks and time.time() - t0 < limit_s:
+        try:
+            r, out = q.get(timeout=20)
+            results[r] = out
+        except queue.Empty:
+            print(f"[{target.__name__}] {len(results)}/{nranks} done, {time.time() - t0:.0f}s", flush=True)
+            if not any(p.is_alive() for p in ps):
+                break
+    for p in ps:
+        if p.is_alive() and len(results) < nranks:
+            p.kill()
+        p.join(timeout=60)
+    assert len(results) == nranks, f"only {len(results)} of {nranks} ranks reported"
+    return results
+
+
+def _trace_env(tag):
+    logf = f"/tmp/nccl_amd_reg_{tag}_{os.getpid()}.log"
+    os.environ["NCCL_DEBUG"] = "TRACE"
+    os.environ["NCCL_DEBUG_FILE"] = logf
+    return logf
+
+
+def _zero_copy_lines(logf, pos=0):
+    if not os.path.exists(logf):
+        return []
+    with open(logf) as f:
+        f.seek(pos)
+        return re.findall(r"(AllReduce|ReduceScatter|AllGather): registered zero-copy", f.read())
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_registered_single_process(built, nranks, monkeypatch):
+    """ncclCommInitAll ranks on one GPU: each registers its whole buffer (ncclCommRegister only, no window);
+    every case of the window suite — 13 type/op pairs, ragged counts, in place, unaligned — bit-exact."""
+    import torch
+    import nccl_amd
+    monkeypatch.setenv("NCCL_PROTO", "^LL")
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0] * nranks)
+    streams = [torch.cuda.Stream() for _ in range(nranks)]
+    bufs = [torch.empty(WIN_BYTES, dtype=torch.uint8, device="cuda") for _ in comms]
+    handles = [c.register_buffer(b.data_ptr(), WIN_BYTES) for c, b in zip(comms, bufs)]
+    cs = list(zip(comms, streams))
+    errs = []
+    for i, case in enumerate(_cases(nranks, quick=nranks > 2)):
+        errs += _run(cs, [(b, b.data_ptr()) for b in bufs], *case, seed=i, root=i % nranks)
+        if errs:
+            break
+    for c, h in zip(comms, handles):
+        c.deregister_buffer(h)
+    # after deregistration the same buffers take the staged path, still bit-exact
+    if not errs:
+        errs += _run(cs, [(b, b.data_ptr()) for b in bufs], "allreduce", 7, 0, 200_003, 0, False, seed=99)
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
+def _mp_worker(rank, nranks, uid, q):
+    try:
+        os.environ["NCCL_PROTO"] = "^LL"
+        logf = _trace_env(f"mp{nranks}")
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        # a different offset inside the registered allocation on every rank: ranks need not agree on offsets
+        shift = 4096 * (rank + 1)
+        alloc = torch.empty(WIN_BYTES + 16 * 4096, dtype=torch.uint8, device="cuda")
+        buf = alloc[shift:shift + WIN_BYTES]
+        h = comm.register_buffer(alloc.data_ptr(), alloc.numel())
+        s = torch.cuda.Stream()
+        errs = []
+        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+        cases = _cases(nranks, quick=True)
+        for i, case in enumerate(cases):
+            errs += _run([(comm, s)], [(buf, buf.data_ptr())], *case, seed=i, root=i % nranks)
+            if errs:
+                break
+        torch.cuda.synchronize()
+        zc = _zero_copy_lines(logf, pos)
+        comm.deregister_buffer(h)
+        # deregistered: the staged path again, every rank alike
+        pos = os.path.getsize(logf)
+        if not errs:
+            errs += _run([(comm, s)], [(buf, buf.data_ptr())], "allreduce", 7, 0, 100_001, 0, False, seed=77)
+        torch.cuda.synchronize()
+        after = _zero_copy_lines(logf, pos)
+        comm.destroy()
+        nonreduce = sum(c[0] != "reduce" for c in cases)
+        q.put((rank, (errs, len(zc), nonreduce, len(after))))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0, 0)))
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_registered_multi_process(built, nranks):
+    """One process per rank (ncclCommInitRank + dma-buf IPC): ncclCommRegister only. Every AllReduce /
+    ReduceScatter / AllGather of the case list runs zero-copy (counted in the NCCL_DEBUG=TRACE plan lines)
+    and is bit-exact; the Reduce falls back to the staged path; after ncclCommDeregister the staged path runs."""
+    res = _spawn(_mp_worker, nranks)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:20])
+    for r, (_, zc, nonreduce, after) in res.items():
+        assert zc == nonreduce, f"rank {r}: {zc} zero-copy plans for {nonreduce} eligible collectives"
+        assert after == 0, f"rank {r}: zero-copy plan after deregistration"
+
+
+def _graph_worker(rank, nranks, uid, q):
+    """NCCL_GRAPH_REGISTER: a captured AllReduce / ReduceScatter / AllGather registers its buffers itself and
+    runs zero-copy on every replay (fresh inputs each time, bit-exact); eager calls on the same buffers keep
+    the staged path (automatic registrations serve captures only)."""
+    try:
+        logf = _trace_env(f"graph{nranks}")
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = nccl_amd.dedicated_stream(0)
+        count = 3 << 20  # 12 MiB fp32: above the one-shot / LL ranges
+        x = torch.empty(count, dtype=torch.float32, device="cuda")
+        y = torch.empty(count, dtype=torch.float32, device="cuda")
+        z = torch.empty(count * nranks, dtype=torch.float32, device="cuda")
+        rs = torch.empty(count // nranks, dtype=torch.float32, device="cuda")
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+        with torch.cuda.graph(g, stream=s):
+            sp = s.cuda_stream
+            comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, sp)
+            comm.reduce_scatter_raw(x.data_ptr(), rs.data_ptr(), count // nranks, 7, 0, sp)
+            comm.all_gather_raw(x.data_ptr(), z.data_ptr(), count, 7, sp)
+        zc = _zero_copy_lines(logf, pos)
+        errs = []
+        for it in range(3):
+            ins = G.make_inputs(nranks, 7, count, seed=500 + it)
+            x.copy_(torch.from_numpy(ins[rank]))
+            torch.cuda.synchronize()
+            with torch.cuda.stream(s):
+                g.replay()
+            torch.cuda.synchronize()
+            if comm.async_error():
+                errs.append(f"rank {rank} replay {it}: async {comm.async_error()}")
+                break
+            checks = (("allreduce", y, oracle.all_reduce(ins, 7, 0)),
+                      ("reducescatter", rs, oracle.reduce_scatter(ins, 7, 0)[rank]),
+                      ("allgather", z, oracle.all_gather(ins)))
+            for name, out, want in checks:
+                if not G.same_bits(out.cpu().numpy(), want, 7):
+                    errs.append(f"rank {rank} replay {it}: {name} differs")
+        # eager on the same (automatically registered) buffers: staged
+        pos = os.path.getsize(logf)
+        G.make_inputs(nranks, 7, count, seed=9)
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+        torch.cuda.synchronize()
+        eager_zc = _zero_copy_lines(logf, pos)
+        del g
+        comm.destroy()
+        q.put((rank, (errs, len(zc), len(eager_zc))))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0)))
+
+
+def test_graph_register_multi_process(built):
+    res = _spawn(_graph_worker, 2)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:20])
+    for r, (_, zc, eager) in res.items():
+        assert zc == 3, f"rank {r}: {zc} zero-copy plans captured (want 3)"
+        assert eager == 0, f"rank {r}: an eager call used an automatic registration"
+
+
+def _large_worker(rank, nranks, uid, q):
+    """The metric's size on registered buffers: 256 MiB fp32 per rank, every rank's sendbuff and recvbuff in
+    separate torch allocations registered with ncclCommRegister, bit-exact vs the oracle at full size."""
+    try:
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        count = 256 * (1 << 20) // 4
+        inputs = [oracle.fill(7, 0x5EED0000 + r, count) for r in range(nranks)]
+        want = oracle.all_reduce(inputs, 7, 0)
+        send = torch.from_numpy(inputs[rank]).cuda()
+        recv = torch.zeros_like(send)
+        hs = [comm.register_buffer(send.data_ptr(), send.numel() * 4),
+              comm.register_buffer(recv.data_ptr(), recv.numel() * 4)]
+        s = torch.cuda.Stream()
+        torch.cuda.synchronize()
+        comm.all_reduce_raw(send.data_ptr(), recv.data_ptr(), count, 7, 0, s.cuda_stream)
+        s.synchronize()
+        errs = [f"rank {rank}: async {comm.async_error()}"] if comm.async_error() else []
+        got = recv.cpu().numpy()
+        if not errs and not G.same_bits(got, want, 7):
+            bad = np.nonzero(got != want)[0]
+            errs.append(f"rank {rank}: {bad.size} mismatches, first {bad[:5].tolist()}")
+        for h in hs:
+            comm.deregister_buffer(h)
+        comm.destroy()
+        q.put((rank, errs))
+    except Exception as e:
+        q.put((rank, [f"rank {rank} exception: {e!r}"]))
+
+
+def test_registered_allreduce_fp32_256MiB_n2(built):
+    res = _spawn(_large_worker, 2)
+    bad = [e for r in sorted(res) for e in res[r]]
+    assert not bad, "\n".join(bad)
