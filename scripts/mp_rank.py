@@ -1,7 +1,8 @@
 """One rank of a 2-process AllReduce on the one-GPU box, rendezvous through a file (no launcher, so one
 of the two processes can run under rocprofv3 without any process being spawned from a profiled one).
-usage: mp_rank.py RANK UIDFILE [ITERS] [staged|sym] — rank 1 creates the ncclUniqueId and writes it to
-UIDFILE; `sym` puts both buffers in a symmetric window (zero-copy kernels)."""
+usage: mp_rank.py RANK UIDFILE [ITERS] [staged|sym|reg] — rank 1 creates the ncclUniqueId and writes it to
+UIDFILE; `sym` puts both buffers in a symmetric window, `reg` registers them with ncclCommRegister (zero-copy
+kernels either way)."""
 import os
 import sys
 import time
@@ -40,6 +41,8 @@ def main():
     else:
         x = torch.full((S // 4,), float(rank + 1), device="cuda")
         y = torch.empty_like(x)
+    if mode == "reg":
+        regs = [comm.register_buffer(x.data_ptr(), S), comm.register_buffer(y.data_ptr(), S)]
     s = torch.cuda.current_stream()
     for _ in range(2 + iters):
         comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), S // 4, 7, 0, s.cuda_stream)
@@ -48,6 +51,9 @@ def main():
     print(f"rank {rank}: ok={ok} async={comm.async_error()}", flush=True)
     if mode == "sym":
         comm.deregister_window(win)
+    if mode == "reg":
+        for h in regs:
+            comm.deregister_buffer(h)
     comm.destroy()
     return 0 if ok else 1
 

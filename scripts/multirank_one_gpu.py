@@ -1,5 +1,5 @@
 """Two ranks of one process on the box's one GPU (ncclCommInitAll([0, 0])): the n=2 AllReduce kernels
-(staged direct, symmetric windows, LL) on the metric's 256 MiB fp32 per rank, for rocprofv3 traces.
+(staged direct, symmetric windows, ncclCommRegister'd buffers, LL) on the metric's 256 MiB fp32 per rank, for rocprofv3 traces.
 Every "remote" byte is local HBM here, so this profiles the protocol and the kernels' HBM traffic, not
 xGMI. No process is spawned (safe under rocprofv3)."""
 import json
@@ -18,7 +18,7 @@ MIB = 1 << 20
 
 def main():
     steps = int(os.environ.get("STEPS", "20"))
-    mode = os.environ.get("MODE", "direct")  # direct | sym | ll
+    mode = os.environ.get("MODE", "direct")  # direct | sym | reg | ll
     torch.cuda.set_device(0)
     comms = nccl_amd.Communicator.init_all([0, 0])
     streams = [torch.cuda.Stream(), torch.cuda.Stream()]
@@ -28,6 +28,8 @@ def main():
     if mode == "sym":
         with nccl_amd.group():
             wins = [cm.register_window(b.data_ptr(), 2 * S) for cm, b in zip(comms, bufs)]
+    if mode == "reg":  # ncclCommRegister only: the zero-copy kernel in registered mode (pointer exchange)
+        regs = [cm.register_buffer(b.data_ptr(), 2 * S) for cm, b in zip(comms, bufs)]
     for r, b in enumerate(bufs):
         b[:S].view(torch.float32).fill_(r + 1)
     torch.cuda.synchronize()
@@ -55,6 +57,9 @@ def main():
     if mode == "sym":
         for cm, w in zip(comms, wins):
             cm.deregister_window(w)
+    if mode == "reg":
+        for cm, h in zip(comms, regs):
+            cm.deregister_buffer(h)
     for cm in comms:
         cm.destroy()
     return 0 if ok else 1
