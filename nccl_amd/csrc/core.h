@@ -70,6 +70,18 @@ const char* lastError();
     }                                                                            \
   } while (0)
 
+// roctx range around an API call (NCCL_AMD_ROCTX=1; reference NVTX ranges, src/collectives.cc:134,170)
+extern int gRoctx;
+struct RoctxRange {
+  bool on = false;
+  void push(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+  ~RoctxRange();
+};
+// the arguments are evaluated only when ranges are on
+#define ROCTX_RANGE(...)                  \
+  ::ncclamd::RoctxRange _roctxRange;      \
+  if (::ncclamd::gRoctx) _roctxRange.push(__VA_ARGS__)
+
 // ---------------------------------------------------------------- params (reference src/misc/param.cc)
 int64_t paramInt(const char* name, int64_t deflt);
 const char* paramStr(const char* name);  // nullptr when unset
@@ -110,6 +122,14 @@ struct IpcImport {  // one mapping of a peer's allocation in this process
 };
 struct FdServer;
 bool ipcLegacy();
+struct HipRuntimeInfo {
+  int version;    // hipRuntimeGetVersion of the runtime bound in this process
+  int driver;     // hipDriverGetVersion
+  char path[256]; // the libamdhip64 it lives in (dladdr)
+};
+const HipRuntimeInfo& hipRuntimeInfo();
+// may an allocation of `size` be shared by hipIpc handle on this runtime? (requested: NCCL_AMD_IPC=legacy)
+bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested);
 ncclResult_t ipcServerStart(ncclComm* comm);
 void ipcServerStop(ncclComm* comm);
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d);
@@ -182,6 +202,7 @@ struct CommTuning {
   int forceElementwise;     // NCCL_AMD_FORCE_ELEMENTWISE (diagnostics)
   int protoFlags;           // NCCL_AMD_PROTO_FLAGS | (no release fence before data flags ? 8 : 0) | pulls
   int p2pFence;             // NCCL_AMD_P2P_FENCE: 1 fence, 0 none, -1 unset (none iff all ranks share one GPU)
+  int linkChannels;         // channel budget of large plans at n >= 3 (enqueue.cc linkChannelBudget; 0 = none)
   int algo;                 // NCCL_ALGO: TuneAlgoForce (ONESHOT, DIRECT, RING, TREE)
   int llOn, simpleOn;       // NCCL_PROTO
   int ll128On;              // NCCL_PROTO lists LL128, or NCCL_AMD_LL128=1: the LL64 line protocol (kernels.h)
@@ -203,6 +224,8 @@ struct CommTuning {
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
 void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known
+int linkChannelBudget(int nranks);                  // enqueue.cc: CU budget of large n >= 3 plans
+void resolveLinkChannels(CommTuning* t, int nranks, bool userMaxCTAs);
 
 struct ncclCommImpl;
 }  // namespace ncclamd

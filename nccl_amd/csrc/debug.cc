@@ -3,6 +3,7 @@
 // Reference behaviour: src/debug.cc:45-132 (levels VERSION/WARN/INFO/ABORT/TRACE, NCCL_DEBUG_FILE with
 // %h/%p substitution), src/init.cc:3415-3443 (ncclGetLastError returns the last WARN text),
 // src/misc/param.cc:54-111 (env first, then NCCL_CONF_FILE, ~/.nccl.conf, /etc/nccl.conf).
+#include <dlfcn.h>
 #include <errno.h>
 #include <stdarg.h>
 #include <stdlib.h>
@@ -151,6 +152,48 @@ int64_t paramInt(const char* name, int64_t deflt) {
     return deflt;
   }
   return x;
+}
+
+// ---- roctx ranges (reference: NVTX ranges on the API entry points, src/collectives.cc:134,170,
+// src/include/nvtx.h:125-137; payload = comm hash + message bytes). NCCL_AMD_ROCTX=1 resolves roctxRangePushA /
+// roctxRangePop from rocprofiler-sdk's roctx library (the one rocprofv3 --marker-trace records; roctracer's
+// libroctx64 as a fallback) at the first range; off, a range costs one load and branch.
+int gRoctx = getenv("NCCL_AMD_ROCTX") && atoi(getenv("NCCL_AMD_ROCTX")) ? -1 : 0;  // -1: asked for, unresolved
+static int (*gRangePush)(const char*) = nullptr;
+static int (*gRangePop)() = nullptr;
+
+static void roctxResolve() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    for (const char* lib : {"librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so", "libroctx64.so.4"}) {
+      void* h = dlopen(lib, RTLD_NOW | RTLD_GLOBAL);
+      if (!h) continue;
+      gRangePush = (int (*)(const char*))dlsym(h, "roctxRangePushA");
+      gRangePop = (int (*)())dlsym(h, "roctxRangePop");
+      if (gRangePush && gRangePop) {
+        INFO("NCCL_AMD_ROCTX: roctx ranges through %s", lib);
+        break;
+      }
+    }
+    if (!gRangePush || !gRangePop) WARN("NCCL_AMD_ROCTX=1 but no roctx library could be loaded; no ranges");
+    __atomic_store_n(&gRoctx, gRangePush && gRangePop ? 1 : 0, __ATOMIC_RELEASE);
+  });
+}
+
+void RoctxRange::push(const char* fmt, ...) {
+  if (gRoctx < 0) roctxResolve();
+  on = gRoctx > 0;
+  if (!on) return;
+  char msg[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof(msg), fmt, ap);
+  va_end(ap);
+  gRangePush(msg);
+}
+
+RoctxRange::~RoctxRange() {
+  if (on) gRangePop();
 }
 
 }  // namespace ncclamd

@@ -146,6 +146,29 @@ void loadTuning(CommTuning* t) {
   t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);
 }
 
+// CU budget of the large staged and zero-copy plans at n >= 3 (reference: channels and threads shrink below
+// saturation, enqueue.cc:2091-2105; tuning.cc:243-400). The links bound those plans on the 8-GPU node: a rank
+// sends 2S/n over each of its n-1 links, taking 2S/n / B_link, while its local HBM moves (2 + 4(n-1)/n) S
+// (staged path), so keeping the links busy takes (3n - 2) B_link of HBM copy traffic, and a
+// workgroup copies at most R_cu ≈ 50 GB/s (profiles/r02_wg_rate_probe.txt). With B_link ≈ 64 GB/s per
+// direction and 2x headroom, rounded up to a power of two (>= 32): 32 channels at n = 3..4, 64 at n = 5..8 —
+// the rest of the chip stays free for the compute a collective overlaps. n = 2 keeps every channel (one link,
+// nothing to overlap in the bench). NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS / config.maxCTAs overrule it, as does
+// NCCL_AMD_LINK_CHANNELS (0 = no budget).
+int linkChannelBudget(int n) {
+  if (n < 3) return 0;
+  const double bLinkGBps = 64.0, cuGBps = 50.0, headroom = 2.0;
+  const double need = (3.0 * n - 2.0) * bLinkGBps / cuGBps * headroom;
+  int c = 32;
+  while (c < need && c < NCCL_AMD_MAX_CHANNELS) c *= 2;
+  return c;
+}
+
+void resolveLinkChannels(CommTuning* t, int nranks, bool userMaxCTAs) {
+  const int64_t env = paramInt("NCCL_AMD_LINK_CHANNELS", -1);
+  t->linkChannels = env >= 0 ? (int)env : userMaxCTAs ? 0 : linkChannelBudget(nranks);
+}
+
 // The fence default once the ranks' devices are known (all ranks see the same peer table and rank 0's knobs).
 void resolveFence(CommTuning* t, bool oneDevice) {
   if (t->p2pFence < 0 && oneDevice) t->protoFlags |= 8;
@@ -517,6 +540,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       } else {
         sp.coll = info.func == FUNC_REDUCESCATTER ? 2 /*SYM_RS*/ : 3 /*SYM_AG*/;
       }
+      if (n >= 3 && comm->tune.linkChannels > 0) maxCh = std::min(maxCh, comm->tune.linkChannels);  // CU budget
       int nch = (int)((spanBytes + minPart - 1) / minPart);
       if (nch < comm->minCTAs) nch = comm->minCTAs;
       if (nch > maxCh) nch = maxCh;
@@ -539,7 +563,9 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     planChannels(comm, count * ts, ts, p, minPart, 32);
   } else {
     size_t minPart = tunedNch > 0 ? (blockElems * ts + tunedNch - 1) / tunedNch : (size_t)comm->tune.minChannelBytes;
-    planChannels(comm, blockElems * ts, ts, p, minPart, comm->chanCap);
+    int maxCh = comm->chanCap;
+    if (n >= 3 && comm->tune.linkChannels > 0 && tunedNch == 0) maxCh = std::min(maxCh, comm->tune.linkChannels);
+    planChannels(comm, blockElems * ts, ts, p, minPart, maxCh);
   }
   TRACE("%s: count %zu dt %d op %d -> nch %d part %lu slice %lu steps %d aligned %d", info.opName, count,
         (int)info.datatype, (int)info.op, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,
@@ -670,6 +696,9 @@ ncclResult_t collJoin(const CollInfo& info) {
 
 ncclResult_t enqueueCheck(CollInfo* info) {
   logInit();
+  // reference NVTX payload (collectives.cc:134,170): the comm and the message size
+  ROCTX_RANGE("nccl%s comm=%p count=%zu datatype=%d op=%d root=%d", info->opName, (void*)info->comm, info->count,
+              (int)info->datatype, (int)info->op, info->root);
   ncclResult_t ret = commCheck(info->comm, info->opName, "comm");
   if (ret != ncclSuccess) {
     groupRecordError(ret);

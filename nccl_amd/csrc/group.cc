@@ -185,10 +185,16 @@ ncclResult_t groupEndInternal(ncclSimInfo_t* simInfo) {
 
 using namespace ncclamd;
 
-NCCL_EXPORT ncclResult_t ncclGroupStart() { return groupStartInternal(); }
+NCCL_EXPORT ncclResult_t ncclGroupStart() {
+  ROCTX_RANGE("ncclGroupStart");
+  return groupStartInternal();
+}
 extern "C" __attribute__((visibility("default"), alias("ncclGroupStart"))) ncclResult_t pncclGroupStart();
 
-NCCL_EXPORT ncclResult_t ncclGroupEnd() { return groupEndInternal(nullptr); }
+NCCL_EXPORT ncclResult_t ncclGroupEnd() {
+  ROCTX_RANGE("ncclGroupEnd");
+  return groupEndInternal(nullptr);
+}
 extern "C" __attribute__((visibility("default"), alias("ncclGroupEnd"))) ncclResult_t pncclGroupEnd();
 
 NCCL_EXPORT ncclResult_t ncclGroupSimulateEnd(ncclSimInfo_t* simInfo) { return groupEndInternal(simInfo); }

@@ -69,10 +69,14 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   // reference env names (env.rst :884/:901): NCCL_MIN/MAX_CTAS, or the older NCCL_MIN/MAX_NCHANNELS
   c->minCTAs = (int)paramInt("NCCL_MIN_CTAS", paramInt("NCCL_MIN_NCHANNELS", 1));
   c->maxCTAs = (int)paramInt("NCCL_MAX_CTAS", paramInt("NCCL_MAX_NCHANNELS", 256));
+  bool userMax = paramStr("NCCL_MAX_CTAS") != nullptr || paramStr("NCCL_MAX_NCHANNELS") != nullptr;
   if (cfg) {
     if (cfg->blocking != NCCL_CONFIG_UNDEF_INT) c->blocking = cfg->blocking != 0;
     if (cfg->minCTAs != NCCL_CONFIG_UNDEF_INT) c->minCTAs = cfg->minCTAs;
-    if (cfg->maxCTAs != NCCL_CONFIG_UNDEF_INT) c->maxCTAs = cfg->maxCTAs;
+    if (cfg->maxCTAs != NCCL_CONFIG_UNDEF_INT) {
+      c->maxCTAs = cfg->maxCTAs;
+      userMax = true;
+    }
     if (cfg->commName) c->commName = cfg->commName;
   }
   if (c->maxCTAs < 1) c->maxCTAs = 1;
@@ -81,6 +85,7 @@ static void commDefaults(ncclComm* c, int rank, int nranks, int dev, const ncclC
   if (c->minCTAs > c->maxCTAs) c->minCTAs = c->maxCTAs;
   c->maxChannels = c->maxCTAs;
   loadTuning(&c->tune);
+  resolveLinkChannels(&c->tune, nranks, userMax);
   c->nSlots = (int)paramInt("NCCL_AMD_NSLOTS", 2);
   if (c->nSlots < 1) c->nSlots = 1;
   // Slot size: the staging slab (maxChannels x 2 kinds x nSlots x nRanks x slot) is sized to a fixed
@@ -153,6 +158,20 @@ static void computeChannelCap(ncclComm* c) {
   resolveFence(&c->tune, oneDevice);
 }
 
+// Which HIP runtime this process bound (reference: init-time INFO lines, src/init.cc:1831-1968): in a torch
+// process it is torch's bundled libamdhip64, not the one the library was built against (ipc.cc).
+static void logRuntimeOnce() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const HipRuntimeInfo& rt = hipRuntimeInfo();
+    INFO("HIP runtime %d.%d.%d (driver %d) from %s; built against HIP %d.%d", rt.version / 10000000,
+         rt.version / 100000 % 100, rt.version % 100000, rt.driver, rt.path, HIP_VERSION_MAJOR, HIP_VERSION_MINOR);
+    if (rt.version / 100000 != HIP_VERSION_MAJOR * 100 + HIP_VERSION_MINOR)
+      INFO("HIP runtime differs from the build's (%d.%d): dma-buf IPC is used, legacy hipIpc handles only on 7.2+",
+           HIP_VERSION_MAJOR, HIP_VERSION_MINOR);
+  });
+}
+
 // Shape parameters every rank must agree on (exchanged with the PeerInfo block).
 struct ShapeInfo {
   int maxChannels, minChannels, nSlots;
@@ -200,6 +219,7 @@ static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id
   if ((res = tunerLoad(comm)) != ncclSuccess) goto fail;
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
   unexportHandles(comm);  // every peer has mapped our slab and flags
+  logRuntimeOnce();
   INFO("comm %p rank %d nRanks %d dev %d busId %s - Init COMPLETE", (void*)comm, rank, nranks, dev,
        comm->peers[rank].busId);
   return ncclSuccess;
@@ -305,6 +325,7 @@ NCCL_EXPORT ncclResult_t ncclCommInitRankConfig(ncclComm_t* newcomm, int nranks,
 NCCL_ALIAS(ncclResult_t, ncclCommInitRankConfig, ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*)
 
 NCCL_EXPORT ncclResult_t ncclCommInitRank(ncclComm_t* newcomm, int nranks, ncclUniqueId commId, int myrank) {
+  ROCTX_RANGE("ncclCommInitRank nranks=%d rank=%d", nranks, myrank);
   return initRankCommon(newcomm, nranks, commId, myrank, nullptr);
 }
 NCCL_ALIAS(ncclResult_t, ncclCommInitRank, ncclComm_t*, int, ncclUniqueId, int)
@@ -331,6 +352,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommInitRankScalable, ncclComm_t*, int, int, int, n
 // no socket rendezvous is needed (reference init.cc:2581-2643 runs the generic path in threads).
 NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
   logInit();
+  ROCTX_RANGE("ncclCommInitAll ndev=%d", ndev);
   if (comms == nullptr) {
     WARN("CommInitAll : comms argument is NULL");
     return ncclInvalidArgument;
@@ -389,6 +411,7 @@ NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
     cs[i]->clique = clique;
     comms[i] = cs[i];
   }
+  logRuntimeOnce();
   INFO("ncclCommInitAll COMPLETE: %d ranks", ndev);
   return ncclSuccess;
 }

@@ -17,6 +17,7 @@
 //
 // Every socket operation is bounded (NCCL_AMD_IPC_TIMEOUT_MS): an import whose exporter died or never
 // published returns ncclSystemError / ncclRemoteError rather than blocking the caller.
+#include <dlfcn.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <poll.h>
@@ -242,23 +243,41 @@ void ipcServerStop(ncclComm* comm) {
   comm->fdServer = nullptr;
 }
 
-static int runtimeVersion() {
-  int v = 0;
-  (void)hipRuntimeGetVersion(&v);
-  return v;  // major * 10000000 + minor * 100000 + patch
+// The HIP runtime this library is actually bound to. Inside any process that imports torch that is torch's
+// bundled libamdhip64 (ROCm 7.0 in this image, same soname, loaded first), not the /opt/rocm 7.2 runtime the
+// library was built against: found with dladdr on a runtime entry point, logged once at
+// the first communicator init (NCCL_DEBUG=INFO) so a runtime-specific defect is attributable.
+const HipRuntimeInfo& hipRuntimeInfo() {
+  static HipRuntimeInfo info = [] {
+    HipRuntimeInfo r = {};
+    (void)hipRuntimeGetVersion(&r.version);  // major * 10000000 + minor * 100000 + patch
+    (void)hipDriverGetVersion(&r.driver);
+    Dl_info dl;
+    if (dladdr((void*)&hipRuntimeGetVersion, &dl) && dl.dli_fname) snprintf(r.path, sizeof(r.path), "%s", dl.dli_fname);
+    else snprintf(r.path, sizeof(r.path), "?");
+    return r;
+  }();
+  return info;
 }
 
-// torch's bundled ROCm 7.0 runtime never returns from hipIpcOpenMemHandle at 2 GiB or more (ipc.cc header)
-static bool legacyOpenable(size_t size) { return size < ((size_t)2 << 30) || runtimeVersion() >= 70200000; }
+// NCCL_AMD_IPC=legacy (hipIpc handles): torch's bundled ROCm 7.0 runtime never returns from
+// hipIpcOpenMemHandle for allocations of 2 GiB or more, and this engine's slabs, windows and
+// registered buffers can reach that size at any time, so legacy handles are refused on runtimes older than
+// 7.2 whatever the size. Without NCCL_AMD_IPC=legacy a hipIpc handle only rides along a dma-buf export as the
+// importer's fallback, and only where it is known to open: below 2 GiB, or on a 7.2+ runtime.
+bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested) {
+  if (runtimeVersion >= 70200000) return true;
+  return !requested && size < ((size_t)2 << 30);
+}
 
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
   memset(d, 0, sizeof(*d));
   d->size = size;
   if (ipcLegacy()) {
-    if (!legacyOpenable(size)) {
-      // torch's bundled ROCm 7.0 runtime never returns from hipIpcOpenMemHandle at this size (ipc.cc header)
-      WARN("ipc: a %zu MiB allocation cannot be shared with NCCL_AMD_IPC=legacy on HIP runtime %d "
-           "(hipIpcOpenMemHandle stalls at >= 2 GiB); use the default dma-buf path", size >> 20, runtimeVersion());
+    const HipRuntimeInfo& rt = hipRuntimeInfo();
+    if (!ipcLegacyAllowed(rt.version, size, true)) {
+      WARN("ipc: NCCL_AMD_IPC=legacy refused on HIP runtime %d (%s): its hipIpcOpenMemHandle stalls on "
+           "allocations of 2 GiB or more; use the default dma-buf path", rt.version, rt.path);
       return ncclSystemError;
     }
     d->legacy = 1;
@@ -275,7 +294,7 @@ ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
   // A hipIpc handle rides along where the runtime can open it (below 2 GiB, or a 7.2+ runtime): an importer
   // whose runtime cannot map the dma-buf (never seen on one GPU; the first multi-GPU node decides) falls back
   // to it with a warning instead of failing the communicator.
-  if (legacyOpenable(size) && !paramInt("NCCL_AMD_IPC_NO_FALLBACK", 0)) {
+  if (ipcLegacyAllowed(hipRuntimeInfo().version, size, false) && !paramInt("NCCL_AMD_IPC_NO_FALLBACK", 0)) {
     if (hipIpcGetMemHandle(&d->handle, base) == hipSuccess) d->hasHandle = 1;
     else (void)hipGetLastError();
   }

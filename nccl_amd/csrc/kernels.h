@@ -45,6 +45,17 @@ constexpr int kThreads = 512;  // 8 waves of 64 per channel workgroup
 // compiler hold that budget (tests/test_occupancy.py checks the build's resource report).
 #define kCoResident __attribute__((amdgpu_waves_per_eu(4)))
 
+// NCCL_AMD_KERNEL_LOG=<path>: each distinct kernel this process launches is named once in that file
+// ("<kernel> grid=<workgroups> block=<threads>", kernels.hip kernelLogNote) — how bench.py names the kernel
+// its roofline measures, from the run itself. Off: one predictable branch per launch.
+extern bool gKernelLog;
+void kernelLogNote(const void* fn, unsigned grid, unsigned block);
+#define NCCL_AMD_LAUNCH(K, G, B, SH, ST, ...)                                                  \
+  do {                                                                                          \
+    if (::ncclamd::gKernelLog) ::ncclamd::kernelLogNote((const void*)(K), (G).x, (B).x);      \
+    hipLaunchKernelGGL(K, G, B, SH, ST, __VA_ARGS__);                                           \
+  } while (0)
+
 // ------------------------------------------------------------------------------------ primitives
 
 __device__ __forceinline__ uint64_t clockTicks() { return __builtin_amdgcn_s_memrealtime(); }
@@ -1330,10 +1341,10 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
 template <typename T, int OP>
 inline ncclResult_t launchSymTyped(const SymPlan& p) {
   switch (p.coll) {
-    case SYM_AR: hipLaunchKernelGGL((symKernel<T, OP, SYM_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
-    case SYM_AR1: hipLaunchKernelGGL((symKernel<T, OP, SYM_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
-    case SYM_RS: hipLaunchKernelGGL((symKernel<T, OP, SYM_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
-    case SYM_AG: hipLaunchKernelGGL((symKernel<T, 0, SYM_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+    case SYM_AR: NCCL_AMD_LAUNCH((symKernel<T, OP, SYM_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+    case SYM_AR1: NCCL_AMD_LAUNCH((symKernel<T, OP, SYM_AR1>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+    case SYM_RS: NCCL_AMD_LAUNCH((symKernel<T, OP, SYM_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+    case SYM_AG: NCCL_AMD_LAUNCH((symKernel<T, 0, SYM_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
   }
   HIPCHECK(hipGetLastError());
   return ncclSuccess;
@@ -1405,9 +1416,9 @@ inline void launchLLK(const LaunchPlan& p) {
   a.nOps = p.ll.nOps;
   for (int k = 0; k < p.ll.nOps && k < K; k++) a.ops[k] = p.ll.ops[k];
   if (p.ll.ops[0].proto == LLP_LL64)
-    hipLaunchKernelGGL((llKernel<T, OP, K, LLP_LL64>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
+    NCCL_AMD_LAUNCH((llKernel<T, OP, K, LLP_LL64>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
   else
-    hipLaunchKernelGGL((llKernel<T, OP, K, LLP_LL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
+    NCCL_AMD_LAUNCH((llKernel<T, OP, K, LLP_LL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, a);
 }
 template <typename T, int OP>
 inline void launchLL(const LaunchPlan& p) {
@@ -1420,9 +1431,9 @@ inline void launchLL(const LaunchPlan& p) {
 template <typename T, int OP, int COLL>
 inline void launchColl(const LaunchPlan& p) {
   if (p.batch.nOps > 1)
-    hipLaunchKernelGGL((collBatchKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.batch);
+    NCCL_AMD_LAUNCH((collBatchKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.batch);
   else
-    hipLaunchKernelGGL((collKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+    NCCL_AMD_LAUNCH((collKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
 }
 
 template <typename T, int OP>
@@ -1433,18 +1444,18 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
     const uint64_t units = aligned ? (p.args.count + kTile - 1) / kTile : (p.args.count + 255) / 256;
     int grid = (int)std::min<uint64_t>(aligned ? (1u << 20) : 1024, units);
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((oneRankKernel<T, OP>), dim3(grid), dim3(256), 0, p.stream, (T*)p.args.recvbuff,
+    NCCL_AMD_LAUNCH((oneRankKernel<T, OP>), dim3(grid), dim3(256), 0, p.stream, (T*)p.args.recvbuff,
                        (const T*)p.args.sendbuff, p.args.count, p.args.redArg, p.args.redArgPtr, aligned);
     HIPCHECK(hipGetLastError());
     return ncclSuccess;
   }
   if (p.algo == ALGO_PIPE) {  // ring / chain (pipe.h); AllGather is type-erased (launchKernGather)
     switch (p.pipeKind) {
-      case PIPE_RING_AR: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_RING_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
-      case PIPE_RING_RS: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_RING_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
-      case PIPE_RING_AG: hipLaunchKernelGGL((pipeKernel<T, 0, PIPE_RING_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
-      case PIPE_CHAIN_AR: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_CHAIN_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
-      case PIPE_CHAIN_REDUCE: hipLaunchKernelGGL((pipeKernel<T, OP, PIPE_CHAIN_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_RING_AR: NCCL_AMD_LAUNCH((pipeKernel<T, OP, PIPE_RING_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_RING_RS: NCCL_AMD_LAUNCH((pipeKernel<T, OP, PIPE_RING_RS>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_RING_AG: NCCL_AMD_LAUNCH((pipeKernel<T, 0, PIPE_RING_AG>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_CHAIN_AR: NCCL_AMD_LAUNCH((pipeKernel<T, OP, PIPE_CHAIN_AR>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
+      case PIPE_CHAIN_REDUCE: NCCL_AMD_LAUNCH((pipeKernel<T, OP, PIPE_CHAIN_REDUCE>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args); break;
       default: return ncclInternalError;
     }
     HIPCHECK(hipGetLastError());

@@ -1,5 +1,10 @@
 // kernels.hip — nRanks==1 streaming copy kernels and the host-side launch dispatch.
 // The collective kernels (kernels.h) are instantiated per element type in kern_<type>.hip.
+#include <cxxabi.h>
+
+#include <mutex>
+#include <set>
+
 #include "kernels.h"
 
 namespace ncclamd {
@@ -42,6 +47,25 @@ ncclResult_t warmKernels() {
                            warmKernF32, warmKernF64, warmKernFp8, warmKernGather};
   for (auto f : fns) HIPCHECK(f());
   return ncclSuccess;
+}
+
+// ------------------------------------------------------------------------------------ kernel log
+
+bool gKernelLog = getenv("NCCL_AMD_KERNEL_LOG") != nullptr;
+
+void kernelLogNote(const void* fn, unsigned grid, unsigned block) {
+  static std::mutex mu;
+  static std::set<std::pair<const void*, unsigned>> seen;
+  std::lock_guard<std::mutex> g(mu);
+  if (!seen.insert({fn, grid}).second) return;
+  const char* raw = hipKernelNameRefByPtr(fn, nullptr);
+  int st = -1;
+  char* dem = raw ? abi::__cxa_demangle(raw, nullptr, nullptr, &st) : nullptr;
+  if (FILE* f = fopen(getenv("NCCL_AMD_KERNEL_LOG"), "a")) {
+    fprintf(f, "%s grid=%u block=%u\n", st == 0 && dem ? dem : raw ? raw : "?", grid, block);
+    fclose(f);
+  }
+  free(dem);
 }
 
 // ------------------------------------------------------------------------------------ nRanks == 1
@@ -96,29 +120,29 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
       u32x4* d = (u32x4*)dst;
       const u32x4* s = (const u32x4*)src;
       switch (var) {
-        case 1: hipLaunchKernelGGL((copyKernel<4, false, -2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 2: hipLaunchKernelGGL((copyKernel<4, false, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 3: hipLaunchKernelGGL((copyKernel<8, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 5: hipLaunchKernelGGL((copyKernel<4, true, 16>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 6: hipLaunchKernelGGL((copyKernel<4, true, 18>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 7: hipLaunchKernelGGL((copyKernel<4, true, 2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 8: hipLaunchKernelGGL((copyKernel<4, true, 0>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 9: hipLaunchKernelGGL((copyKernel<4, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 4: hipLaunchKernelGGL((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        default: hipLaunchKernelGGL((copyKernel<2, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 1: NCCL_AMD_LAUNCH((copyKernel<4, false, -2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 2: NCCL_AMD_LAUNCH((copyKernel<4, false, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 3: NCCL_AMD_LAUNCH((copyKernel<8, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 5: NCCL_AMD_LAUNCH((copyKernel<4, true, 16>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 6: NCCL_AMD_LAUNCH((copyKernel<4, true, 18>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 7: NCCL_AMD_LAUNCH((copyKernel<4, true, 2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 8: NCCL_AMD_LAUNCH((copyKernel<4, true, 0>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 9: NCCL_AMD_LAUNCH((copyKernel<4, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 4: NCCL_AMD_LAUNCH((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        default: NCCL_AMD_LAUNCH((copyKernel<2, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
       }
       HIPCHECK(hipGetLastError());
     }
     uint64_t done = npk << 4;
     if (done < bytes) {
-      hipLaunchKernelGGL(copyBytesKernel, dim3(1), dim3(64), 0, stream, (char*)dst + done, (const char*)src + done,
+      NCCL_AMD_LAUNCH(copyBytesKernel, dim3(1), dim3(64), 0, stream, (char*)dst + done, (const char*)src + done,
                          (uint64_t)(bytes - done));
       HIPCHECK(hipGetLastError());
     }
     return ncclSuccess;
   }
   int grid = (int)std::min<uint64_t>(2048, (bytes + 255) / 256);
-  hipLaunchKernelGGL(copyBytesKernel, dim3(grid), dim3(256), 0, stream, (char*)dst, (const char*)src, (uint64_t)bytes);
+  NCCL_AMD_LAUNCH(copyBytesKernel, dim3(grid), dim3(256), 0, stream, (char*)dst, (const char*)src, (uint64_t)bytes);
   HIPCHECK(hipGetLastError());
   return ncclSuccess;
 }

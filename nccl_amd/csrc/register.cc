@@ -357,6 +357,7 @@ NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, siz
   }
   int st = comm->asyncResult.load();
   if (st != ncclSuccess) return st == ncclInProgress ? ncclInProgress : ncclInvalidUsage;
+  ROCTX_RANGE("ncclCommRegister comm=%p size=%zu", (void*)comm, size);
   RegHandle* h = new RegHandle{buff, size, nullptr};
   // NCCL_LOCAL_REGISTER=0: the handle only records the buffer (reference register.cc:156-159 returns NULL;
   // a handle is kept here so that ncclCommDeregister of it stays valid)

@@ -108,6 +108,28 @@ int main(int argc, char** argv) {
   ipcUnexport(comm, db);
   CHECK(ipcFetchFd(db, &fd) == ncclRemoteError);  // retired: refused, not served stale
 
+  // 3b. the registration requests (register.cc): a RELEASE of a mapping the server does not hold is a no-op
+  // success, an IMPORT without a descriptor attached is refused (status != 0 -> ncclRemoteError), neither
+  // touches the GPU; fetches keep working around them
+  ipcRemoteRelease(da.server, 3, 0x1234);
+  uint64_t addr = 0;
+  CHECK(ipcRemoteImport(da.server, 3, 0x1234, -1, 4096, &addr) == ncclRemoteError && addr == 0);
+  CHECK(ipcRemoteImport(nowhere.server, 3, 0x1234, -1, 4096, &addr) == ncclRemoteError);
+  fd = -1;
+  CHECK(ipcFetchFd(da, &fd) == ncclSuccess && readsBack(fd, 'a', kSize));
+  if (fd >= 0) close(fd);
+  // server names carry a random nonce besides pid and serial (pid reuse across PID namespaces)
+  CHECK(strlen(da.server) > strlen("ncclamd.") + 8);
+
+  // 3c. legacy hipIpc handles (NCCL_AMD_IPC=legacy) are refused on runtimes older than 7.2 at any size; a
+  // fallback handle rides along a dma-buf export below 2 GiB there, at any size on 7.2+
+  CHECK(!ipcLegacyAllowed(70051831, 4096, true));
+  CHECK(!ipcLegacyAllowed(70051831, (size_t)3 << 30, true));
+  CHECK(ipcLegacyAllowed(70200000, (size_t)3 << 30, true));
+  CHECK(ipcLegacyAllowed(70051831, 4096, false));
+  CHECK(!ipcLegacyAllowed(70051831, (size_t)2 << 30, false));
+  CHECK(ipcLegacyAllowed(70253211, (size_t)2 << 30, false));
+
   // 4. stop while clients fetch
   std::atomic<int> finished{0};
   std::vector<std::thread> late;

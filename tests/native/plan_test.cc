@@ -94,6 +94,7 @@ int main(int argc, char** argv) {
   comm.chanCap = !batch && argc > 6 ? atoi(argv[6]) : 256;
   comm.devComm = (DevComm*)0x1000;
   loadTuning(&comm.tune);
+  resolveLinkChannels(&comm.tune, n, getenv("NCCL_MAX_CTAS") != nullptr);
   if (batch) {
     // the group.cc loop: plan in order, extend the open run while batchable, else launch it
     gBatchMode = true;

@@ -237,3 +237,20 @@ def test_ll128_class_protocol(exe):
         p = plan(exe, 3, "ar", 7, count, NCCL_PROTO="LL128", NCCL_AMD_LL128_CHANNEL_BYTES=56)
         lines = -(-count * 4 // 56)
         assert (p["nch"] - 1) * p["part"] < lines <= p["nch"] * p["part"]
+
+
+@pytest.mark.parametrize("n,want", [(2, 256), (3, 32), (4, 32), (5, 64), (8, 64)])
+def test_link_channel_budget(exe, n, want):
+    """large staged plans at n >= 3 take a CU budget from the link cost model
+    (enqueue.cc linkChannelBudget: (3n-2) x 64 GB/s of HBM copy traffic / 50 GB/s per workgroup x 2, rounded
+    up to a power of two >= 32) instead of every channel; n = 2 keeps all of them."""
+    assert plan(exe, n, "ar", 7, (256 << 20) // 4)["nch"] == want
+    if n >= 3:
+        assert plan(exe, n, "rs", 9, (1 << 30) // 2 // n)["nch"] == want        # C3's ReduceScatter
+        assert plan(exe, n, "ag", 9, (1 << 30) // 2 // n)["nch"] == want        # and AllGather
+        # NCCL_MAX_CTAS (reference env.rst:901) or NCCL_AMD_LINK_CHANNELS overrule the budget
+        assert plan(exe, n, "ar", 7, (256 << 20) // 4, NCCL_MAX_CTAS=256)["nch"] == 256
+        assert plan(exe, n, "ar", 7, (256 << 20) // 4, NCCL_AMD_LINK_CHANNELS=0)["nch"] == 256
+        assert plan(exe, n, "ar", 7, (256 << 20) // 4, NCCL_AMD_LINK_CHANNELS=16)["nch"] == 16
+        # the co-residency cap still applies below the budget (several ranks per GPU)
+        assert plan(exe, n, "ar", 7, (256 << 20) // 4, chancap=24)["nch"] == 24
