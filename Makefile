@@ -22,7 +22,8 @@ DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test xgmi-probe atomicity-probe
+all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test xgmi-probe atomicity-probe \
+     fp8-probe
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -147,3 +148,12 @@ tests/native/store_atomicity_probe: tests/native/store_atomicity_probe.hip
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -o $@ $<
 
 .PHONY: atomicity-probe
+
+# fp8 conversion probe: gfx950's fp8 convert instructions vs numerics.h's software conversions, every code and
+# every half value (GPU test tests/test_gpu_numerics.py; decides the hardware fp8 path)
+fp8-probe: tests/native/fp8_cvt_probe
+
+tests/native/fp8_cvt_probe: tests/native/fp8_cvt_probe.hip $(SRCDIR)/numerics.h
+	$(HIPCC) -O3 --offload-arch=$(ARCH) -ffp-contract=off -fno-gpu-flush-denormals-to-zero -o $@ $<
+
+.PHONY: fp8-probe

@@ -220,6 +220,17 @@ constexpr int kCopyUnroll = NCCL_AMD_COPY_UNROLL;
 #define NCCL_AMD_FOLD_UNROLL 4
 #endif
 constexpr int kFoldUnroll = NCCL_AMD_FOLD_UNROLL;
+#ifndef NCCL_AMD_FOLD_UNROLL_SWAR
+#define NCCL_AMD_FOLD_UNROLL_SWAR 2
+#endif
+#ifndef NCCL_AMD_FOLD_UNROLL_1B
+#define NCCL_AMD_FOLD_UNROLL_1B 1
+#endif
+constexpr int kFoldUnrollSwar = NCCL_AMD_FOLD_UNROLL_SWAR;
+constexpr int kFoldUnroll1B = NCCL_AMD_FOLD_UNROLL_1B;
+#ifndef NCCL_AMD_FOLD_REPACK
+#define NCCL_AMD_FOLD_REPACK 0
+#endif
 
 // Copy [0,nbytes) from src to dst. Both 16-byte aligned when `aligned`; nbytes multiple of sizeof(T).
 template <typename T, bool REMOTE>
@@ -293,7 +304,7 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
   // separate registers, so they keep one pack per batch to stay within the register budget (kCoResident;
   // two packs spilled up to 55 VGPRs for fp8)
   constexpr bool kSwar = std::is_same<T, uint8_t>::value && Swar8<OP>::ok;
-  constexpr int U = sizeof(T) > 1 ? kFoldUnroll : kSwar ? 2 : 1;
+  constexpr int U = sizeof(T) > 1 ? kFoldUnroll : kSwar ? kFoldUnrollSwar : kFoldUnroll1B;
   uint32_t swarMask = 0;
   if constexpr (kSwar) swarMask = (uint32_t)(uint8_t)fn.arg * 0x01010101u;
   if (aligned) {
@@ -325,6 +336,8 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
               T x = fn.pre(cur[u].e[e]);
               acc[u].e[e] = k == 0 ? x : fn.red(x, acc[u].e[e]);
             }
+            // 1-byte types: keep the accumulator packed between sources (4 registers, not 16 unpacked bytes)
+            if constexpr (sizeof(T) == 1 && NCCL_AMD_FOLD_REPACK) asm volatile("" : "+v"(acc[u].v));
           }
           cur[u] = nxt[u];
         }

@@ -95,6 +95,33 @@ __host__ __device__ inline uint8_t f32ToFp8Sat(float f) {
   return sign | (uint8_t)code;
 }
 
+// ---- fp8 through gfx950's convert instructions (device only) ----
+// v_cvt_f32_fp8 / _bf8 decode one OCP code exactly; v_cvt_pk_fp8_f32 / _bf8_f32 encode with round to nearest
+// even. tests/native/fp8_cvt_probe (GPU test tests/test_gpu_numerics.py) checks these two functions against the
+// software ones above for every code and every half value: they differ only in NaN sign handling (the hardware
+// decodes 0x7f as a negative NaN and encodes every NaN as 0xff), so NaN takes the software result; saturation
+// (__NV_SATFINITE) is a clamp to +-max finite before the round, exact because the input is a half value (fromF
+// rounds to half first). Each replaces ~20 integer ops of the software conversion by one instruction.
+#ifndef NCCL_AMD_HW_FP8
+#define NCCL_AMD_HW_FP8 1
+#endif
+#if defined(__HIP__)  // HIP compilations only (the host-only numerics test build is plain C++)
+template <bool E5M2>
+__device__ inline float fp8ToF32Hw(uint8_t v) {
+  const float f = E5M2 ? __builtin_amdgcn_cvt_f32_bf8((int)v, 0) : __builtin_amdgcn_cvt_f32_fp8((int)v, 0);
+  const bool nan = E5M2 ? ((v & 0x7c) == 0x7c && (v & 3) != 0) : ((v & 0x7f) == 0x7f);
+  return nan ? u32AsF32(((uint32_t)(v & 0x80) << 24) | 0x7fc00000u) : f;
+}
+template <bool E5M2>
+__device__ inline uint8_t f32ToFp8SatHw(float f) {  // f must be a half value
+  if (f != f) return (uint8_t)(((f32AsU32(f) >> 24) & 0x80) | 0x7f);
+  const float mx = E5M2 ? 57344.0f : 448.0f;
+  const float x = __builtin_fminf(__builtin_fmaxf(f, -mx), mx);
+  const int r = E5M2 ? __builtin_amdgcn_cvt_pk_bf8_f32(x, x, 0, false) : __builtin_amdgcn_cvt_pk_fp8_f32(x, x, 0, false);
+  return (uint8_t)(r & 0xff);
+}
+#endif
+
 // ---- min/max with a defined signed-zero order ----
 // The reference uses fminf/fmaxf (reduce_kernel.h:409-410) and __hmin/__hmax: NaN-ignoring, but the
 // result for (+0, -0) is implementation-defined in C. Here -0 orders below +0 (IEEE 754-2019
@@ -135,16 +162,32 @@ template <> struct Traits<bf16_t> {
   __host__ __device__ static float toF(bf16_t v) { return bf16ToF32(v.x); }
   __host__ __device__ static bf16_t fromF(float f) { return bf16_t{f32ToBf16(f)}; }
 };
+template <bool E5M2>
+__host__ __device__ inline float fp8Decode(uint8_t v) {
+#if defined(__HIP_DEVICE_COMPILE__) && NCCL_AMD_HW_FP8
+  return fp8ToF32Hw<E5M2>(v);
+#else
+  return fp8ToF32<E5M2>(v);
+#endif
+}
+// the reference's fp8 ops run on __half and convert back with saturation: round to half first
+template <bool E5M2>
+__host__ __device__ inline uint8_t fp8Encode(float f) {
+#if defined(__HIP_DEVICE_COMPILE__) && NCCL_AMD_HW_FP8
+  return f32ToFp8SatHw<E5M2>(halfToF32(f32ToHalf(f)));
+#else
+  return f32ToFp8Sat<E5M2>(halfToF32(f32ToHalf(f)));
+#endif
+}
 template <> struct Traits<e4m3_t> {
   static constexpr bool isFloat = true;
-  __host__ __device__ static float toF(e4m3_t v) { return fp8ToF32<false>(v.x); }
-  // the reference's fp8 ops run on __half and convert back with saturation: round to half first
-  __host__ __device__ static e4m3_t fromF(float f) { return e4m3_t{f32ToFp8Sat<false>(halfToF32(f32ToHalf(f)))}; }
+  __host__ __device__ static float toF(e4m3_t v) { return fp8Decode<false>(v.x); }
+  __host__ __device__ static e4m3_t fromF(float f) { return e4m3_t{fp8Encode<false>(f)}; }
 };
 template <> struct Traits<e5m2_t> {
   static constexpr bool isFloat = true;
-  __host__ __device__ static float toF(e5m2_t v) { return fp8ToF32<true>(v.x); }
-  __host__ __device__ static e5m2_t fromF(float f) { return e5m2_t{f32ToFp8Sat<true>(halfToF32(f32ToHalf(f)))}; }
+  __host__ __device__ static float toF(e5m2_t v) { return fp8Decode<true>(v.x); }
+  __host__ __device__ static e5m2_t fromF(float f) { return e5m2_t{fp8Encode<true>(f)}; }
 };
 
 // ---- functors: pre(x), red(preLocal, acc), post(acc) ----

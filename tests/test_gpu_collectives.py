@@ -98,8 +98,9 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (3, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
             (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}),
             (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"}),
-            # cross-process memory: every dma-buf import refused -> the hipIpc handle fallback (ipc.cc); legacy only
-            (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}), (2, {"NCCL_AMD_IPC": "legacy"}),
+            # cross-process memory: every dma-buf import refused -> the hipIpc handle fallback (ipc.cc); legacy
+            # handles only (NCCL_AMD_IPC=legacy) run where the runtime is 7.2+, see test_legacy_ipc_runtime_gate
+            (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}),
             # the LL128-class protocol (LL64 lines): forced for everything it fits, and in its size-table range
             (3, {"NCCL_PROTO": "LL128"}), (4, {"NCCL_AMD_LL128": "1"})]
 
@@ -141,6 +142,51 @@ def test_multi_process(built, nranks, env):
         p.join(timeout=60)
     bad = [e for r in sorted(results) for e in results[r]]
     assert not bad, "\n".join(bad[:20])
+
+
+def _torch_hip_runtime():
+    import torch
+    parts = (torch.version.hip or "0.0").split(".")
+    return int(parts[0]) * 100 + int(parts[1])
+
+
+def test_legacy_ipc_runtime_gate(built):
+    """NCCL_AMD_IPC=legacy (hipIpc handles) is refused on HIP runtimes older than 7.2 — the
+    one bound in a torch process is torch's bundled runtime, whose hipIpcOpenMemHandle stalls at 2 GiB — with a
+    clean ncclSystemError naming that runtime, within seconds, never a hang; on a 7.2+ runtime it runs and is
+    bit-exact."""
+    import queue
+    import time
+    _torch()
+    import nccl_amd
+    old = _torch_hip_runtime() < 702
+    uid = nccl_amd.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    env = {"NCCL_AMD_IPC": "legacy"}
+    ps = [ctx.Process(target=_mp_worker, args=(r, 2, uid, True, q, env)) for r in range(2)]
+    t0 = time.time()
+    for p in ps:
+        p.start()
+    results = {}
+    while len(results) < 2 and time.time() - t0 < 300:
+        try:
+            r, errs = q.get(timeout=30)
+            results[r] = errs
+        except queue.Empty:
+            if not any(p.is_alive() for p in ps):
+                break
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+        p.join(timeout=60)
+    assert len(results) == 2, f"only {len(results)} of 2 ranks reported"
+    errs = [e for r in sorted(results) for e in results[r]]
+    if old:
+        assert len(errs) == 2 and all("refused on HIP runtime" in e and "libamdhip64" in e for e in errs), errs
+        assert time.time() - t0 < 200
+    else:
+        assert not errs, errs
 
 
 def test_reference_example_known_answer(built):
