@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 2 call 14: A/B of the previous build (ablib/libnccl_prev.so) and this one, n=2 sweeps alternating.
+# A/B of the previous build (ablib/libnccl_prev.so) and this one, n=2 sweeps alternating.
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp NCCL_AMD_SPIN_TIMEOUT_MS=20000; O=gpurun_out/r02c14; rm -rf $O; mkdir -p $O
 CFG=scripts/cfg/ab_refactor.json
 i=0

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 2 call 22: randomized parity fuzz with the LL128 class in the knob mix: single process (4 minutes),
+# randomized parity fuzz with the LL128 class in the knob mix: single process (4 minutes),
 # then 2-4 processes.
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp; O=gpurun_out/r02c22; rm -rf $O; mkdir -p $O
 timeout -k 10 300 python3 -u scripts/fuzz.py 240 22 > $O/fuzz.log 2>&1; rc=$?

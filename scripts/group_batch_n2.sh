@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 2 call 11: group batching across processes + aggregated vs unaggregated group timing (n=2, one GPU).
+# group batching across processes + aggregated vs unaggregated group timing (n=2, one GPU).
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp NCCL_AMD_SPIN_TIMEOUT_MS=20000; O=gpurun_out/r02c11; rm -rf $O; mkdir -p $O/g
 timeout -k 10 400 python3 -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_gpu_api.py -k "batches or aggregates" > $O/pytest.log 2>&1; rc=$?
 tail -8 $O/pytest.log; echo "pytest rc=$rc"; [ $rc -eq 0 ] || exit 1
