@@ -264,6 +264,7 @@ struct ncclComm {
   ncclamd::DevComm hostDevComm;          // host mirror
   uint32_t* hostAbort = nullptr;         // pinned, mapped: host→device abort flag
   uint32_t* hostError = nullptr;         // pinned, mapped: device→host error word
+  size_t stagingAllocBytes = 0, flagsAllocBytes = 0, countersAllocBytes = 0;  // as allocated (ncclCommMemStats)
   size_t slotBytes = 0;
   int nSlots = 0;
   int maxChannels = 0;

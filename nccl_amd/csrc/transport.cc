@@ -33,11 +33,14 @@ static size_t flagsBytes(const ncclComm* c) {
 
 // Device memory this communicator holds on its GPU (ncclCommMemStats): staging slab, flag/LL lines,
 // step counters and the device copy of DevComm. All of it lives as long as the communicator.
+// The sizes are the ones recorded when the memory was allocated (llChannels is lowered to the
+// co-residency cap AFTER the flag / LL block was allocated at the full count, so recomputing from the comm's
+// current shape under-reported it).
 size_t commDeviceBytes(const ncclComm* c) {
   size_t b = 0;
-  if (c->staging) b += stagingBytes(c);
-  if (c->flags) b += flagsBytes(c);
-  if (c->counters) b += (size_t)c->maxChannels * CTR_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
+  if (c->staging) b += c->stagingAllocBytes;
+  if (c->flags) b += c->flagsAllocBytes;
+  if (c->counters) b += c->countersAllocBytes;
   if (c->devComm) b += sizeof(DevComm);
   return b;
 }
@@ -50,7 +53,9 @@ ncclResult_t transportSetup(ncclComm* comm) {
     HIPCHECK(hipMalloc(&comm->staging, sb));
   else
     HIPCHECK(hipExtMallocWithFlags(&comm->staging, sb, hipDeviceMallocUncached));
+  comm->stagingAllocBytes = sb;
   HIPCHECK(hipExtMallocWithFlags((void**)&comm->flags, fb, hipDeviceMallocUncached));
+  comm->flagsAllocBytes = fb;
   HIPCHECK(hipMemset(comm->flags, 0, fb));
   HIPCHECK(hipDeviceSynchronize());
   INFO("rank %d dev %d: staging %zu MiB (%d ch x %d slots x %zu KiB), flags %zu KiB", comm->rank, comm->device,
@@ -166,6 +171,7 @@ ncclResult_t commAllocDevState(ncclComm* comm) {
   HIPCHECK(hipSetDevice(comm->device));
   size_t cb = (size_t)comm->maxChannels * CTR_KINDS * NCCL_AMD_MAX_RANKS * sizeof(uint64_t);
   HIPCHECK(hipMalloc((void**)&comm->counters, cb));
+  comm->countersAllocBytes = cb;
   HIPCHECK(hipMemset(comm->counters, 0, cb));
   // Test knob (reference TEST_LL_CLEANUP, include/device.h:99-106, shrinks the LL flag space to exercise
   // wraparound): start every channel's LL epoch at NCCL_AMD_LL_EPOCH_BASE, e.g. just below 2^32.
