@@ -224,12 +224,12 @@ constexpr int kFoldUnroll = NCCL_AMD_FOLD_UNROLL;
 #define NCCL_AMD_FOLD_UNROLL_SWAR 2
 #endif
 #ifndef NCCL_AMD_FOLD_UNROLL_1B
-#define NCCL_AMD_FOLD_UNROLL_1B 1
+#define NCCL_AMD_FOLD_UNROLL_1B 2
 #endif
 constexpr int kFoldUnrollSwar = NCCL_AMD_FOLD_UNROLL_SWAR;
 constexpr int kFoldUnroll1B = NCCL_AMD_FOLD_UNROLL_1B;
 #ifndef NCCL_AMD_FOLD_REPACK
-#define NCCL_AMD_FOLD_REPACK 0
+#define NCCL_AMD_FOLD_REPACK 1
 #endif
 
 // Copy [0,nbytes) from src to dst. Both 16-byte aligned when `aligned`; nbytes multiple of sizeof(T).
@@ -289,6 +289,72 @@ union PackU {
   T e[16 / sizeof(T)];
 };
 
+// fp8 fold over 16-byte packs (numerics.h fp8Decode4 / fp8RoundF / fp8Encode4): the accumulator lives as the
+// f32 values of its codes, each hop rounded to the value the per-element functor would store, the codes
+// written once at the end; the same element results as foldRange's generic path, at a fraction of the
+// conversion work (the fp8 fold is ALU-bound: profiles/r03_dtype_rates_n2_onegpu.json). One pack per thread
+// per batch, the next source's pack in flight; 16-byte aligned ranges only (the < 16-byte tail per element).
+template <typename T, int OP>
+__device__ __forceinline__ void foldFp8Packs(const Red<T, OP>& fn, int n, const char* const* src, uint64_t nelem,
+                                             char* dstLocal, char* const* dstPush, int nPush) {
+  constexpr bool E5 = IsFp8<T>::e5m2;
+  const uint64_t npk = nelem / 16;
+  for (uint64_t i = threadIdx.x; i < npk; i += kThreads) {
+    u32x4 cur = __builtin_nontemporal_load((const u32x4*)src[0] + i), nxt = cur;
+    float acc[16];
+    for (int k = 0; k < n; k++) {
+      if (k + 1 < n) nxt = __builtin_nontemporal_load((const u32x4*)src[k + 1] + i);
+      float x[16];
+#pragma unroll
+      for (int w = 0; w < 4; w++) fp8Decode4<E5>(cur[w], x + 4 * w);
+      if constexpr (OP == DEV_PREMULSUM) {  // pre(x) = fromF(x * s), rounded like the functor
+#pragma unroll
+        for (int e = 0; e < 16; e += 2) {
+          x[e] = opaqueF(x[e] * fn.s);
+          x[e + 1] = opaqueF(x[e + 1] * fn.s);
+          fp8RoundF<E5>(x[e], x[e + 1]);
+        }
+      }
+      if (k == 0) {
+#pragma unroll
+        for (int e = 0; e < 16; e++) acc[e] = x[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 16; e += 2) {
+          float r0, r1;
+          if (OP == DEV_PROD) {
+            r0 = opaqueF(x[e] * acc[e]);
+            r1 = opaqueF(x[e + 1] * acc[e + 1]);
+          } else if (OP == DEV_MINMAX) {
+            r0 = fn.isMin ? minOrdered(x[e], acc[e]) : maxOrdered(x[e], acc[e]);
+            r1 = fn.isMin ? minOrdered(x[e + 1], acc[e + 1]) : maxOrdered(x[e + 1], acc[e + 1]);
+          } else {
+            r0 = x[e] + acc[e];
+            r1 = x[e + 1] + acc[e + 1];
+          }
+          fp8RoundF<E5>(r0, r1);
+          acc[e] = r0;
+          acc[e + 1] = r1;
+        }
+      }
+      cur = nxt;
+    }
+    u32x4 out;
+#pragma unroll
+    for (int w = 0; w < 4; w++) out[w] = fp8Encode4<E5>(acc + 4 * w);
+    if (dstLocal) __builtin_nontemporal_store(out, (u32x4*)dstLocal + i);
+    for (int p = 0; p < nPush; p++) storeRemoteAt(remoteRsrc((u32x4*)dstPush[p] + (i - threadIdx.x)), threadIdx.x * 16u, out);
+  }
+  const uint64_t t = npk * 16 + threadIdx.x;  // < 16-byte tail
+  if (t < nelem) {
+    T a = fn.pre(((const T*)src[0])[t]);
+    for (int k = 1; k < n; k++) a = fn.red(fn.pre(((const T*)src[k])[t]), a);
+    a = fn.post(a);
+    if (dstLocal) ((T*)dstLocal)[t] = a;
+    for (int p = 0; p < nPush; p++) storeRemoteElt((T*)dstPush[p] + t, a);
+  }
+}
+
 // Fold n sources into dst (and optionally into nPush remote copies). src[k] is the k-th source in
 // fold order: acc = pre(src[0]); acc = red(pre(src[k]), acc) ...; out = post(acc).
 // Source/destination pointer lists live in LDS (uniform, read by broadcast). Each thread owns U packs
@@ -307,6 +373,12 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
   constexpr int U = sizeof(T) > 1 ? kFoldUnroll : kSwar ? kFoldUnrollSwar : kFoldUnroll1B;
   uint32_t swarMask = 0;
   if constexpr (kSwar) swarMask = (uint32_t)(uint8_t)fn.arg * 0x01010101u;
+  if constexpr (IsFp8<T>::value && NCCL_AMD_HW_FP8) {
+    if (aligned) {
+      foldFp8Packs<T, OP>(fn, n, src, nelem, dstLocal, dstPush, nPush);
+      return;
+    }
+  }
   if (aligned) {
     const uint64_t npk = nelem / EPP;
     for (uint64_t base = threadIdx.x; base < npk; base += (uint64_t)U * kThreads) {

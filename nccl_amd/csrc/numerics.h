@@ -321,6 +321,63 @@ struct Red<bf16_t, OP> {
 template <int OP> struct Red<e4m3_t, OP> : RedSmall<e4m3_t, OP> { using RedSmall<e4m3_t, OP>::RedSmall; };
 template <int OP> struct Red<e5m2_t, OP> : RedSmall<e5m2_t, OP> { using RedSmall<e5m2_t, OP>::RedSmall; };
 
+// ---- fp8 packs: four codes per dword through the paired convert instructions (device only) ----
+// The staged / zero-copy fold keeps an fp8 accumulator as the f32 VALUES of its codes between sources and
+// rounds each hop with fp8RoundF (the value fromF would store: RNE to half, satfinite, RNE to fp8), encoding
+// only once at the end: per element one half round trip, a clamp and half a paired encode + decode per hop,
+// instead of a full decode + encode per hop. Bit-identical to Red<e4m3_t / e5m2_t, OP> per element (the
+// decode / encode instructions equal the software conversions on every code and every half value,
+// tests/native/fp8_cvt_probe; tests/test_gpu_numerics.py runs every code pair through both paths).
+template <typename T> struct IsFp8 { static constexpr bool value = false; };
+template <> struct IsFp8<e4m3_t> { static constexpr bool value = true; static constexpr bool e5m2 = false; };
+template <> struct IsFp8<e5m2_t> { static constexpr bool value = true; static constexpr bool e5m2 = true; };
+
+#if defined(__HIP__)
+typedef float fp8v2f __attribute__((ext_vector_type(2)));
+__device__ inline float withSignOf(float x, uint32_t s) {  // x's magnitude, bit 31 of s: one v_bfi_b32
+  // (written as and / and / or, the backend emits three instructions; a VALU-only asm has no hazards)
+  uint32_t r;
+  asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x7fffffffu), "v"(f32AsU32(x)), "v"(s));  // gfx9 VOP3: no literal
+  return u32AsF32(r);
+}
+// four codes -> four values; NaN codes keep their own sign (the instruction makes every NaN negative)
+template <bool E5M2>
+__device__ inline void fp8Decode4(uint32_t w, float* f) {
+  const fp8v2f lo = E5M2 ? __builtin_amdgcn_cvt_pk_f32_bf8((int)w, false) : __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
+  const fp8v2f hi = E5M2 ? __builtin_amdgcn_cvt_pk_f32_bf8((int)w, true) : __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+  f[0] = withSignOf(lo.x, w << 24);
+  f[1] = withSignOf(lo.y, w << 16);
+  f[2] = withSignOf(hi.x, w << 8);
+  f[3] = withSignOf(hi.y, w);
+}
+// the values fromF would store for a and b: RNE to half, then satfinite RNE to fp8 (paired encode + decode);
+// NaN stays NaN with its sign
+template <bool E5M2>
+__device__ inline void fp8RoundF(float& a, float& b) {
+  const float mx = E5M2 ? 57344.0f : 448.0f;
+  const float ha = halfToF32(f32ToHalf(a)), hb = halfToF32(f32ToHalf(b));
+  const float ca = __builtin_fminf(__builtin_fmaxf(ha, -mx), mx), cb = __builtin_fminf(__builtin_fmaxf(hb, -mx), mx);
+  // the high word of the paired encode is never read: any register serves as its "old" operand (no v_mov)
+  const int old = (int)f32AsU32(ca);
+  const int w = E5M2 ? __builtin_amdgcn_cvt_pk_bf8_f32(ca, cb, old, false) : __builtin_amdgcn_cvt_pk_fp8_f32(ca, cb, old, false);
+  const fp8v2f d = E5M2 ? __builtin_amdgcn_cvt_pk_f32_bf8(w, false) : __builtin_amdgcn_cvt_pk_f32_fp8(w, false);
+  a = ha != ha ? ha : d.x;
+  b = hb != hb ? hb : d.y;
+}
+// four fp8 VALUES (fp8RoundF results or decoded codes: exact, no rounding) -> four codes; NaN -> sign | 0x7f
+template <bool E5M2>
+__device__ inline uint32_t fp8Encode4(const float* f) {
+  const int old = (int)f32AsU32(f[0]);  // high word overwritten below
+  int w = E5M2 ? __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], old, false) : __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], old, false);
+  w = E5M2 ? __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], w, true) : __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
+  // the instruction encodes every NaN as 0xff: a positive NaN is 0x7f (clear bit 7 of its byte)
+  uint32_t clr = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) clr |= f32AsU32(f[i]) - 0x7f800001u < 0x007fffffu ? 0x80u << (8 * i) : 0u;  // +NaN
+  return (uint32_t)w & ~clr;
+}
+#endif
+
 // ---- 1-byte integer Sum / MinMax on four bytes per dword (SWAR) ----
 // Bit-identical to Red<uint8_t, OP>::red on each byte (tests/test_numerics.py checks every byte pair). The fold
 // uses it for uint8 / int8 so a 16-byte pack stays four registers instead of sixteen unpacked bytes, which
