@@ -29,6 +29,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -49,7 +50,39 @@ struct FdServer {
   // proxy thread maps a registered buffer for ncclIpcLocalRegisterBuffer, src/transport/p2p.cc ipcRegister):
   // (registering rank, its registration tag) -> mapping. Touched only by the server thread.
   std::map<std::pair<int, uint64_t>, IpcImport> imports;
+  // Unmapping a peer's buffer (hipFree of the mapping) waits for this device's outstanding work, which may
+  // be a collective kernel waiting for the very rank whose RELEASE request is being served: the server thread
+  // therefore only answers and hands the mapping to this reaper thread, which may block as long as it needs
+  // (found by the multi-process fuzz: a deregistration on one rank stalled its peers' next collective until
+  // the spin timeout).
+  std::thread reaper;
+  std::mutex reapMu;
+  std::condition_variable reapCv;
+  std::vector<IpcImport> reapQueue;
+  bool reapStop = false;
 };
+
+static void reapLater(FdServer* s, const IpcImport& m) {
+  std::lock_guard<std::mutex> g(s->reapMu);
+  s->reapQueue.push_back(m);
+  s->reapCv.notify_one();
+}
+
+static void reaperLoop(FdServer* s) {
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;  // see serverLoop
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  std::unique_lock<std::mutex> lk(s->reapMu);
+  while (true) {
+    s->reapCv.wait(lk, [s] { return s->reapStop || !s->reapQueue.empty(); });
+    if (s->reapQueue.empty()) break;  // stopping and drained
+    std::vector<IpcImport> batch;
+    batch.swap(s->reapQueue);
+    lk.unlock();
+    (void)hipSetDevice(s->device);
+    for (IpcImport& m : batch) ipcRelease(&m);
+    lk.lock();
+  }
+}
 
 // Requests on the fd server's socket (one per connection). FETCH: hand over the fd published under `key`.
 // IMPORT: map the dma-buf fd attached to the request (SCM_RIGHTS) on this comm's device on behalf of rank
@@ -165,7 +198,7 @@ static void serveOne(FdServer* s, int c) {
       inFd = -1;  // owned by the mapping now
       auto key = std::make_pair((int)q.from, q.key);
       auto old = s->imports.find(key);
-      if (old != s->imports.end()) ipcRelease(&old->second);  // a re-registration replaces its mapping
+      if (old != s->imports.end()) reapLater(s, old->second);  // a re-registration replaces its mapping
       s->imports[key] = m;
       reply.status = 0;
       reply.value = (uint64_t)m.ptr;
@@ -175,8 +208,7 @@ static void serveOne(FdServer* s, int c) {
   } else if (q.op == IPC_RELEASE) {
     auto it = s->imports.find(std::make_pair((int)q.from, q.key));
     if (it != s->imports.end()) {
-      (void)hipSetDevice(s->device);
-      ipcRelease(&it->second);
+      reapLater(s, it->second);  // never block the server on the device (FdServer::reaper)
       s->imports.erase(it);
     }
     reply.status = 0;
@@ -223,6 +255,7 @@ ncclResult_t ipcServerStart(ncclComm* comm) {
     return ncclSystemError;
   }
   s->thread = std::thread(serverLoop, s);
+  s->reaper = std::thread(reaperLoop, s);
   comm->fdServer = s;
   TRACE("rank %d: fd server %s", comm->rank, s->name);
   return ncclSuccess;
@@ -233,6 +266,12 @@ void ipcServerStop(ncclComm* comm) {
   if (!s) return;
   if (s->wakePipe[1] >= 0) (void)!write(s->wakePipe[1], "x", 1);
   if (s->thread.joinable()) s->thread.join();
+  {
+    std::lock_guard<std::mutex> g(s->reapMu);
+    s->reapStop = true;
+    s->reapCv.notify_one();
+  }
+  if (s->reaper.joinable()) s->reaper.join();  // drains what RELEASE requests queued
   for (auto& kv : s->table) close(kv.second);
   if (!s->imports.empty()) (void)hipSetDevice(comm->device);
   for (auto& kv : s->imports) ipcRelease(&kv.second);  // peers' registrations still mapped here

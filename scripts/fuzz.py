@@ -1,8 +1,8 @@
 """Randomized parity fuzzing on the GPU: random communicator settings (ranks 2-4 in one process, slot size,
 slot count, channel cap, protocol / algorithm, pull variants) and, per communicator, random collectives
 (type, op, count incl. ragged and tiny, misaligned bases, in place, root; sometimes a group of several
-collectives, so small AllReduces aggregate into LL batches between other ops) checked bit-exact
-against the CPU oracle. Usage: python scripts/fuzz.py SECONDS [SEED]. Prints one line per communicator."""
+collectives, so small AllReduces aggregate into LL batches between other ops; a quarter of the communicators
+in symmetric windows, a quarter on ncclCommRegister'd buffers) checked bit-exact against the CPU oracle. Usage: python scripts/fuzz.py SECONDS [SEED]. Prints one line per communicator."""
 import os
 import random
 import sys
@@ -18,7 +18,7 @@ from tests import gpu_cases as G  # noqa: E402
 
 KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_AG_PULL",
          "NCCL_AMD_RS_PULL", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_LL_CHANNEL_BYTES", "NCCL_AMD_LL128",
-         "NCCL_AMD_LL128_CHANNEL_BYTES", "NCCL_AMD_SYM_WT")
+         "NCCL_AMD_LL128_CHANNEL_BYTES", "NCCL_AMD_SYM_WT", "NCCL_AMD_P2P_FENCE", "NCCL_AMD_LINK_CHANNELS")
 
 
 def settings(rng):
@@ -47,17 +47,26 @@ def settings(rng):
         env["NCCL_AMD_LL128_CHANNEL_BYTES"] = str(rng.choice([56, 512, 16384]))
     if rng.random() < 0.3:
         env["NCCL_AMD_SYM_WT"] = "0"  # the symmetric kernels' write-back publish instead of write-through
+    if rng.random() < 0.3:
+        env["NCCL_AMD_P2P_FENCE"] = "1"  # the release fence the cross-device default keeps
+    if rng.random() < 0.2:
+        env["NCCL_AMD_LINK_CHANNELS"] = str(rng.choice([2, 8, 16]))  # the n >= 3 CU budget, tightened
     return env
 
 
-def run_window_cases(cs, rng, k):
+def run_window_cases(cs, rng, k, registered=False):
     """k random cases with every buffer inside NCCL_WIN_COLL_SYMMETRIC windows at the same offsets on every
-    rank (the symmetric kernels; Reduce and LL-sized ops take their usual paths), checked bit-exact."""
+    rank (the symmetric kernels; Reduce and LL-sized ops take their usual paths), or with registered=True in
+    buffers registered with ncclCommRegister (the zero-copy kernel in registered mode), checked bit-exact."""
     import numpy as np
     import oracle
     from tests import test_gpu_windows as W
     n = len(cs)
-    bufs, wins = W._windows([c for c, _ in cs])
+    if registered:
+        bufs = [torch.empty(W.WIN_BYTES, dtype=torch.uint8, device="cuda") for _ in cs]
+        wins = [c.register_buffer(b.data_ptr(), W.WIN_BYTES) for (c, _), b in zip(cs, bufs)]
+    else:
+        bufs, wins = W._windows([c for c, _ in cs])
     bases = [(b, b.data_ptr()) for b in bufs]
     errs, done = [], 0
     for _ in range(k):
@@ -77,10 +86,14 @@ def run_window_cases(cs, rng, k):
         e = W._run(cs, bases, coll, dt, op, count, off, inplace, seed=rng.randrange(1 << 30), root=root)
         done += 1
         if e:
-            errs.append(f"window {coll} dt={dt} op={op} count={count} off={off} inplace={inplace} root={root}: {e[:3]}")
+            errs.append(f"{'registered' if registered else 'window'} {coll} dt={dt} op={op} count={count} off={off} "
+                        f"inplace={inplace} root={root}: {e[:3]}")
             break
     for (c, _), w in zip(cs, wins):
-        c.deregister_window(w)
+        if registered:
+            c.deregister_buffer(w)
+        else:
+            c.deregister_window(w)
     return errs, done
 
 
@@ -143,8 +156,9 @@ def main():
         streams = [torch.cuda.Stream() for _ in range(n)]
         cs = list(zip(comms, streams))
         done = 0
-        if rng.random() < 0.25:  # symmetric windows for this communicator
-            errs, k = run_window_cases(cs, rng, rng.randint(4, 12))
+        mode = rng.random()
+        if mode < 0.5:  # symmetric windows (a quarter) or registered buffers (a quarter) for this communicator
+            errs, k = run_window_cases(cs, rng, rng.randint(4, 12), registered=mode >= 0.25)
             total += k
             done += k
             if errs:

@@ -28,6 +28,35 @@ def worker(rank, n, uids, seed, q):
                 os.environ.pop(k, None)
             os.environ.update(env)
             comm = nccl_amd.Communicator.init(n, rank, uid)
+            if rng.random() < 0.3:  # ncclCommRegister'd buffers: the zero-copy kernel in registered mode
+                from tests import test_gpu_windows as W
+                import numpy as np
+                import oracle
+                buf = torch.empty(W.WIN_BYTES, dtype=torch.uint8, device="cuda")
+                h = comm.register_buffer(buf.data_ptr(), W.WIN_BYTES)
+                for _ in range(rng.randint(3, 8)):
+                    coll = rng.choice(["allreduce", "allreduce", "reducescatter", "allgather", "reduce"])
+                    dt = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
+                    op = 0 if coll == "allgather" else rng.choice([0, 1, 2, 3, 4])
+                    es = np.dtype(oracle.NP_STORAGE[dt]).itemsize
+                    off = rng.choice([0, 0, 1, 3])
+                    inplace = off == 0 and rng.random() < 0.3
+                    span = (W.HALF - 64) // es
+                    count = rng.choice([1, 7, 1000, 4099, 65_536, 300_001])
+                    if coll in ("reducescatter", "allgather"):
+                        count = min(count, span // n)
+                        count = max(1, count // n) * n if coll == "reducescatter" else max(1, count)
+                    count = min(count, span)
+                    root = rng.randrange(n)
+                    errs = W._run([(comm, s)], [(buf, buf.data_ptr())], coll, dt, op, count, off, inplace,
+                                  seed=rng.randrange(1 << 30), root=root)
+                    total += 1
+                    if errs:
+                        comm.destroy()
+                        q.put((rank, [f"env={env} registered {coll} dt={dt} op={op} count={count} off={off} "
+                                      f"inplace={inplace}: {errs[:2]}"], total))
+                        return
+                comm.deregister_buffer(h)
             for _ in range(rng.randint(4, 10)):
                 coll = rng.choice(["allreduce", "allreduce", "reducescatter", "allgather", "reduce"])
                 dt = rng.choice([0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])

@@ -245,3 +245,45 @@ def test_registered_allreduce_fp32_256MiB_n2(built):
     res = _spawn(_large_worker, 2)
     bad = [e for r in sorted(res) for e in res[r]]
     assert not bad, "\n".join(bad)
+
+
+def _dereg_worker(rank, nranks, uid, q):
+    """Rank 0 deregisters at once and starts its next (staged) collective; the others deregister later, while
+    rank 0's kernel already waits for them. Their release requests reach rank 0's fd server, which must answer
+    without waiting for rank 0's device (the unmapping runs on its reaper thread): before that fix the server's
+    hipFree waited for rank 0's kernel, which waited for the ranks blocked on the server — a stall until the
+    spin timeout (found by scripts/fuzz_mp.py)."""
+    try:
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "15000"
+        import torch
+        import nccl_amd
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.Stream()
+        errs = []
+        t0 = time.time()
+        for it in range(3):
+            buf = torch.empty(WIN_BYTES, dtype=torch.uint8, device="cuda")
+            h = comm.register_buffer(buf.data_ptr(), WIN_BYTES)
+            errs += _run([(comm, s)], [(buf, buf.data_ptr())], "allreduce", 7, 0, 200_003, 0, False, seed=60 + it)
+            torch.cuda.synchronize()
+            if rank != 0:
+                time.sleep(1.0)
+            comm.deregister_buffer(h)
+            errs += G.run_case([(comm, s)], "allreduce", 7, 0, 300_001, 0, seed=70 + it)
+            if errs or comm.async_error():
+                errs.append(f"rank {rank} iteration {it}: async {comm.async_error()}")
+                break
+        elapsed = time.time() - t0
+        comm.destroy()
+        q.put((rank, (errs, elapsed)))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0)))
+
+
+def test_deregister_while_peers_run(built):
+    res = _spawn(_dereg_worker, 3)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:10])
+    assert all(t < 12 for _, t in res.values()), res  # three 1 s delays, no spin timeout
