@@ -221,6 +221,7 @@ struct CommTuning {
   int64_t oneShotChannelBytes;  // NCCL_AMD_ONESHOT_CHANNEL_BYTES
   int copyVariant;          // NCCL_AMD_COPY_VARIANT (nRanks == 1 copy kernel, diagnostics)
   int64_t copyGrid;         // NCCL_AMD_COPY_GRID (cap on its workgroups; default: one per 16 KiB tile)
+  int64_t ringChunkBytes;   // NCCL_ALGO=RING AllReduce chunk: NCCL_BUFFSIZE / NCCL_STEPS * ALLREDUCE_CHUNKSTEPS
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
 void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known

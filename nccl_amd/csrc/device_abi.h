@@ -100,6 +100,10 @@ struct CollArgs {
   int root;
   int aligned;         // send/recv base pointers are 16-byte aligned
   int protoFlags;      // NCCL_AMD_PROTO_FLAGS diagnostics (kernels.h collKernel)
+  // Ring AllReduce (PIPE_RING_AR) in the reference's partition: channel parts lo / mid (= part) / hi
+  // (ncclCollCbdPart, reference src/include/device.h:337-361), each walked in loops of n chunks of `chunk`
+  // elements (all_reduce.h:21-38). Unused by every other kernel.
+  uint64_t cbdLo, cbdHi;
 };
 
 // Staged batch: up to kMaxCollBatch ops of one group with the same collective, type and op (and the same

@@ -144,6 +144,11 @@ void loadTuning(CommTuning* t) {
   t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
   t->copyVariant = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
   t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);
+  // the reference's RING/SIMPLE chunk: stepSize (NCCL_BUFFSIZE / NCCL_STEPS) x ALLREDUCE_CHUNKSTEPS (NCCL_STEPS / 2),
+  // in 512-byte grains (enqueue.cc:2222-2225, 2321; collectives.h:19-20; default NCCL_BUFFSIZE 4 MiB, init.cc:813)
+  const int64_t buff = paramInt("NCCL_BUFFSIZE", 4 << 20);
+  t->ringChunkBytes = buff / 8 * 4 / 512 * 512;
+  if (t->ringChunkBytes < 512) t->ringChunkBytes = 512;
 }
 
 // CU budget of the large staged and zero-copy plans at n >= 3 (reference: channels and threads shrink below
@@ -242,6 +247,51 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
   p.args.part = part;
   p.args.slice = slice;
   p.args.nSteps = (int)((part + slice - 1) / slice);
+}
+
+// NCCL_ALGO=RING AllReduce: the reference's own partition, so that every element is finalised by the same ring
+// position as in the reference's RING/SIMPLE AllReduce on a communicator of K channels (here K = chanCap, i.e.
+// NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS = K there) with the same NCCL_BUFFSIZE — bit-identical results, floats
+// included. For one task, starting on channel 0 with no traffic planned yet:
+//  * channels: K shrunk while the bytes are below K x 512 threads x 64 (topoGetAlgoInfo, enqueue.cc:2091-2097;
+//    NCCL_SIMPLE_MAX_NTHREADS and NCCL_SIMPLE_THREAD_THRESHOLD, tuning.cc:246, 591);
+//  * channel parts over 16 KiB cells (32 KiB of AllReduce traffic): a first part sized to the traffic per
+//    channel, equal middle parts, a remainder part (scheduleCollTasksToPlan, enqueue.cc:576-757);
+//  * each part walked in loops of n chunks of tune.ringChunkBytes, the last loop re-cut (kernel, pipe.h).
+struct RingParts {
+  int nch;
+  uint64_t lo, mid, hi;
+};
+static RingParts ringParts(uint64_t count, int ts, int K) {
+  const uint64_t bytes = count * (uint64_t)ts;
+  int nc = K;
+  while (nc >= 2 && bytes < (uint64_t)nc * 512 * 64) nc--;
+  const uint64_t cell = 16 << 10, trafficCell = 2 * cell;  // AllReduce moves 2 bytes of traffic per byte
+  const uint64_t eltsPerCell = cell / ts;
+  const uint64_t cells = (bytes + cell - 1) / cell;
+  const uint64_t traffic = std::max<uint64_t>(32 << 10, 2 * bytes);
+  const uint64_t perChannel = (traffic / nc + 15) / 16 * 16;
+  const uint64_t perChannelCells = (perChannel + trafficCell - 1) / trafficCell;
+  uint64_t cellsPerCh = std::min(cells, perChannelCells);
+  const uint64_t cellsLo = K == 1 ? cells : std::min(cells, perChannelCells);
+  int64_t nMid = (int64_t)((cells - cellsLo) / cellsPerCh);
+  uint64_t cellsHi = (cells - cellsLo) % cellsPerCh;
+  if ((int64_t)K < (cellsLo ? 1 : 0) + nMid + (cellsHi ? 1 : 0)) {  // more parts than channels
+    nMid = K - 2;
+    cellsPerCh = (cells - cellsLo) / (uint64_t)(nMid + 1);
+    cellsHi = cellsPerCh + (cells - cellsLo) % (uint64_t)(nMid + 1);
+  }
+  if (cellsHi == 0 && nMid != 0) {
+    cellsHi = cellsPerCh;
+    nMid--;
+  }
+  RingParts r;
+  r.lo = cellsLo * eltsPerCell;
+  r.mid = nMid ? cellsPerCh * eltsPerCell : 0;
+  r.hi = cellsHi * eltsPerCell;
+  (r.hi ? r.hi : r.lo) -= cells * eltsPerCell - count;  // the last part ends at count
+  r.nch = (r.lo ? 1 : 0) + (int)nMid + (cellsHi ? 1 : 0);
+  return r;
 }
 
 // LL eligibility and channel plan of one AllReduce, ReduceScatter, AllGather or Reduce (reference tuning: LL for
@@ -462,6 +512,16 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       if (chain) p.args.chunk = count;  // one block: the chain folds every element in the same order
       const size_t span = chain ? count * ts : blockElems * ts;
       planChannels(comm, span, ts, p, (size_t)comm->tune.minChannelBytes, comm->chanCap);
+      if (kind == PIPE_RING_AR) {  // the reference's channel parts and loop chunk (ringParts above)
+        const RingParts r = ringParts(count, ts, comm->chanCap);
+        p.nChannels = r.nch;
+        p.args.cbdLo = r.lo;
+        p.args.part = r.mid;
+        p.args.cbdHi = r.hi;
+        p.args.chunk = (uint64_t)comm->tune.ringChunkBytes / ts;
+        p.args.slice = std::min<uint64_t>(p.args.chunk, comm->slotBytes / ts / epp * epp);
+        p.args.nSteps = 0;  // per channel and loop (pipe.h)
+      }
       TRACE("%s: %s kind %d nch %d part %lu slice %lu steps %d", info.opName, ring ? "RING" : "TREE", kind,
             p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps);
       return ncclSuccess;

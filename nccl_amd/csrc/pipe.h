@@ -14,11 +14,11 @@
 // direction per rank (busBW <= B_link) and the chain by one link (algBW <= B_link); the direct kernel uses
 // all n-1 links. They exist for the reference's algorithm choice (C4's ring-vs-tree curve), not speed.
 //
-// Fold orders. Ring: rank blocks as in the direct kernel (block q = alignUp(divUp(count, n), 16/sizeof(T))
-// elements, all_reduce.h:38); block q starts at rank q+1 with pre(x_{q+1}) and each next rank folds
-// red(pre(x_r), acc), ending at q — exactly the oracle's order, so ring results are bit-identical to the
-// direct kernel's. Chain AllReduce: the reference's intra-node tree with treeIntra = (0, 1, ..., n-1): leaf
-// n-1 sends pre(x_{n-1}), rank k folds red(pre(x_k), acc) and the root 0 finishes (post) and broadcasts
+// Fold orders. Ring AllReduce: the reference's own partition (channel parts, loops of n chunks, the last loop
+// re-cut, all_reduce.h:21-81; planned by enqueue.cc ringParts); chunk q of a loop starts at rank q+1 with
+// pre(x_{q+1}) and each next rank folds red(pre(x_r), acc), ending at q — the reference's RING/SIMPLE order
+// on the same channel count (oracle_all_reduce_ring_nccl). Ring ReduceScatter: block q folds from q+1.
+// Chain AllReduce: the reference's intra-node tree with treeIntra = (0, 1, ..., n-1): leaf n-1 sends pre(x_{n-1}), rank k folds red(pre(x_k), acc) and the root 0 finishes (post) and broadcasts
 // back down: order n-1, n-2, ..., 0 for every element (oracle_all_reduce_chain). Chain Reduce: the
 // reference's ring reduce, root+1, ..., root (reduce.h:34-52).
 #pragma once
@@ -204,19 +204,65 @@ __global__ void __launch_bounds__(kThreads) kCoResident pipeKernel(CollArgs a) {
   char* outb = (char*)a.recvbuff;
   const int next = (me + 1) % n, prev = (me + n - 1) % n;
   bool ok = true;
-  if (KIND == PIPE_RING_AR || KIND == PIPE_RING_RS || KIND == PIPE_RING_AG) {
-    // AllReduce / Reduce-scatter: blocks of a.chunk elements (AllReduce: the last may be short);
-    // AllGather: block q of the output is rank q's input
-    auto blockLen = [&](int q) -> uint64_t {
-      if (KIND != PIPE_RING_AR) return a.chunk;
-      const uint64_t b = (uint64_t)q * a.chunk;
-      return b >= a.count ? 0 : min(a.chunk, a.count - b);
-    };
+  if (KIND == PIPE_RING_AR) {
+    // The reference's runRing over its own partition (all_reduce.h:21-81): this channel's part
+    // (ncclCollCbdPart, device.h:337-361: the first channel takes cbdLo elements, the middle ones `part`, the
+    // last cbdHi), walked in loops of n chunks of a.chunk elements; the last loop re-cuts the chunk to
+    // alignUp(divUp(rem, n), 16 / sizeof(T)) (:38). Chunk q of a loop starts at rank q+1 and is finalised by
+    // rank q, so every element folds exactly as in the reference's RING/SIMPLE AllReduce on the same number of
+    // channels. A chunk moves through the staging slots in slices of a.slice elements; every rank walks the
+    // same loops and slices (the counts are shared), so the hops pair up.
+    constexpr uint64_t EPP = 16 / ts;
+    const int nch = (int)gridDim.x;
+    uint64_t pOff, pCnt;
+    if (c == 0) pOff = 0, pCnt = a.cbdLo;
+    else if (c == nch - 1) pOff = a.cbdLo + (uint64_t)(nch - 2) * a.part, pCnt = a.cbdHi;
+    else pOff = a.cbdLo + (uint64_t)(c - 1) * a.part, pCnt = a.part;
+    const uint64_t loopCount = (uint64_t)n * a.chunk;
+    for (uint64_t eo = 0; ok && eo < pCnt; eo += loopCount) {
+      const uint64_t rem = pCnt - eo;
+      const uint64_t ck = rem < loopCount ? ((rem + n - 1) / n + EPP - 1) / EPP * EPP : a.chunk;
+      const char* inL = in + (pOff + eo) * ts;
+      char* outL = outb + (pOff + eo) * ts;
+      const uint64_t nSub = (ck + a.slice - 1) / a.slice;
+      for (uint64_t s = 0; ok && s < nSub; s++) {
+        uint64_t lo, hi;
+        auto sl = [&](int q) {  // slice s of chunk q (empty past the loop's end)
+          const uint64_t b = (uint64_t)q * ck, len = b >= rem ? 0 : min(ck, rem - b);
+          lo = min(s * a.slice, len);
+          hi = min(lo + a.slice, len);
+        };
+        auto at = [&](int q) { return ((uint64_t)q * ck + lo) * ts; };
+        int q = prev;  // step 0: send chunk ringIx - 1
+        sl(q);
+        ok = p.template hop<MV_PRE>(STG_RS, -1, next, inL + at(q), nullptr, hi - lo);
+        for (int j = 2; ok && j < n; j++) {  // n-2 x recvReduceSend
+          q = (me + n - j) % n;
+          sl(q);
+          ok = p.template hop<MV_FOLD>(STG_RS, prev, next, inL + at(q), nullptr, hi - lo);
+        }
+        if (!ok) break;
+        sl(me);  // recvReduceCopySend: the final value of my chunk
+        ok = p.template hop<MV_FINAL>(STG_RS, prev, next, inL + at(me), outL + at(me), hi - lo);
+        for (int j = 1; ok && j < n - 1; j++) {  // n-2 x recvCopySend
+          q = (me + n - j) % n;
+          sl(q);
+          ok = p.template hop<MV_COPY>(STG_RS, prev, next, nullptr, outL + at(q), hi - lo);
+        }
+        if (!ok) break;
+        q = next;  // recv: the chunk next finalised
+        sl(q);
+        ok = p.template hop<MV_COPY>(STG_RS, prev, -1, nullptr, outL + at(q), hi - lo);
+      }
+    }
+  } else if (KIND == PIPE_RING_RS || KIND == PIPE_RING_AG) {
+    // Reduce-scatter: block q (a.chunk = recvcount elements) is rank q's output and folds from q+1 whatever the
+    // partition; AllGather: block q of the output is rank q's input. Each channel takes a part of every block.
     for (int s = 0; ok && s < a.nSteps; s++) {
       uint64_t lo, hi;
-      auto sl = [&](int q) { sliceRange(a, c, s, blockLen(q), lo, hi); };
-      if (KIND != PIPE_RING_AG) {
-        int q = prev;  // step 0 of the reference's runRing: send chunk ringIx-1
+      auto sl = [&](int) { sliceRange(a, c, s, a.chunk, lo, hi); };
+      if (KIND == PIPE_RING_RS) {
+        int q = prev;  // step 0 of the reference's ring: send chunk ringIx-1
         sl(q);
         ok = p.template hop<MV_PRE>(STG_RS, -1, next, in + ((uint64_t)q * a.chunk + lo) * ts, nullptr, hi - lo);
         for (int j = 2; ok && j < n; j++) {  // n-2 x recvReduceSend
@@ -225,10 +271,9 @@ __global__ void __launch_bounds__(kThreads) kCoResident pipeKernel(CollArgs a) {
           ok = p.template hop<MV_FOLD>(STG_RS, prev, next, in + ((uint64_t)q * a.chunk + lo) * ts, nullptr, hi - lo);
         }
         if (!ok) break;
-        sl(me);  // recvReduceCopy(Send): the final value of my block
-        char* o = KIND == PIPE_RING_RS ? outb + lo * ts : outb + ((uint64_t)me * a.chunk + lo) * ts;
-        ok = p.template hop<MV_FINAL>(STG_RS, prev, KIND == PIPE_RING_AR ? next : -1,
-                                      in + ((uint64_t)me * a.chunk + lo) * ts, o, hi - lo);
+        sl(me);  // recvReduceCopy: the final value of my block
+        ok = p.template hop<MV_FINAL>(STG_RS, prev, -1, in + ((uint64_t)me * a.chunk + lo) * ts, outb + lo * ts,
+                                      hi - lo);
       } else {
         sl(me);  // AllGather step 0: my input to my output block and to next
         char* o = outb + ((uint64_t)me * a.chunk + lo) * ts;

@@ -34,6 +34,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_host_to_dev_op.argtypes = [I, I, I, ctypes.POINTER(I), ctypes.POINTER(U64)]
         L.oracle_all_reduce.argtypes = [I, I, U64, I, PP, S, P]
         L.oracle_all_reduce_chain.argtypes = [I, I, U64, I, PP, S, P]
+        L.oracle_all_reduce_ring_nccl.argtypes = [I, I, U64, I, PP, S, P, I, S]
+        L.oracle_ring_nccl_plan.argtypes = [S, I, I, I, S, ctypes.POINTER(U64)]
         L.oracle_reduce_scatter.argtypes = [I, I, U64, I, PP, S, PP]
         L.oracle_reduce.argtypes = [I, I, U64, I, I, PP, S, P]
         L.oracle_fill.argtypes = [I, U64, S, P, I]
@@ -92,6 +94,29 @@ def all_reduce_chain(inputs: Sequence[np.ndarray], dtype: int, op: int = 0):
     ins = [np.ascontiguousarray(x) for x in inputs]
     out = np.empty_like(ins[0])
     rc = lib().oracle_all_reduce_chain(dtype, d, arg, n, _ptrs(ins), ins[0].size, out.ctypes.data)
+    assert rc == 0
+    return out
+
+
+def ring_nccl_plan(count: int, type_size: int, nranks: int, nchannels: int, buffsize: int = 0):
+    """The reference's RING/SIMPLE AllReduce partition of `count` elements on a communicator of `nchannels`
+    channels (nccl_oracle.c oracle_ring_nccl_plan): (channels, countLo, countMid, countHi, chunk elements)."""
+    plan = (ctypes.c_uint64 * 5)()
+    rc = lib().oracle_ring_nccl_plan(count, type_size, nranks, nchannels, buffsize, plan)
+    if rc:
+        raise ValueError("invalid ring plan arguments")
+    return tuple(int(x) for x in plan)
+
+
+def all_reduce_ring_nccl(inputs: Sequence[np.ndarray], dtype: int, op: int, nchannels: int, buffsize: int = 0):
+    """ncclAllReduce with NCCL_ALGO=RING, NCCL_PROTO=Simple in the reference's full-size order: channel parts,
+    loops of n chunks, last loop re-cut (all_reduce.h:21-81) on a communicator of `nchannels` channels."""
+    n = len(inputs)
+    d, arg = dev_op(op, dtype, n)
+    ins = [np.ascontiguousarray(x) for x in inputs]
+    out = np.empty_like(ins[0])
+    rc = lib().oracle_all_reduce_ring_nccl(dtype, d, arg, n, _ptrs(ins), ins[0].size, out.ctypes.data, nchannels,
+                                           buffsize)
     assert rc == 0
     return out
 

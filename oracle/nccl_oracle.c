@@ -16,7 +16,9 @@
  *   - ring fold order: the value owned by ring position c is folded starting at c+1, c+2, ...,
  *     ending with c's own input, rounded to T after every hop:
  *       AllReduce      src/device/all_reduce.h:13-83 (chunk c finalised at ringIx c; one channel,
- *                      one loop iteration: chunkCount = alignUp(divUp(count,n), 16/sizeof(T)), :38)
+ *                      one loop iteration: chunkCount = alignUp(divUp(count,n), 16/sizeof(T)), :38);
+ *                      at full size on K channels (RING/SIMPLE): oracle_all_reduce_ring_nccl, the
+ *                      reference's channel parts and loops (enqueue.cc:576-757, 2070-2097, 2182-2321)
  *       ReduceScatter  src/device/reduce_scatter.h:13-56 (block d finalised at rank d)
  *       Reduce         src/device/reduce.h:13-53 (chain: root+1 sends, root reduces last)
  *     Ring order is the identity permutation (ring index = rank, src/init.cc:791-808 on a full mesh).
@@ -339,6 +341,121 @@ int oracle_all_reduce(int dt, int devop, uint64_t arg, int n, const void* const*
   for (size_t i = 0; i < count; i++) {
     int owner = (int)(i / rc);
     st(dt, out, i, fold_elem(dt, devop, arg, n, in, i, (owner + 1) % n));
+  }
+  return 0;
+}
+
+/* ---- the reference's RING/SIMPLE AllReduce partition at full size (more than one channel and loop) ----
+ * NCCL cuts a large AllReduce into channel parts and each part into loops of n chunks; a chunk's elements are
+ * finalised by the ring position of the chunk INSIDE ITS LOOP, so which rank's input an element's fold starts
+ * from depends on this partition. Restated for ONE task on a communicator of `nchannels` channels with an
+ * NCCL_BUFFSIZE of `buffsize` bytes (0 = the 4 MiB default, src/init.cc:813):
+ *   channel count   topoGetAlgoInfo, RING/SIMPLE: nc = nchannels, decremented while
+ *                   nBytes < nc * nt * threshold with nt = 512 (NCCL_SIMPLE_MAX_NTHREADS, tuning.cc:244-247,
+ *                   NVLink-class bandwidth) and threshold 64 (NCCL_SIMPLE_THREAD_THRESHOLD, tuning.cc:591):
+ *                   src/enqueue.cc:2070-2097
+ *   parts (CBD)     scheduleCollTasksToPlan for a lone task (channelId 0, no traffic yet): 16 KiB cells
+ *                   (32 KiB of traffic at 2 bytes per byte for AllReduce), lo / mid / hi channel parts:
+ *                   src/enqueue.cc:576-757, trafficPerByte :91-94; the part of channel c: device.h:337-361
+ *   chunk           calcCollChunking, RING/SIMPLE: buffsize / NCCL_STEPS (8) * ALLREDUCE_CHUNKSTEPS (4),
+ *                   in 512-byte grains: src/enqueue.cc:2222-2225, 2321; collectives.h:19-20; device.h:328-334
+ *   loops           runRing: loopCount = n * chunkCount; the last loop re-cuts chunkCount to
+ *                   alignUp(divUp(rem, n), 16 / sizeof(T)): src/device/all_reduce.h:21-38
+ * plan[0..4] = {channels, countLo, countMid, countHi, chunk elements}. */
+static size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
+
+int oracle_ring_nccl_plan(size_t count, int ts, int nranks, int nchannels, size_t buffsize, uint64_t* plan) {
+  if (ts <= 0 || nranks <= 0 || nchannels <= 0 || count == 0) return 4;
+  if (buffsize == 0) buffsize = (size_t)1 << 22;
+  /* channel count (enqueue.cc:2093-2096) */
+  const size_t nBytes = count * (size_t)ts;
+  int nc = nchannels;
+  while (nBytes < (size_t)nc * 512 * 64) {
+    if (nc >= 2) nc--;
+    else break;
+  }
+  /* CBD (enqueue.cc:580-604, 617-620, 657-701) */
+  const size_t minTraffic = (size_t)32 << 10;
+  const size_t trafficPerByte = 2;
+  size_t trafficBytes = count * (size_t)ts * trafficPerByte;
+  if (trafficBytes < minTraffic) trafficBytes = minTraffic;
+  const size_t trafficPerChannel = div_up(trafficBytes / (size_t)nc, 16) * 16;
+  const size_t cellSize = div_up(div_up(minTraffic, trafficPerByte), 16) * 16;
+  const size_t elementsPerCell = cellSize / (size_t)ts;
+  const size_t cells = div_up(count * (size_t)ts, cellSize);
+  const size_t trafficPerCell = cellSize * trafficPerByte;
+  size_t cellsPerChannel = div_up(trafficPerChannel, trafficPerCell);
+  if (cellsPerChannel > cells) cellsPerChannel = cells;
+  /* the traffic per channel divides by the task's channel count nc, the bounds below compare with the
+   * communicator's (nMaxChannels[kind] = comm->nChannels, enqueue.cc:583) */
+  size_t cellsLo;
+  if (nchannels == 1) cellsLo = cells; /* channelId + 1 == nMaxChannels */
+  else {
+    cellsLo = div_up(trafficPerChannel, trafficPerCell);
+    if (cellsLo > cells) cellsLo = cells;
+  }
+  long nMid = (long)((cells - cellsLo) / cellsPerChannel);
+  size_t cellsHi = (cells - cellsLo) % cellsPerChannel;
+  long used = (cellsLo != 0) + nMid + (cellsHi != 0);
+  if (nchannels < used) { /* overflowed the channels */
+    nMid = nchannels - 2;
+    cellsPerChannel = (cells - cellsLo) / (size_t)(nMid + 1);
+    cellsHi = cellsPerChannel + (cells - cellsLo) % (size_t)(nMid + 1);
+  }
+  if (cellsHi == 0 && nMid != 0) {
+    cellsHi = cellsPerChannel;
+    nMid -= 1;
+  }
+  /* cellsLo == 0 cannot happen for the first task of a plan (count > 0) */
+  size_t countMid = nMid != 0 ? cellsPerChannel * elementsPerCell : 0;
+  size_t countLo = cellsLo * elementsPerCell;
+  size_t countHi = cellsHi * elementsPerCell;
+  const size_t excess = cells * elementsPerCell - count;
+  if (countHi != 0) countHi -= excess;
+  else countLo -= excess;
+  used = (countLo != 0) + nMid + (cellsHi != 0);
+  /* chunk (enqueue.cc:2222-2225, 2321): SIMPLE grain 512 bytes */
+  size_t chunkBytes = buffsize / 8 * 4;
+  chunkBytes = chunkBytes / 512 * 512;
+  plan[0] = (uint64_t)used;
+  plan[1] = countLo;
+  plan[2] = countMid;
+  plan[3] = countHi;
+  plan[4] = chunkBytes / (size_t)ts;
+  return 0;
+}
+
+/* AllReduce in the reference's RING/SIMPLE order at full size: element e of channel part [off, off + cnt) in
+ * loop l = (e - off) / (n * chunk) lies in chunk q of that loop and is finalised by ring position q, i.e. folded
+ * from q + 1 (all_reduce.h:42-81; ring index = rank). */
+int oracle_all_reduce_ring_nccl(int dt, int devop, uint64_t arg, int n, const void* const* in, size_t count,
+                                void* out, int nchannels, size_t buffsize) {
+  int ts = oracle_type_size(dt);
+  if (ts <= 0 || n <= 0) return 4;
+  if (count == 0) return 0;
+  if (n == 1) return oracle_all_reduce(dt, devop, arg, n, in, count, out);
+  uint64_t plan[5];
+  if (oracle_ring_nccl_plan(count, ts, n, nchannels, buffsize, plan)) return 4;
+  const int nch = (int)plan[0];
+  const size_t epp = (size_t)(16 / ts);
+  for (int c = 0; c < nch; c++) {
+    size_t off, cnt; /* ncclCollCbdPart (device.h:337-361) with channelLo = 0, channelHi = nch - 1 */
+    if (c == 0) { off = 0; cnt = plan[1]; }
+    else if (c == nch - 1) { off = plan[1] + (size_t)(nch - 2) * plan[2]; cnt = plan[3]; }
+    else { off = plan[1] + (size_t)(c - 1) * plan[2]; cnt = plan[2]; }
+    size_t chunk = plan[4];
+    const size_t loopCount = (size_t)n * chunk;
+    for (size_t eo = 0; eo < cnt; eo += loopCount) {
+      const size_t rem = cnt - eo;
+      if (rem < loopCount) chunk = div_up(div_up(rem, (size_t)n), epp) * epp;
+      const size_t len = rem < loopCount ? rem : loopCount;
+#pragma omp parallel for schedule(static)
+      for (size_t j = 0; j < len; j++) {
+        const int q = (int)(j / chunk);
+        const size_t i = off + eo + j;
+        st(dt, out, i, fold_elem(dt, devop, arg, n, in, i, (q + 1) % n));
+      }
+    }
   }
   return 0;
 }

@@ -4,7 +4,8 @@ reference's reduction semantics (not the C oracle, which these fixtures pin).
 
 Reference rules restated (NVIDIA/nccl 2.30.7):
   - ring fold order: AllReduce block c (c = i // chunk, chunk = alignUp(divUp(count,n), 16/sizeof(T)),
-    src/device/all_reduce.h:38-66) folds ranks c+1, c+2, ..., c; ReduceScatter block d folds d+1..d
+    src/device/all_reduce.h:38-66) folds ranks c+1, c+2, ..., c — and, for NCCL_ALGO=RING at full size, the
+    reference's own channel parts and loops (ring_parts / ring_owners below); ReduceScatter block d folds d+1..d
     (reduce_scatter.h:34-55); Reduce folds root+1..root (reduce.h:34-52).
   - every hop rounds to T (the FIFO holds T); acc_new = f(pre(x_local), acc) (common_kernel.h:83-121)
   - Min/Max/Sum/Prod semantics of reduce_kernel.h; avg = PreMulSum(1/n) on floats, SumPostDiv on ints.
@@ -119,6 +120,64 @@ def allreduce(kind, dtype, ins):
     return out
 
 
+def ring_parts(count, esize, n, nchannels, buffsize):
+    """The reference's RING/SIMPLE AllReduce partition of one task on a communicator of `nchannels` channels
+    (restated from src/enqueue.cc:2091-2097 channel shrink, :576-757 continuous-byte-distribution over 16 KiB
+    cells with the first channel's part sized to the traffic per channel, :2222-2321 chunk = buffsize / 8 * 4 in
+    512-byte grains): returns the element counts of the channel parts, in channel order, and the chunk."""
+    nbytes = count * esize
+    nc = nchannels
+    while nc > 1 and nbytes < nc * 512 * 64:
+        nc -= 1
+    cell = 16384                              # 32 KiB minimum traffic / 2 traffic bytes per AllReduce byte
+    ncells = -(-nbytes // cell)
+    per_channel = -(-(max(32768, 2 * nbytes) // nc) // 16) * 16
+    per = -(-per_channel // (2 * cell))       # cells of traffic per channel
+    step = min(ncells, per)
+    first = ncells if nchannels == 1 else min(ncells, per)
+    mids, last = divmod(ncells - first, step)
+    if (first > 0) + mids + (last > 0) > nchannels:
+        mids = nchannels - 2
+        step = (ncells - first) // (mids + 1)
+        last = step + (ncells - first) % (mids + 1)
+    if last == 0 and mids:
+        last, mids = step, mids - 1
+    cells = [first] + [step] * mids + ([last] if last else [])
+    parts = [c * cell // esize for c in cells]
+    parts[-1] -= ncells * cell // esize - count
+    chunk = (buffsize // 8 * 4) // 512 * 512 // esize
+    return parts, chunk
+
+
+def ring_owners(count, esize, n, nchannels, buffsize):
+    """Ring position that finalises each element: inside each channel part, loops of n chunks; the last loop's
+    chunk is re-cut to alignUp(divUp(rem, n), 16 / esize) (src/device/all_reduce.h:34-38)."""
+    parts, chunk = ring_parts(count, esize, n, nchannels, buffsize)
+    epp = 16 // esize
+    owner = np.empty(count, dtype=np.int64)
+    base = 0
+    for p in parts:
+        for start in range(0, p, n * chunk):
+            rem = p - start
+            ck = chunk if rem >= n * chunk else -(-(-(-rem // n)) // epp) * epp
+            j = np.arange(min(rem, n * chunk))
+            owner[base + start: base + start + j.size] = j // ck
+        base += p
+    assert base == count
+    return owner
+
+
+def allreduce_ring(kind, dtype, ins, nchannels, buffsize):
+    n, count = len(ins), ins[0].size
+    owner = ring_owners(count, ESIZE[dtype], n, nchannels, buffsize)
+    out = np.empty_like(ins[0])
+    for c in range(n):
+        idx = np.nonzero(owner == c)[0]
+        if idx.size:
+            out[idx] = fold(kind, dtype, ins, idx, (c + 1) % n, n)
+    return out
+
+
 def reducescatter(kind, dtype, ins):
     n = len(ins)
     rc = ins[0].size // n
@@ -141,6 +200,13 @@ CASES = [
     ("reducescatter", "sum", "f32", 4, 4 * 1001), ("reducescatter", "sum", "bf16", 8, 8 * 301),
     ("reducescatter", "max", "u32", 2, 2 * 1000),
     ("reduce", "min", "i32", 8, 3000), ("reduce", "max", "i32", 8, 3000), ("reduce", "sum", "f32", 4, 3000),
+]
+# NCCL_ALGO=RING AllReduce in the reference's full-size partition: (op, dtype, n, count, channels, NCCL_BUFFSIZE);
+# small buffer sizes give several channel parts and several loops (the last one re-cut) at fixture sizes
+RING_CASES = [
+    ("sum", "f32", 3, 20000, 4, 16384), ("sum", "bf16", 4, 50001, 8, 16384), ("sum", "f16", 2, 70000, 3, 32768),
+    ("max", "f32", 5, 30011, 6, 8192), ("avg", "f32", 8, 40000, 5, 16384), ("sum", "i32", 3, 9000, 2, 8192),
+    ("sum", "f32", 2, 300_000, 7, 65536),
 ]
 
 
@@ -166,7 +232,16 @@ def main():
             d["out"] = reduce_root(kind, dtype, ins, root)
             name += f"_root{root}"
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
-    print(f"wrote {len(CASES)} fixtures to {HERE}")
+    for j, (kind, dtype, n, count, nch, buffsize) in enumerate(RING_CASES):
+        ins = gen_inputs(rng, dtype, n, count)
+        d = {"coll": "allreduce_ring", "dtype": NCCL_DT[dtype], "op": NCCL_OP[kind], "n": n, "nchannels": nch,
+             "buffsize": buffsize}
+        for r, x in enumerate(ins):
+            d[f"in{r}"] = x
+        d["out"] = allreduce_ring(kind, dtype, ins, nch, buffsize)
+        name = f"{len(CASES) + j:02d}_allreduce_ring_{kind}_{dtype}_n{n}_k{nch}"
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+    print(f"wrote {len(CASES) + len(RING_CASES)} fixtures to {HERE}")
 
 
 if __name__ == "__main__":

@@ -2,6 +2,8 @@
 device buffers and compare with the CPU oracle. Imported by tests only."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 
 import oracle
@@ -43,10 +45,49 @@ def make_inputs(n: int, dtype: int, count: int, seed: int, kind: int = 0):
     return [oracle.fill(dtype, seed * 131 + r, count, kind) for r in range(n)]
 
 
+def _env_int(name: str, default: int) -> int:
+    v = os.environ.get(name)
+    return int(v) if v not in (None, "") else default
+
+
+def ring_channels(n: int, ranks_per_gpu: int | None = None) -> int:
+    """The channel count K a NCCL_ALGO=RING AllReduce is planned on (enqueue.cc ringParts: the communicator's
+    co-resident channel cap): NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS (default 256) capped at 2 workgroups per CU
+    divided by the ranks per GPU (init.cc computeChannelCap; every test rank shares the box's one GPU)."""
+    import torch
+    k = _env_int("NCCL_MAX_CTAS", _env_int("NCCL_MAX_NCHANNELS", 256))
+    k = max(1, min(k, 256))
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    return max(1, min(k, 2 * cus // (ranks_per_gpu or n)))
+
+
+def ring_runs(n: int) -> bool:
+    """Whether NCCL_ALGO=RING (from the environment the communicator was created under) runs the ring kernel for
+    an AllReduce: it needs the Simple protocol and two staging slots (enqueue.cc planColl)."""
+    if os.environ.get("NCCL_ALGO", "").upper() != "RING" or n < 2:
+        return False
+    proto = os.environ.get("NCCL_PROTO", "")
+    if proto:
+        toks = {t.strip().lower() for t in proto.lstrip("^").split(",")}
+        simple = ("simple" not in toks) if proto.startswith("^") else ("simple" in toks)
+        if not simple:
+            return False
+    return _env_int("NCCL_AMD_NSLOTS", 2) >= 2
+
+
 def expected(coll: str, inputs, dtype: int, op: int, root: int = 0, algo: str = ""):
     if coll == "allreduce":
-        # NCCL_ALGO=TREE folds every element in the chain's order; every other path in the ring's
-        out = oracle.all_reduce_chain(inputs, dtype, op) if algo == "TREE" else oracle.all_reduce(inputs, dtype, op)
+        # NCCL_ALGO=TREE folds every element in the chain's order; NCCL_ALGO=RING in the reference's ring order
+        # over its own channel parts and loops (NCCL_MAX_CTAS / NCCL_BUFFSIZE as set for the communicator);
+        # every other path in the one-loop ring order
+        n = len(inputs)
+        algo = algo or os.environ.get("NCCL_ALGO", "").upper()
+        if algo == "TREE":
+            out = oracle.all_reduce_chain(inputs, dtype, op)
+        elif algo == "RING" and ring_runs(n):
+            out = oracle.all_reduce_ring_nccl(inputs, dtype, op, ring_channels(n), _env_int("NCCL_BUFFSIZE", 0))
+        else:
+            out = oracle.all_reduce(inputs, dtype, op)
         return [out] * len(inputs)
     if coll == "reducescatter":
         return oracle.reduce_scatter(inputs, dtype, op)

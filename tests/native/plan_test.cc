@@ -5,7 +5,7 @@
 //
 //   plan_test NRANKS FUNC(ar|rs|ag|reduce) DTYPE COUNT [ALIGN_OFFSET_BYTES] [CHANCAP]
 // prints one line: algo=<copy|onerank|direct|oneshot|ll|ring|chain> nch=<channels> part=<elements|payloads>
-//                  slice=<elements> steps=<n> chunk=<elements>
+//                  slice=<elements> steps=<n> chunk=<elements> (ring / chain also: kind= cbdlo= cbdhi=)
 //   plan_test NRANKS batch FUNC:DTYPE:COUNT[:OP] ...
 // plans the ops as one group (enqueue.cc planColl / batchable / launchBatch, in group.cc's order) and prints one
 // line per launch: algo=<...> ops=<ops in the launch> grid=<workgroups> ranges=<chOff+nch per op, comma-separated>
@@ -151,9 +151,9 @@ int main(int argc, char** argv) {
   const char* pipes[] = {"ring", "ring", "ring", "chain", "chain"};
   const LaunchPlan& p = gPlan;
   if (p.algo == ALGO_PIPE) {
-    printf("algo=%s kind=%d nch=%d part=%lu slice=%lu steps=%d chunk=%lu\n", pipes[p.pipeKind], p.pipeKind,
-           p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps,
-           (unsigned long)p.args.chunk);
+    printf("algo=%s kind=%d nch=%d part=%lu slice=%lu steps=%d chunk=%lu cbdlo=%lu cbdhi=%lu\n", pipes[p.pipeKind],
+           p.pipeKind, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps,
+           (unsigned long)p.args.chunk, (unsigned long)p.args.cbdLo, (unsigned long)p.args.cbdHi);
     return 0;
   }
   if (p.algo == ALGO_LL)

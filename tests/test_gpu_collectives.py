@@ -98,6 +98,8 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (3, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
             (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}),
             (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"}),
+            # the reference's ring partition with many channel parts and loops at test sizes (small chunks)
+            (3, {"NCCL_ALGO": "RING", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "5"}),
             # cross-process memory: every dma-buf import refused -> the hipIpc handle fallback (ipc.cc); legacy
             # handles only (NCCL_AMD_IPC=legacy) run where the runtime is 7.2+, see test_legacy_ipc_runtime_gate
             (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}),
@@ -615,8 +617,9 @@ def test_forced_ring_and_tree(built, algo, nranks, monkeypatch):
     """NCCL_ALGO=RING / TREE run the reference's own algorithms (pipe.h): the ring for AllReduce /
     ReduceScatter / AllGather and the chain to the root for Reduce (RING), the intra-node tree = chain for
     AllReduce (TREE; RS / AG / Reduce fall back to the default plan, as the reference has no tree for them).
-    Bit-exact vs the oracle: the ring folds in the oracle's order, the chain in oracle_all_reduce_chain's.
-    Tiny slots force many pipeline hops and credit wrap-around."""
+    Bit-exact vs the oracle: the ring AllReduce folds in the reference's own partition (channel parts, loops
+    of n chunks, oracle_all_reduce_ring_nccl), the chain in oracle_all_reduce_chain's order. Tiny slots force
+    many pipeline hops and credit wrap-around; a small NCCL_BUFFSIZE (chunk) many ring loops per channel."""
     torch = _torch()
     import nccl_amd
     from tests import gpu_cases as G
@@ -625,7 +628,8 @@ def test_forced_ring_and_tree(built, algo, nranks, monkeypatch):
     torch.cuda.set_device(0)
     errs = []
     # (the ring needs >= 2 slots per link, enqueue.cc; the chain also runs with 1)
-    for env in ({}, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2" if algo == "RING" else "1"}):
+    for env in ({}, {"NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2" if algo == "RING" else "1",
+                     "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "6"}):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
         comms = nccl_amd.Communicator.init_all([0] * nranks)

@@ -2,7 +2,8 @@
 independent numpy restatement of the reference's fold order and arithmetic): every fixture runs through
 the C ABI with its own rank count — one process per rank, all on the box's one GPU, HIP IPC between
 them — under the default size table and with each protocol forced (LL, one-shot, direct), and every
-rank's output must match the fixture bit for bit."""
+rank's output must match the fixture bit for bit. The NCCL_ALGO=RING fixtures (the reference's full-size ring
+partition) run on a ring communicator of their own channel count and NCCL_BUFFSIZE."""
 import glob
 import multiprocessing as mp
 import os
@@ -19,7 +20,7 @@ FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
 # protocol settings, each its own communicator (tuning knobs are read at init)
 SETTINGS = [{}, {"NCCL_PROTO": "LL"}, {"NCCL_PROTO": "^LL", "NCCL_ALGO": "ONESHOT"},
             {"NCCL_PROTO": "^LL", "NCCL_ALGO": "DIRECT"}]
-KNOBS = ("NCCL_PROTO", "NCCL_ALGO")
+KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_MAX_CTAS", "NCCL_BUFFSIZE")
 
 
 def _fixtures(n):
@@ -31,6 +32,13 @@ def _fixtures(n):
     return out
 
 
+def _ring_setting(z):
+    """NCCL_ALGO=RING fixtures (the reference's full-size ring partition) run on a ring communicator of the
+    fixture's channel count and NCCL_BUFFSIZE only."""
+    return {"NCCL_ALGO": "RING", "NCCL_PROTO": "Simple", "NCCL_MAX_CTAS": str(int(z["nchannels"])),
+            "NCCL_BUFFSIZE": str(int(z["buffsize"]))}
+
+
 def _worker(rank, n, uids, q):
     try:
         os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "30000"
@@ -40,14 +48,18 @@ def _worker(rank, n, uids, q):
         torch.cuda.set_device(0)
         dev = torch.device("cuda", 0)
         errs = []
-        for setting, uid in zip(SETTINGS, uids):
+        fixtures = _fixtures(n)
+        runs = [(setting, [f for f in fixtures if str(f[1]["coll"]) != "allreduce_ring"]) for setting in SETTINGS]
+        runs += [(_ring_setting(z), [(name, z)]) for name, z in fixtures if str(z["coll"]) == "allreduce_ring"]
+        for (setting, fx), uid in zip(runs, uids):
             for k in KNOBS:
                 os.environ.pop(k, None)
             os.environ.update(setting)
             comm = nccl_amd.Communicator.init(n, rank, uid)
             s = torch.cuda.Stream()
-            for name, z in _fixtures(n):
+            for name, z in fx:
                 coll, dtype, op = str(z["coll"]), int(z["dtype"]), int(z["op"])
+                coll = "allreduce" if coll == "allreduce_ring" else coll
                 root = int(z["root"]) if "root" in z else 0
                 x = z[f"in{rank}"]
                 want = z[f"out{rank}"] if coll == "reducescatter" else z["out"]
@@ -81,7 +93,8 @@ def test_golden_fixtures(built, n):
     import torch
     assert torch.cuda.is_available(), "GPU test on a box without a GPU"
     import nccl_amd
-    uids = [nccl_amd.get_unique_id() for _ in SETTINGS]
+    nring = sum(str(z["coll"]) == "allreduce_ring" for _, z in _fixtures(n))
+    uids = [nccl_amd.get_unique_id() for _ in range(len(SETTINGS) + nring)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     ps = [ctx.Process(target=_worker, args=(r, n, uids, q)) for r in range(n)]

@@ -68,6 +68,9 @@ def test_oracle_matches_golden(built, fname):
     if coll == "allreduce":
         got = [oracle.all_reduce(ins, dtype, op)]
         want = [z["out"]]
+    elif coll == "allreduce_ring":  # NCCL_ALGO=RING at full size: the reference's channel parts and loops
+        got = [oracle.all_reduce_ring_nccl(ins, dtype, op, int(z["nchannels"]), int(z["buffsize"]))]
+        want = [z["out"]]
     elif coll == "reducescatter":
         got = oracle.reduce_scatter(ins, dtype, op)
         want = [z[f"out{r}"] for r in range(n)]
@@ -141,3 +144,40 @@ def test_cpu_baseline_equals_oracle(built):
     out, used = oracle.cpu_allreduce_f32(ins, 2)
     assert used >= 1
     assert np.array_equal(out, oracle.all_reduce(ins, 7, 0))
+
+
+def test_ring_partition_matches_golden_restatement(built):
+    """The C oracle's RING/SIMPLE partition (oracle_ring_nccl_plan) against the independent numpy restatement of
+    tests/golden/make_golden.py over a sweep of sizes, types, rank and channel counts and NCCL_BUFFSIZE values;
+    the parts tile [0, count) and every plan uses at most the communicator's channels."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    rng = np.random.default_rng(8)
+    counts = [1, 3, 4096, 8191, 100_003, 1 << 20, 67_108_864, 536_870_912] + [int(x) for x in rng.integers(1, 1 << 27, 40)]
+    for count in counts:
+        for es in (1, 2, 4, 8):
+            for n, k in ((2, 1), (2, 256), (3, 7), (8, 32), (8, 64), (4, 2), (5, 3)):
+                for buff in (0, 16384, 1 << 20):
+                    nch, lo, mid, hi, chunk = oracle.ring_nccl_plan(count, es, n, k, buff)
+                    parts, ck = mg.ring_parts(count, es, n, k, buff or (4 << 20))
+                    assert [lo] + [mid] * (nch - 2) + ([hi] if nch > 1 else []) == parts, (count, es, n, k, buff)
+                    assert ck == chunk and 1 <= nch <= k and sum(parts) == count and min(parts) > 0
+
+
+def test_ring_order_is_the_one_loop_order_when_one_loop(built):
+    """On one channel and one loop the reference's ring order is the one-loop order every other path uses;
+    beyond that the finalising ring position moves (so float sums differ), while integer sums never do."""
+    for dt, count in ((7, 1000), (9, 4099), (6, 30_000)):
+        ins = [oracle.fill(dt, 50 + r, count) for r in range(3)]
+        assert np.array_equal(oracle.all_reduce_ring_nccl(ins, dt, 0, 1), oracle.all_reduce(ins, dt, 0))
+    ins = [oracle.fill(9, 70 + r, 300_000) for r in range(3)]  # bf16: every hop rounds
+    a, b = oracle.all_reduce_ring_nccl(ins, 9, 0, 16, 16384), oracle.all_reduce(ins, 9, 0)
+    assert not np.array_equal(a, b)
+    fa, fb = oracle.to_f32(9, a), oracle.to_f32(9, b)
+    exact = sum(oracle.to_f32(9, x).astype(np.float64) for x in ins)
+    bound = oracle.float_tolerance(9, ins, fb)
+    assert np.all(np.abs(fa - exact) <= bound) and np.all(np.abs(fb - exact) <= bound)
+    ins = [oracle.fill(2, 90 + r, 300_000) for r in range(3)]
+    assert np.array_equal(oracle.all_reduce_ring_nccl(ins, 2, 0, 16, 16384), oracle.all_reduce(ins, 2, 0))

@@ -155,7 +155,8 @@ def test_forced_reference_algorithms(exe, func, algo, want):
         assert p["algo"] == want[0], (n, count, p)
         if want[1] is not None:
             assert p["kind"] == want[1]
-            assert p["part"] * p["nch"] >= p["chunk"] and p["steps"] == -(-p["part"] // p["slice"])
+            if want[1] != 0:  # (the ring AllReduce's partition: test_ring_allreduce_takes_the_reference_partition)
+                assert p["part"] * p["nch"] >= p["chunk"] and p["steps"] == -(-p["part"] // p["slice"])
             if want[0] == "chain":
                 assert p["chunk"] == count
 
@@ -254,3 +255,25 @@ def test_link_channel_budget(exe, n, want):
         assert plan(exe, n, "ar", 7, (256 << 20) // 4, NCCL_AMD_LINK_CHANNELS=16)["nch"] == 16
         # the co-residency cap still applies below the budget (several ranks per GPU)
         assert plan(exe, n, "ar", 7, (256 << 20) // 4, chancap=24)["nch"] == 24
+
+
+def test_ring_allreduce_takes_the_reference_partition(exe, built):
+    """NCCL_ALGO=RING AllReduce is planned on the reference's own channel parts and chunk (enqueue.cc ringParts;
+    reference enqueue.cc:576-757, 2091-2097, 2222-2321), identical to the C oracle's restatement over a sweep
+    of sizes, types, rank counts, channel caps and NCCL_BUFFSIZE values."""
+    import numpy as np
+    import oracle
+    rng = np.random.default_rng(3)
+    counts = [1, 7, 4099, 100_003, 1 << 20, 67_108_864] + [int(x) for x in rng.integers(1, 1 << 26, 12)]
+    for count in counts:
+        for dt in (0, 6, 7, 8):
+            for n, k in ((2, 256), (3, 7), (8, 32), (4, 1)):
+                for buff in (None, 16384):
+                    env = {"NCCL_ALGO": "RING"}
+                    if buff:
+                        env["NCCL_BUFFSIZE"] = buff
+                    p = plan(exe, n, "ar", dt, count, chancap=k, **env)
+                    want = oracle.ring_nccl_plan(count, SIZES[dt], n, k, buff or 0)
+                    assert p["algo"] == "ring", p
+                    assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (count, dt, n, k, buff)
+                    assert 0 < p["slice"] <= p["chunk"] and p["slice"] % (16 // SIZES[dt]) == 0
