@@ -206,7 +206,7 @@ CASES = [
 RING_CASES = [
     ("sum", "f32", 3, 20000, 4, 16384), ("sum", "bf16", 4, 50001, 8, 16384), ("sum", "f16", 2, 70000, 3, 32768),
     ("max", "f32", 5, 30011, 6, 8192), ("avg", "f32", 8, 40000, 5, 16384), ("sum", "i32", 3, 9000, 2, 8192),
-    ("sum", "f32", 2, 300_000, 7, 65536),
+    ("sum", "f32", 2, 120_000, 7, 65536),
 ]
 
 
