@@ -401,7 +401,8 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
     """Buckets that start and end in pinned host memory: H2D copy + AllReduce + D2H copy per step."""
     import torch
     S = count * 4
-    h_in = torch.empty(count, dtype=torch.float32, pin_memory=True).uniform_(-1, 1)
+    # dyadic values k/256: every sum is exact in any fold order, so the chunked bucket checks against the whole one
+    h_in = (torch.randint(-1024, 1025, (count,), dtype=torch.int32).float() / 256).pin_memory()
     h_out = torch.empty(count, dtype=torch.float32, pin_memory=True)
     d_in = torch.empty(count, dtype=torch.float32, device="cuda")
     d_out = torch.empty_like(d_in)
@@ -416,9 +417,49 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
     ms_dev = _time_ms(lambda: comm.all_reduce_raw(d_in.data_ptr(), d_out.data_ptr(), count, 7, 0,
                                                   stream.cuda_stream), stream, 5, warmup=2)
     ms_dev = max_over_ranks(dist, [ms_dev])[0]
+    # pipelined: the bucket in chunks over three streams — H2D of chunk k+1, the AllReduce of chunk k and the D2H
+    # of chunk k-1 overlap, so both PCIe directions stay busy at once (the reference's proxy pipelines its
+    # network-staged transfers the same way, src/proxy.cc:954-1012)
+    nchunk = 16
+    cc = count // nchunk
+    s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
+    ev_start = torch.cuda.Event()
+    ev_in = [torch.cuda.Event() for _ in range(nchunk)]
+    ev_ar = [torch.cuda.Event() for _ in range(nchunk)]
+    ev_end = torch.cuda.Event()
+
+    def piped():
+        ev_start.record(stream)
+        s_in.wait_event(ev_start)
+        s_out.wait_event(ev_start)
+        for k in range(nchunk):
+            lo, hi = k * cc, (k + 1) * cc if k + 1 < nchunk else count
+            with torch.cuda.stream(s_in):
+                d_in[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
+                ev_in[k].record(s_in)
+            stream.wait_event(ev_in[k])
+            comm.all_reduce_raw(d_in[lo:].data_ptr(), d_out[lo:].data_ptr(), hi - lo, 7, 0, stream.cuda_stream)
+            ev_ar[k].record(stream)
+            with torch.cuda.stream(s_out):
+                s_out.wait_event(ev_ar[k])
+                h_out[lo:hi].copy_(d_out[lo:hi], non_blocking=True)
+        ev_end.record(s_out)
+        stream.wait_event(ev_end)
+
+    ms_p = _time_ms(piped, stream, 5, warmup=2)
+    ms_p = max_over_ranks(dist, [ms_p])[0]
+    torch.cuda.synchronize()
+    ref = h_out.clone()
+    step()
+    torch.cuda.synchronize()
+    same = bool(torch.equal(ref, h_out))  # the pipelined bucket equals the one-stream result bit for bit
     return {"bytes_per_rank": S, "ms_per_step": round(ms, 4), "algbw_GBps_incl_pcie": round(S / (ms * 1e-3) / 1e9, 2),
             "device_resident_ms": round(ms_dev, 4),
-            "method": "pinned hipMemcpyAsync H2D + ncclAllReduce + D2H on one stream, HIP events"}
+            "method": "pinned hipMemcpyAsync H2D + ncclAllReduce + D2H on one stream, HIP events",
+            "pipelined": {"chunks": nchunk, "ms_per_step": round(ms_p, 4),
+                          "algbw_GBps_incl_pcie": round(S / (ms_p * 1e-3) / 1e9, 2),
+                          "check": "pass" if same else "FAIL",
+                          "method": "16 chunks: H2D stream, AllReduce on the launch stream, D2H stream, event-chained"}}
 
 
 def cpu_baseline(count: int, budget_s: float, nbuf: int = 8):

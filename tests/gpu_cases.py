@@ -63,7 +63,9 @@ def ring_channels(n: int, ranks_per_gpu: int | None = None) -> int:
 
 def ring_runs(n: int) -> bool:
     """Whether NCCL_ALGO=RING (from the environment the communicator was created under) runs the ring kernel for
-    an AllReduce: it needs the Simple protocol and two staging slots (enqueue.cc planColl)."""
+    an AllReduce: two staging slots are needed (enqueue.cc planColl). With only LL-class protocols enabled the LL
+    kernel takes what fits its line area and the ring the rest, a size rule this helper does not restate: the
+    tests never combine NCCL_ALGO=RING with an NCCL_PROTO that excludes Simple (ValueError)."""
     if os.environ.get("NCCL_ALGO", "").upper() != "RING" or n < 2:
         return False
     proto = os.environ.get("NCCL_PROTO", "")
@@ -71,7 +73,7 @@ def ring_runs(n: int) -> bool:
         toks = {t.strip().lower() for t in proto.lstrip("^").split(",")}
         simple = ("simple" not in toks) if proto.startswith("^") else ("simple" in toks)
         if not simple:
-            return False
+            raise ValueError(f"NCCL_ALGO=RING with NCCL_PROTO={proto}: the AllReduce order depends on the LL capacity")
     return _env_int("NCCL_AMD_NSLOTS", 2) >= 2
 
 
