@@ -419,8 +419,9 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
     ms_dev = max_over_ranks(dist, [ms_dev])[0]
     # pipelined: the bucket in chunks over three streams — H2D of chunk k+1, the AllReduce of chunk k and the D2H
     # of chunk k-1 overlap, so both PCIe directions stay busy at once (the reference's proxy pipelines its
-    # network-staged transfers the same way, src/proxy.cc:954-1012)
-    nchunk = 16
+    # network-staged transfers the same way, src/proxy.cc:954-1012). 4 chunks: 6.6 ms vs 7.6 ms at 16 (per-copy
+    # cost) and 9.5 ms serial on the MI355X box (scripts/host_pipe_probe.py, profiles/r03_host_staged_pipeline.json)
+    nchunk = 4
     cc = count // nchunk
     s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
     ev_start = torch.cuda.Event()
@@ -459,7 +460,8 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
             "pipelined": {"chunks": nchunk, "ms_per_step": round(ms_p, 4),
                           "algbw_GBps_incl_pcie": round(S / (ms_p * 1e-3) / 1e9, 2),
                           "check": "pass" if same else "FAIL",
-                          "method": "16 chunks: H2D stream, AllReduce on the launch stream, D2H stream, event-chained"}}
+                          "method": f"{nchunk} chunks: H2D stream, AllReduce on the launch stream, D2H stream, "
+                                    "event-chained"}}
 
 
 def cpu_baseline(count: int, budget_s: float, nbuf: int = 8):
