@@ -289,59 +289,115 @@ union PackU {
   T e[16 / sizeof(T)];
 };
 
-// fp8 fold over 16-byte packs (numerics.h fp8Decode4 / fp8RoundF / fp8Encode4): the accumulator lives as the
-// f32 values of its codes, each hop rounded to the value the per-element functor would store, the codes
-// written once at the end; the same element results as foldRange's generic path, at a fraction of the
-// conversion work (the fp8 fold is ALU-bound: profiles/r03_dtype_rates_n2_onegpu.json). One pack per thread
-// per batch, the next source's pack in flight; 16-byte aligned ranges only (the < 16-byte tail per element).
+// fp8 fold of one 16-byte pack in f32 (numerics.h fp8Decode4 / fp8RoundF / fp8Encode4): the accumulator lives as
+// the f32 values of its codes, each hop rounded to the value the per-element functor would store, the codes
+// written once at the end. Handles every code, NaN and Inf included.
+template <typename T, int OP>
+__device__ __forceinline__ u32x4 fp8PackF32(const Red<T, OP>& fn, int n, const char* const* src, uint64_t i) {
+  constexpr bool E5 = IsFp8<T>::e5m2;
+  u32x4 cur = __builtin_nontemporal_load((const u32x4*)src[0] + i), nxt = cur;
+  float acc[16];
+  for (int k = 0; k < n; k++) {
+    if (k + 1 < n) nxt = __builtin_nontemporal_load((const u32x4*)src[k + 1] + i);
+    float x[16];
+#pragma unroll
+    for (int w = 0; w < 4; w++) fp8Decode4<E5>(cur[w], x + 4 * w);
+    if constexpr (OP == DEV_PREMULSUM) {  // pre(x) = fromF(x * s), rounded like the functor
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        x[e] = opaqueF(x[e] * fn.s);
+        x[e + 1] = opaqueF(x[e + 1] * fn.s);
+        fp8RoundF<E5>(x[e], x[e + 1]);
+      }
+    }
+    if (k == 0) {
+#pragma unroll
+      for (int e = 0; e < 16; e++) acc[e] = x[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        float r0, r1;
+        if (OP == DEV_PROD) {
+          r0 = opaqueF(x[e] * acc[e]);
+          r1 = opaqueF(x[e + 1] * acc[e + 1]);
+        } else if (OP == DEV_MINMAX) {
+          r0 = fn.isMin ? minOrdered(x[e], acc[e]) : maxOrdered(x[e], acc[e]);
+          r1 = fn.isMin ? minOrdered(x[e + 1], acc[e + 1]) : maxOrdered(x[e + 1], acc[e + 1]);
+        } else {
+          r0 = x[e] + acc[e];
+          r1 = x[e + 1] + acc[e + 1];
+        }
+        fp8RoundF<E5>(r0, r1);
+        acc[e] = r0;
+        acc[e + 1] = r1;
+      }
+    }
+    cur = nxt;
+  }
+  u32x4 out;
+#pragma unroll
+  for (int w = 0; w < 4; w++) out[w] = fp8Encode4<E5>(acc + 4 * w);
+  return out;
+}
+
+// fp8 fold over 16-byte packs (the fp8 fold is ALU-bound: profiles/r03_dtype_rates_n2_onegpu.json). Default: the
+// packed-half path (numerics.h fp8DecodeH2 / fp8RoundH2 / fp8EncodeH2x2) — the reference's half arithmetic two
+// lanes per instruction, the accumulator as eight half pairs, one paired encode + decode per hop and lane pair;
+// a pack with a NaN / Inf code in any source is recomputed by fp8PackF32 (NCCL_AMD_FP8_H2=0: always). One pack per
+// thread per batch, the next source's pack in flight; 16-byte aligned ranges only (the < 16-byte tail per element).
+#ifndef NCCL_AMD_FP8_H2
+#define NCCL_AMD_FP8_H2 1
+#endif
 template <typename T, int OP>
 __device__ __forceinline__ void foldFp8Packs(const Red<T, OP>& fn, int n, const char* const* src, uint64_t nelem,
                                              char* dstLocal, char* const* dstPush, int nPush) {
   constexpr bool E5 = IsFp8<T>::e5m2;
   const uint64_t npk = nelem / 16;
+  const _Float16 sh = (_Float16)fn.s;  // PreMulSum scalar: an fp8 value, exact in half
+  const fp8h2 s2 = {sh, sh};
+  // a NaN / Inf scalar (a user PreMulSum op) can make NaN from finite codes: the f32 path then takes every pack
+  const uint32_t scalarSpecial = (OP == DEV_PREMULSUM && !(__builtin_fabsf(fn.s) <= 65504.0f)) ? 1u : 0u;
   for (uint64_t i = threadIdx.x; i < npk; i += kThreads) {
-    u32x4 cur = __builtin_nontemporal_load((const u32x4*)src[0] + i), nxt = cur;
-    float acc[16];
-    for (int k = 0; k < n; k++) {
-      if (k + 1 < n) nxt = __builtin_nontemporal_load((const u32x4*)src[k + 1] + i);
-      float x[16];
-#pragma unroll
-      for (int w = 0; w < 4; w++) fp8Decode4<E5>(cur[w], x + 4 * w);
-      if constexpr (OP == DEV_PREMULSUM) {  // pre(x) = fromF(x * s), rounded like the functor
-#pragma unroll
-        for (int e = 0; e < 16; e += 2) {
-          x[e] = opaqueF(x[e] * fn.s);
-          x[e + 1] = opaqueF(x[e + 1] * fn.s);
-          fp8RoundF<E5>(x[e], x[e + 1]);
-        }
-      }
-      if (k == 0) {
-#pragma unroll
-        for (int e = 0; e < 16; e++) acc[e] = x[e];
-      } else {
-#pragma unroll
-        for (int e = 0; e < 16; e += 2) {
-          float r0, r1;
-          if (OP == DEV_PROD) {
-            r0 = opaqueF(x[e] * acc[e]);
-            r1 = opaqueF(x[e + 1] * acc[e + 1]);
-          } else if (OP == DEV_MINMAX) {
-            r0 = fn.isMin ? minOrdered(x[e], acc[e]) : maxOrdered(x[e], acc[e]);
-            r1 = fn.isMin ? minOrdered(x[e + 1], acc[e + 1]) : maxOrdered(x[e + 1], acc[e + 1]);
-          } else {
-            r0 = x[e] + acc[e];
-            r1 = x[e + 1] + acc[e + 1];
-          }
-          fp8RoundF<E5>(r0, r1);
-          acc[e] = r0;
-          acc[e + 1] = r1;
-        }
-      }
-      cur = nxt;
-    }
     u32x4 out;
+    if (NCCL_AMD_FP8_H2) {
+      u32x4 cur = __builtin_nontemporal_load((const u32x4*)src[0] + i), nxt = cur;
+      fp8h2 acc[8];
+      uint32_t special = scalarSpecial;
+      for (int k = 0; k < n; k++) {
+        if (k + 1 < n) nxt = __builtin_nontemporal_load((const u32x4*)src[k + 1] + i);
+        special |= fp8Special<E5>(cur[0]) | fp8Special<E5>(cur[1]) | fp8Special<E5>(cur[2]) | fp8Special<E5>(cur[3]);
+        fp8h2 x[8];
 #pragma unroll
-    for (int w = 0; w < 4; w++) out[w] = fp8Encode4<E5>(acc + 4 * w);
+        for (int w = 0; w < 4; w++) {
+          x[2 * w] = fp8DecodeH2<E5>(cur[w], false);
+          x[2 * w + 1] = fp8DecodeH2<E5>(cur[w], true);
+        }
+        if constexpr (OP == DEV_PREMULSUM) {  // pre(x) = fromF(__hmul(x, s))
+#pragma unroll
+          for (int j = 0; j < 8; j++) x[j] = fp8RoundH2<E5>(x[j] * s2);
+        }
+        if (k == 0) {
+#pragma unroll
+          for (int j = 0; j < 8; j++) acc[j] = x[j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 8; j++) {
+            if (OP == DEV_MINMAX)  // finite values: IEEE minimum / maximum order -0 below +0, like minOrdered
+              acc[j] = fn.isMin ? __builtin_elementwise_minimum(x[j], acc[j]) : __builtin_elementwise_maximum(x[j], acc[j]);
+            else if (OP == DEV_PROD)
+              acc[j] = fp8RoundH2<E5>(x[j] * acc[j]);
+            else
+              acc[j] = fp8RoundH2<E5>(x[j] + acc[j]);
+          }
+        }
+        cur = nxt;
+      }
+#pragma unroll
+      for (int w = 0; w < 4; w++) out[w] = fp8EncodeH2x2<E5>(acc[2 * w], acc[2 * w + 1]);
+      if (__builtin_expect(special != 0, 0)) out = fp8PackF32<T, OP>(fn, n, src, i);
+    } else {
+      out = fp8PackF32<T, OP>(fn, n, src, i);
+    }
     if (dstLocal) __builtin_nontemporal_store(out, (u32x4*)dstLocal + i);
     for (int p = 0; p < nPush; p++) storeRemoteAt(remoteRsrc((u32x4*)dstPush[p] + (i - threadIdx.x)), threadIdx.x * 16u, out);
   }

@@ -364,6 +364,48 @@ __device__ inline void fp8RoundF(float& a, float& b) {
   a = ha != ha ? ha : d.x;
   b = hb != hb ? hb : d.y;
 }
+// ---- fp8 packs as packed halves (gfx950 v_cvt_scalef32_pk_f16_fp8 / _pk_fp8_f16, scale 1.0) ----
+// The reference computes every fp8 operation in half and converts back with saturation (reduce_kernel.h:461-487):
+// v_pk_add_f16 / v_pk_mul_f16 ARE __hadd / __hmul on two lanes, v_pk_maximum3_f16 / v_pk_minimum3_f16 clamp to
+// +-max finite (__NV_SATFINITE), and the packed converts move two codes per instruction. Probed on the MI355X
+// against the software conversions for every code and every half value (tests/native/fp8_f16_probe,
+// profiles/r03_fp8_f16_probe.json): decode exact, clamped encode exact, only NaN differs (every NaN decodes
+// negative; NaN encodes 0xff / 0xfe). The packed fold therefore runs only on packs with no NaN / Inf code in any
+// source (fp8Special): finite fp8 inputs never create NaN or Inf under satfinite, and a pack that holds one is
+// recomputed by the f32 path above.
+typedef _Float16 fp8h2 __attribute__((ext_vector_type(2)));
+typedef short fp8s2 __attribute__((ext_vector_type(2)));
+// codes 0, 1 (hi = false) or 2, 3 (hi = true) of w -> their values as two halves
+template <bool E5M2>
+__device__ inline fp8h2 fp8DecodeH2(uint32_t w, bool hi) {
+  if (hi) return E5M2 ? __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w, 1.0f, true) : __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w, 1.0f, true);
+  return E5M2 ? __builtin_amdgcn_cvt_scalef32_pk_f16_bf8(w, 1.0f, false) : __builtin_amdgcn_cvt_scalef32_pk_f16_fp8(w, 1.0f, false);
+}
+// nonzero when a byte of w is a NaN code (e4m3 S.1111.111) or a NaN / Inf code (e5m2 S.11111.xx)
+template <bool E5M2>
+__device__ inline uint32_t fp8Special(uint32_t w) {
+  return ((w & 0x7f7f7f7fu) + (E5M2 ? 0x04040404u : 0x01010101u)) & 0x80808080u;
+}
+// two finite half results -> the fp8 values fromF would store (satfinite clamp, RNE encode, decode)
+template <bool E5M2>
+__device__ inline fp8h2 fp8RoundH2(fp8h2 v) {
+  const _Float16 m = (_Float16)(E5M2 ? 57344.0f : 448.0f);
+  const fp8h2 hiB = {m, m}, loB = {-m, -m};
+  v = __builtin_elementwise_minimum(__builtin_elementwise_maximum(v, loB), hiB);
+  const fp8s2 old = __builtin_bit_cast(fp8s2, v);  // the high word of the encode is never read
+  const fp8s2 c = E5M2 ? __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(old, v, 1.0f, false)
+                       : __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(old, v, 1.0f, false);
+  return fp8DecodeH2<E5M2>(__builtin_bit_cast(uint32_t, c), false);
+}
+// four finite fp8 values (two halves each in a, b) -> four codes (exact: no rounding happens)
+template <bool E5M2>
+__device__ inline uint32_t fp8EncodeH2x2(fp8h2 a, fp8h2 b) {
+  fp8s2 w = __builtin_bit_cast(fp8s2, a);
+  w = E5M2 ? __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(w, a, 1.0f, false) : __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(w, a, 1.0f, false);
+  w = E5M2 ? __builtin_amdgcn_cvt_scalef32_pk_bf8_f16(w, b, 1.0f, true) : __builtin_amdgcn_cvt_scalef32_pk_fp8_f16(w, b, 1.0f, true);
+  return __builtin_bit_cast(uint32_t, w);
+}
+
 // four fp8 VALUES (fp8RoundF results or decoded codes: exact, no rounding) -> four codes; NaN -> sign | 0x7f
 template <bool E5M2>
 __device__ inline uint32_t fp8Encode4(const float* f) {

@@ -26,6 +26,17 @@ def test_fp8_convert_probe(built):
         assert r[f"{fmt}_decode_mismatch"] == 0 and r[f"{fmt}_encode_mismatch"] == 0, r
 
 
+def test_fp8_packed_half_probe(built):
+    """The packed fp8 <-> half converts the packed-half fold runs on (numerics.h fp8DecodeH2 / fp8RoundH2): decode
+    exact for every code, clamped encode exact for every non-NaN half (NaN packs take the f32 path)."""
+    exe = os.path.join(ROOT, "tests", "native", "fp8_f16_probe")
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    r = json.loads(out.stdout.strip().splitlines()[-1])
+    for fmt in ("e4m3", "e5m2"):
+        assert r[f"{fmt}_decode_mismatch"] == 0 and r[f"{fmt}_encode_clamped_mismatch"] == 0, r
+
+
 def _pairs(dtype):
     a = np.repeat(np.arange(256, dtype=np.uint8), 256)
     b = np.tile(np.arange(256, dtype=np.uint8), 256)
