@@ -425,10 +425,14 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
   // (4 reach the 128-VGPR cap and spill in MinMax); other 1-byte folds (fp8, Prod, PreMulSum, integer avg) unpack 16 elements per pack into
   // separate registers, so they keep one pack per batch to stay within the register budget (kCoResident;
   // two packs spilled up to 55 VGPRs for fp8)
-  constexpr bool kSwar = std::is_same<T, uint8_t>::value && Swar8<OP>::ok;
+  // (integer avg on 1-byte types: the Sum fold on four bytes per dword, then numerics.h swarDivBytes)
+  constexpr bool kSwarDiv = std::is_same<T, uint8_t>::value && OP == DEV_SUMPOSTDIV;
+  constexpr bool kSwar = std::is_same<T, uint8_t>::value && (Swar8<OP>::ok || kSwarDiv);
+  constexpr int kSwarOp = kSwarDiv ? DEV_SUM : OP;
   constexpr int U = sizeof(T) > 1 ? kFoldUnroll : kSwar ? kFoldUnrollSwar : kFoldUnroll1B;
-  uint32_t swarMask = 0;
-  if constexpr (kSwar) swarMask = (uint32_t)(uint8_t)fn.arg * 0x01010101u;
+  uint32_t swarMask = 0, divMagic = 0;
+  if constexpr (kSwar && !kSwarDiv) swarMask = (uint32_t)(uint8_t)fn.arg * 0x01010101u;
+  if constexpr (kSwarDiv) divMagic = swarDivMagic(fn.divisor);
   if constexpr (IsFp8<T>::value && NCCL_AMD_HW_FP8) {
     if (aligned) {
       foldFp8Packs<T, OP>(fn, n, src, nelem, dstLocal, dstPush, nPush);
@@ -457,7 +461,7 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
         for (int u = 0; u < U; u++) {
           if constexpr (kSwar) {
 #pragma unroll
-            for (int w = 0; w < 4; w++) acc[u].v[w] = k == 0 ? cur[u].v[w] : Swar8<OP>::red(cur[u].v[w], acc[u].v[w], swarMask);
+            for (int w = 0; w < 4; w++) acc[u].v[w] = k == 0 ? cur[u].v[w] : Swar8<kSwarOp>::red(cur[u].v[w], acc[u].v[w], swarMask);
           } else {
 #pragma unroll
             for (int e = 0; e < EPP; e++) {
@@ -475,8 +479,13 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
       for (int u = 0; u < U; u++) {
         uint64_t i = base + (uint64_t)u * kThreads;
         if (i >= npk) continue;
+        if constexpr (kSwarDiv) {
 #pragma unroll
-        for (int e = 0; e < EPP; e++) acc[u].e[e] = fn.post(acc[u].e[e]);
+          for (int w = 0; w < 4; w++) acc[u].v[w] = swarDivBytes(acc[u].v[w], divMagic, fn.isSigned);
+        } else {
+#pragma unroll
+          for (int e = 0; e < EPP; e++) acc[u].e[e] = fn.post(acc[u].e[e]);
+        }
         if (dstLocal) ls.put(threadIdx.x + u * kThreads, acc[u].v);
         for (int p = 0; p < nPush; p++) {
           // resource rebased on the batch's first pack: 32-bit offsets at any range size

@@ -444,4 +444,24 @@ template <> struct Swar8<2> {  // DEV_MINMAX: (a^m) < (b^m) ? a : b per byte; M 
   }
 };
 
+// SumPostDiv on 1-byte integers (integer avg): the fold is the byte-wise Sum (Swar8<0>, the sum wraps mod 256 for
+// either signedness) and the post-op divides each byte: magnitude / n, sign restored for signed types
+// (reduce_kernel.h:936-966). For a magnitude x <= 255 and a divisor 1 <= d <= 256 the quotient is
+// (x * M) >> 16 with M = ceil(2^16 / d) exactly (x * (M d - 2^16) < x d < 2^16), so no division is issued.
+// Bit-identical to Red<uint8_t, DEV_SUMPOSTDIV>::post on each byte (tests/test_numerics.py, every byte and d).
+__host__ __device__ inline uint32_t swarDivMagic(uint32_t d) { return (65536u + d - 1) / d; }
+__host__ __device__ inline uint32_t swarDivBytes(uint32_t w, uint32_t M, bool isSigned) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int b = 0; b < 4; b++) {
+    const uint32_t x = (w >> (8 * b)) & 0xffu;
+    const bool neg = isSigned && (x & 0x80u);
+    const uint32_t mag = neg ? ((0u - x) & 0xffu) : x;
+    uint32_t q = (mag * M) >> 16;
+    if (neg) q = 0u - q;
+    r |= (q & 0xffu) << (8 * b);
+  }
+  return r;
+}
+
 }  // namespace ncclamd

@@ -14,6 +14,7 @@ uint64_t nx_red(int dtype, int op, uint64_t arg, uint64_t a, uint64_t b);
 uint64_t nx_pre(int dtype, int op, uint64_t arg, uint64_t a);
 uint64_t nx_post(int dtype, int op, uint64_t arg, uint64_t a);
 uint32_t nx_swar8(int op, uint32_t mask, uint32_t a, uint32_t b);
+uint32_t nx_swar_div(uint32_t w, uint32_t d, int isSigned) { return swarDivBytes(w, swarDivMagic(d), isSigned != 0); }
 }
 uint32_t nx_swar8(int op, uint32_t mask, uint32_t a, uint32_t b) {
   uint32_t M = (mask & 0xff) * 0x01010101u;

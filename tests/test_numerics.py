@@ -28,6 +28,8 @@ def nx(built):
         getattr(L, f).argtypes = [I, I, U64, U64]
     L.nx_swar8.restype = ctypes.c_uint32
     L.nx_swar8.argtypes = [I, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]
+    L.nx_swar_div.restype = ctypes.c_uint32
+    L.nx_swar_div.argtypes = [ctypes.c_uint32, ctypes.c_uint32, I]
     L.nx_f32_to_fp8.restype = ctypes.c_uint8
     L.nx_f32_to_fp8.argtypes = [ctypes.c_float, I]
     L.nx_fp8_to_f32.restype = ctypes.c_float
@@ -146,3 +148,18 @@ def test_swar_bytes_match_functor(nx, op, mask):
                 ea, eb = (wa >> (8 * l)) & 0xff, (wb >> (8 * l)) & 0xff
                 want = nx.nx_red(1, op, mask, ea, eb)
                 assert (got >> (8 * l)) & 0xff == want, (op, mask, hex(wa), hex(wb), l)
+
+
+def test_swar_byte_division_matches_functor(nx):
+    """numerics.h swarDivBytes (the uint8 / int8 avg post-op on four bytes, multiply-shift instead of a divide)
+    equals Red<uint8_t, DEV_SUMPOSTDIV>::post — magnitude / n, sign restored — for every byte in every lane, every
+    rank count 1..16 and both signednesses."""
+    for d in range(1, 17):
+        for signed in (0, 1):
+            arg = (d << 1) | signed
+            for x in range(256):
+                w = x | (((x * 7 + 1) & 0xff) << 8) | (((x * 13 + 5) & 0xff) << 16) | (((255 - x) & 0xff) << 24)
+                got = nx.nx_swar_div(w, d, signed)
+                for l in range(4):
+                    want = nx.nx_post(1, 4, arg, (w >> (8 * l)) & 0xff)
+                    assert (got >> (8 * l)) & 0xff == want, (d, signed, hex(w), l)
