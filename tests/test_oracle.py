@@ -181,3 +181,17 @@ def test_ring_order_is_the_one_loop_order_when_one_loop(built):
     assert np.all(np.abs(fa - exact) <= bound) and np.all(np.abs(fb - exact) <= bound)
     ins = [oracle.fill(2, 90 + r, 300_000) for r in range(3)]
     assert np.array_equal(oracle.all_reduce_ring_nccl(ins, 2, 0, 16, 16384), oracle.all_reduce(ins, 2, 0))
+
+
+def test_two_ranks_fold_order_never_matters(built):
+    """At n = 2 every element folds red(pre(x_b), pre(x_a)) with {a, b} = {0, 1}, and Sum / Prod / Min / Max / avg
+    are commutative bit for bit (IEEE add and multiply, the ordered min / max), so the default one-loop order and
+    the reference's full-size ring partition give identical bits for every type: config C2 (fp32 Sum, 2 ranks)
+    equals the reference's RING/SIMPLE result on any channel count, not just within the float bound."""
+    for dt in (7, 9, 6, 10, 11, 8):
+        for op in (0, 1, 2, 3, 4):
+            ins = [oracle.fill(dt, 500 + 7 * dt + op + r, 200_003) for r in range(2)]
+            a = oracle.all_reduce(ins, dt, op)
+            for k, buff in ((1, 0), (7, 16384), (64, 65536)):
+                b = oracle.all_reduce_ring_nccl(ins, dt, op, k, buff)
+                assert np.array_equal(a.view(np.uint8), b.view(np.uint8)), (dt, op, k, buff)
