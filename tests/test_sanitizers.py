@@ -49,6 +49,10 @@ def test_planning_asan(sanitized):
                             (8, "ag", 0, 4097), (8, "reduce", 2, 1 << 25), (3, "reduce", 4, 777)):
         assert "algo=" in _run(exe, str(n), f, str(dt), str(count))
     _run(exe, "4", "ar", "7", str(1 << 22), NCCL_ALGO="TREE")
+    # the ring AllReduce's reference partition (enqueue.cc ringParts): one channel, many channels, tiny chunks
+    for n, dt, count, cap in ((2, 7, 1 << 26, 256), (3, 8, 100_003, 7), (8, 10, 5, 1), (4, 6, (1 << 30) + 3, 64)):
+        assert "algo=ring" in _run(exe, str(n), "ar", str(dt), str(count), "0", str(cap), NCCL_ALGO="RING",
+                                   NCCL_BUFFSIZE="16384")
     out = _run(exe, "2", "batch", *[f"rs:9:{2 * c}" for c in (100, 2000, 100_000, 1_000_000)], "ag:7:5000",
                *(["ar:7:100000"] * 10))
     assert out.count("algo=") == 5
