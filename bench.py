@@ -111,6 +111,12 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     where they get measured): RS+AG bf16 1 GiB bucket (configs[2]), AllReduce fp16 8 B..256 MiB sweep,
     LL / one-shot / direct / ring / tree (configs[3]: the reference's ring vs tree), Reduce int32 min/max 128 MiB root 0 (configs[4]); each with a
     size-independent exactness check, plus xGMI peer-copy probes for the roofline denominator."""
+    t_start = time.perf_counter()
+
+    def trace(part):  # BENCH_TRACE=1: when each suite part starts (diagnostics for stalls), on stderr
+        if os.environ.get("BENCH_TRACE"):
+            print(f"[rank {rank}] suite +{time.perf_counter() - t_start:.2f}s {part}", file=sys.stderr, flush=True)
+
     import torch
     import nccl_amd
     out = {} if out is None else out  # filled as it goes: a watchdog can report the finished parts
@@ -124,6 +130,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     def tmax(ms: float) -> float:
         return max_over_ranks(dist, [ms])[0]
 
+    trace("rs_ag_bf16")
     # --- configs[2]: ZeRO bucket, bf16, 1 GiB ---
     bucket = (64 if quick else 1024) * MIB
     cnt = bucket // 2
@@ -167,6 +174,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                                  "env": "NCCL_AMD_RS_PULL=1 NCCL_AMD_AG_PULL=1"}
     del send, shard, full, base
 
+    trace("ar_fp16_sweep")
     # --- configs[3]: fp16 AllReduce sweep: LL vs one-shot vs direct. Protocol/algorithm knobs are read at
     #     communicator init (like the reference's NCCL_PARAMs), so each column gets its own communicator ---
     top = (16 if quick else 256) * MIB
@@ -198,6 +206,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         cm.destroy()
     out["ar_fp16_sweep"] = [rows[k] for k in sorted(rows)]
 
+    trace("group_aggregation")
     # --- group aggregation: 32 small AllReduce ops in one ncclGroupStart/End,
     #     one LL launch vs one launch per op ---
     agg = {}
@@ -223,6 +232,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
             os.environ[k] = v
     del buf, res
 
+    trace("reduce_int32")
     # --- configs[4]: Reduce int32 min / max, 128 MiB, root 0 ---
     S = (16 if quick else 128) * MIB
     c = S // 4
@@ -246,6 +256,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     out["reduce_int32"] = red
     del send, recv, base
 
+    trace("symmetric_window")
     # --- symmetric windows (zero-copy pull kernels): the headline AllReduce and the
     #     fp16 latency curve with send/recv inside an NCCL_WIN_COLL_SYMMETRIC window ---
     S = (16 if quick else 256) * MIB
@@ -284,6 +295,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     comm.deregister_window(win)
     del win_t, sendw, recvw, base, hbuf, hres
 
+    trace("registered")
     # --- buffers registered with ncclCommRegister (zero-copy kernel in registered mode): the
     #     headline AllReduce on plain torch allocations, no window ---
     S = (16 if quick else 256) * MIB
@@ -307,6 +319,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         comm.deregister_buffer(h)
     del sendr, recvr, base
 
+    trace("staged_tuning")
     # --- staged-path tuning matrix at the headline size (data for the next tuning round: knobs are read
     #     at communicator init, so each setting gets its own communicator). Every column's result must equal the
     #     default column's bit for bit (same fold order), which checks the fence-free release over the links ---
@@ -330,6 +343,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
             os.environ.pop(k, None)
         os.environ.update(env)
         cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+        trace(f"staged_tuning {env or 'default'}")
         ms = tmax(_time_ms(lambda: cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, sp), stream, 10))
         torch.cuda.synchronize()
         if ref is None:
@@ -348,6 +362,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}", "runs": tuning}
     del xs, ys, ref
 
+    trace("xgmi_probe")
     # --- xGMI probes (rank 0, peer copies via hipMemcpyPeerAsync) ---
     ndev = torch.cuda.device_count()
     if rank == 0 and ndev > 1:

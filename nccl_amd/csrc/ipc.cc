@@ -328,7 +328,30 @@ ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
     return ncclInternalError;
   }
   int fd = -1;
-  HIPCHECK(hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0));
+  hipError_t e = paramInt("NCCL_AMD_IPC_FAIL_EXPORT", 0)  // tests: exercise the fallback below
+                     ? hipErrorInvalidValue
+                     : hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
+  const int err = errno;
+  if (e != hipSuccess) {
+    // Seen on the one-GPU box after many communicators and registrations in one process (bench.py's N = 4
+    // rehearsal): the runtime refuses the dma-buf export of a fresh slab with "invalid argument". The slab then
+    // goes to its peers as a hipIpc handle where the runtime can open one (below 2 GiB, or a 7.2+ runtime)
+    // instead of failing the communicator; the details are logged for the report.
+    (void)hipGetLastError();
+    hipDeviceptr_t ab = nullptr;
+    size_t as = 0;
+    const hipError_t ea = hipMemGetAddressRange(&ab, &as, (hipDeviceptr_t)base);
+    (void)hipGetLastError();
+    const bool fallback = ipcLegacyAllowed(hipRuntimeInfo().version, size, false) &&
+                          hipIpcGetMemHandle(&d->handle, base) == hipSuccess;
+    (void)hipGetLastError();
+    WARN("ipc: dma-buf export of %p (+%zu MiB) failed: %s (allocation %p +%zu MiB: %s; errno %d %s)%s", base,
+         size >> 20, hipGetErrorString(e), (void*)ab, as >> 20, hipGetErrorString(ea), err, strerror(err),
+         fallback ? "; peers open a hipIpc handle instead" : "");
+    if (!fallback) return ncclUnhandledCudaError;
+    d->legacy = 1;
+    return ncclSuccess;
+  }
   NCCLCHECK(ipcPublish(comm, fd, size, d));
   // A hipIpc handle rides along where the runtime can open it (below 2 GiB, or a 7.2+ runtime): an importer
   // whose runtime cannot map the dma-buf (never seen on one GPU; the first multi-GPU node decides) falls back
