@@ -295,30 +295,6 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     comm.deregister_window(win)
     del win_t, sendw, recvw, base, hbuf, hres
 
-    trace("registered")
-    # --- buffers registered with ncclCommRegister (zero-copy kernel in registered mode, DESIGN.md §10.3): the
-    #     headline AllReduce on plain torch allocations, no window ---
-    S = (16 if quick else 256) * MIB
-    c = S // 4
-    g.manual_seed(4322)
-    base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
-    sendr = base * (rank + 1)
-    recvr = torch.empty_like(sendr)
-    hs = [comm.register_buffer(sendr.data_ptr(), S), comm.register_buffer(recvr.data_ptr(), S)]
-    fn = lambda: comm.all_reduce_raw(sendr.data_ptr(), recvr.data_ptr(), c, 7, 0, sp)
-    ms = tmax(_time_ms(fn, stream, 20, warmup=5))
-    recvr.zero_()
-    fn()
-    torch.cuda.synchronize()
-    okr = bool(torch.equal(recvr, base * (n * (n + 1) / 2)))
-    out["registered"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, ncclCommRegister'd buffers, n={n}",
-                         "ms": round(ms, 4), "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
-                         "check": "pass (dyadic, exact)" if agree(okr) else "FAIL"}
-    torch.cuda.synchronize()
-    for h in hs:
-        comm.deregister_buffer(h)
-    del sendr, recvr, base
-
     trace("staged_tuning")
     # --- staged-path tuning matrix at the headline size (data for the next tuning round: knobs are read
     #     at communicator init, so each setting gets its own communicator). Every column's result must equal the
@@ -409,6 +385,34 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                 probe["store_atomicity"] = {"error": repr(e)}
         out["xgmi_probe"] = probe
         del src, dsts
+    if dist is not None:
+        dist.barrier()  # the other ranks wait here, not spinning in a collective, while rank 0 probes the links
+
+    trace("registered")
+    # --- buffers registered with ncclCommRegister (zero-copy kernel in registered mode, DESIGN.md §10.3): the
+    #     headline AllReduce on plain torch allocations, no window. Last: the newest path, and its deregistration
+    #     makes every peer release a mapping ---
+    S = (16 if quick else 256) * MIB
+    c = S // 4
+    g.manual_seed(4322)
+    base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
+    sendr = base * (rank + 1)
+    recvr = torch.empty_like(sendr)
+    hs = [comm.register_buffer(sendr.data_ptr(), S), comm.register_buffer(recvr.data_ptr(), S)]
+    fn = lambda: comm.all_reduce_raw(sendr.data_ptr(), recvr.data_ptr(), c, 7, 0, sp)
+    ms = tmax(_time_ms(fn, stream, 20, warmup=5))
+    recvr.zero_()
+    fn()
+    torch.cuda.synchronize()
+    okr = bool(torch.equal(recvr, base * (n * (n + 1) / 2)))
+    out["registered"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, ncclCommRegister'd buffers, n={n}",
+                         "ms": round(ms, 4), "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+                         "check": "pass (dyadic, exact)" if agree(okr) else "FAIL"}
+    torch.cuda.synchronize()
+    for h in hs:
+        comm.deregister_buffer(h)
+    del sendr, recvr, base
+
     return out
 
 
@@ -778,9 +782,16 @@ def main(argv=None):
         threading.Thread(target=watchdog, daemon=True).start()
         try:
             run_suite(comm, n, rank, dist, stream, quick=args.quick_suite, out=suite)
+            torch.cuda.synchronize()
         except Exception as e:  # secondary measurements never fail the headline line
-            suite["error"] = repr(e)
-        torch.cuda.synchronize()
+            # (a device error is sticky: report the headline with the parts that finished and leave at once; the
+            # other ranks end through their watchdogs)
+            suite["error"] = repr(e)[:600]
+            suite["seconds"] = round(time.perf_counter() - t_suite, 1)
+            done.set()
+            if rank == 0:
+                print(json.dumps(headline()), flush=True)
+            os._exit(0 if ok else 1)
         barrier()
         done.set()
         suite["seconds"] = round(time.perf_counter() - t_suite, 1)

@@ -122,6 +122,12 @@ struct IpcImport {  // one mapping of a peer's allocation in this process
 };
 struct FdServer;
 bool ipcLegacy();
+// Release peers' mappings whose owner deregistered them (ipc.cc): called on the caller's thread at library entry
+// points (not inside a stream capture of `stream`); a no-op unless a RELEASE request arrived.
+void ipcDrainReleases(hipStream_t stream);
+// Held around this library's device allocations, imports and releases (ipc.cc gMapMu): no allocation of ours can
+// interleave with a mapping being torn down on another thread (a non-blocking init runs on its own thread).
+std::mutex& ipcMapMutex();
 struct HipRuntimeInfo {
   int version;    // hipRuntimeGetVersion of the runtime bound in this process
   int driver;     // hipDriverGetVersion

@@ -764,6 +764,7 @@ ncclResult_t enqueueCheck(CollInfo* info) {
     groupRecordError(ret);
     return ret;
   }
+  ipcDrainReleases(info->stream);  // peers' deregistered buffers, released on this thread (ipc.cc)
   ret = argsCheck(info);
   if (ret == ncclSuccess && info->comm->asyncResult.load() != ncclSuccess) {
     WARN("%s: communicator is in error state %d", info->opName, info->comm->asyncResult.load());

@@ -302,6 +302,7 @@ static ncclResult_t initRankCommon(ncclComm_t* newcomm, int nranks, ncclUniqueId
     return ncclInvalidArgument;
   }
   NCCLCHECK(checkConfig(config));
+  ipcDrainReleases(nullptr);
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
   ncclConfig_t cfgCopy;
@@ -353,6 +354,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommInitRankScalable, ncclComm_t*, int, int, int, n
 NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
   logInit();
   ROCTX_RANGE("ncclCommInitAll ndev=%d", ndev);
+  ipcDrainReleases(nullptr);
   if (comms == nullptr) {
     WARN("CommInitAll : comms argument is NULL");
     return ncclInvalidArgument;
@@ -458,6 +460,7 @@ static ncclResult_t commFree(ncclComm* comm) {
 NCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;  // reference: destroying NULL is a no-op
   NCCLCHECK(commCheck(comm, "ncclCommDestroy", "comm"));
+  ipcDrainReleases(nullptr);
   int old = 0;
   (void)hipGetDevice(&old);
   if (comm->initThread.joinable()) comm->initThread.join();

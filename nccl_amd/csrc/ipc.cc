@@ -29,7 +29,6 @@
 
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
 #include <map>
 #include <mutex>
 #include <thread>
@@ -50,38 +49,60 @@ struct FdServer {
   // proxy thread maps a registered buffer for ncclIpcLocalRegisterBuffer, src/transport/p2p.cc ipcRegister):
   // (registering rank, its registration tag) -> mapping. Touched only by the server thread.
   std::map<std::pair<int, uint64_t>, IpcImport> imports;
-  // Unmapping a peer's buffer (hipFree of the mapping) waits for this device's outstanding work, which may
-  // be a collective kernel waiting for the very rank whose RELEASE request is being served: the server thread
-  // therefore only answers and hands the mapping to this reaper thread, which may block as long as it needs
-  // (found by the multi-process fuzz: a deregistration on one rank stalled its peers' next collective until
-  // the spin timeout).
-  std::thread reaper;
-  std::mutex reapMu;
-  std::condition_variable reapCv;
-  std::vector<IpcImport> reapQueue;
-  bool reapStop = false;
 };
 
-static void reapLater(FdServer* s, const IpcImport& m) {
-  std::lock_guard<std::mutex> g(s->reapMu);
-  s->reapQueue.push_back(m);
-  s->reapCv.notify_one();
+// Releasing a mapping frees its address range and tears the interop mapping down in two runtime calls (hipFree,
+// hipDestroyExternalMemory). Round 3 released peers' registered buffers on a helper thread, concurrently with
+// whatever the caller's thread did next; bench.py's N = 4 rehearsal (a deregistration, then a new communicator
+// whose slab is allocated, exported and imported right away) then failed three runs out of three at that new
+// communicator — a refused dma-buf export, a spin timeout, an illegal access in its first collective — which is
+// what a fresh allocation landing in a range still being torn down would do. So mappings are released only on a
+// thread that is inside the library — the caller's, between its own runtime calls — and every release and
+// import of this library is serialized by gMapMu. Peers' registered buffers whose owner deregistered
+// them (RELEASE requests, served without blocking: the server never waits for the device) wait in gPending until
+// the next library call on any thread drains them (ipcDrainReleases), or until their communicator's server stops.
+static std::mutex gMapMu;
+std::mutex& ipcMapMutex() { return gMapMu; }
+struct PendingRelease {
+  IpcImport map;
+  int device;
+};
+static std::mutex gPendMu;
+static std::vector<PendingRelease> gPending;
+static std::atomic<bool> gHavePending{false};
+
+static void releaseLater(int device, const IpcImport& m) {
+  std::lock_guard<std::mutex> g(gPendMu);
+  gPending.push_back({m, device});
+  gHavePending.store(true, std::memory_order_release);
 }
 
-static void reaperLoop(FdServer* s) {
-  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;  // see serverLoop
-  (void)hipThreadExchangeStreamCaptureMode(&mode);
-  std::unique_lock<std::mutex> lk(s->reapMu);
-  while (true) {
-    s->reapCv.wait(lk, [s] { return s->reapStop || !s->reapQueue.empty(); });
-    if (s->reapQueue.empty()) break;  // stopping and drained
-    std::vector<IpcImport> batch;
-    batch.swap(s->reapQueue);
-    lk.unlock();
-    (void)hipSetDevice(s->device);
-    for (IpcImport& m : batch) ipcRelease(&m);
-    lk.lock();
+void ipcDrainReleases(hipStream_t stream) {
+  if (!gHavePending.load(std::memory_order_acquire)) return;
+  if (stream) {  // never inside a capture (hipFree synchronizes): a later call drains them
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    const hipError_t e = hipStreamIsCapturing(stream, &st);
+    (void)hipGetLastError();
+    if (e != hipSuccess || st != hipStreamCaptureStatusNone) return;
   }
+  std::vector<PendingRelease> batch;
+  {
+    std::lock_guard<std::mutex> g(gPendMu);
+    batch.swap(gPending);
+    gHavePending.store(false, std::memory_order_release);
+  }
+  if (batch.empty()) return;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;  // another thread may be capturing in global mode
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  for (PendingRelease& r : batch) {
+    (void)hipSetDevice(r.device);
+    ipcRelease(&r.map);
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  (void)hipSetDevice(dev);
+  TRACE("ipc: released %zu peer mapping(s) of deregistered buffers", batch.size());
 }
 
 // Requests on the fd server's socket (one per connection). FETCH: hand over the fd published under `key`.
@@ -198,7 +219,7 @@ static void serveOne(FdServer* s, int c) {
       inFd = -1;  // owned by the mapping now
       auto key = std::make_pair((int)q.from, q.key);
       auto old = s->imports.find(key);
-      if (old != s->imports.end()) reapLater(s, old->second);  // a re-registration replaces its mapping
+      if (old != s->imports.end()) releaseLater(s->device, old->second);  // a re-registration replaces its mapping
       s->imports[key] = m;
       reply.status = 0;
       reply.value = (uint64_t)m.ptr;
@@ -208,7 +229,7 @@ static void serveOne(FdServer* s, int c) {
   } else if (q.op == IPC_RELEASE) {
     auto it = s->imports.find(std::make_pair((int)q.from, q.key));
     if (it != s->imports.end()) {
-      reapLater(s, it->second);  // never block the server on the device (FdServer::reaper)
+      releaseLater(s->device, it->second);  // never block the server on the device (gPending above)
       s->imports.erase(it);
     }
     reply.status = 0;
@@ -255,7 +276,6 @@ ncclResult_t ipcServerStart(ncclComm* comm) {
     return ncclSystemError;
   }
   s->thread = std::thread(serverLoop, s);
-  s->reaper = std::thread(reaperLoop, s);
   comm->fdServer = s;
   TRACE("rank %d: fd server %s", comm->rank, s->name);
   return ncclSuccess;
@@ -266,12 +286,7 @@ void ipcServerStop(ncclComm* comm) {
   if (!s) return;
   if (s->wakePipe[1] >= 0) (void)!write(s->wakePipe[1], "x", 1);
   if (s->thread.joinable()) s->thread.join();
-  {
-    std::lock_guard<std::mutex> g(s->reapMu);
-    s->reapStop = true;
-    s->reapCv.notify_one();
-  }
-  if (s->reaper.joinable()) s->reaper.join();  // drains what RELEASE requests queued
+  ipcDrainReleases(nullptr);  // what RELEASE requests queued (for any communicator of this process)
   for (auto& kv : s->table) close(kv.second);
   if (!s->imports.empty()) (void)hipSetDevice(comm->device);
   for (auto& kv : s->imports) ipcRelease(&kv.second);  // peers' registrations still mapped here
@@ -473,6 +488,7 @@ static bool closeIfMine(int fd, uint64_t dev, uint64_t ino) {
 }
 
 static ncclResult_t importLegacy(const IpcDesc& d, IpcImport* out) {
+  std::lock_guard<std::mutex> g(gMapMu);
   HIPCHECK(hipIpcOpenMemHandle(&out->ptr, d.handle, hipIpcMemLazyEnablePeerAccess));
   out->legacy = 1;
   return ncclSuccess;
@@ -480,6 +496,7 @@ static ncclResult_t importLegacy(const IpcDesc& d, IpcImport* out) {
 
 // Map a dma-buf fd (owned from here on: kept by the mapping, or closed on failure).
 static ncclResult_t importFd(int fd, uint64_t size, IpcImport* out) {
+  std::lock_guard<std::mutex> g(gMapMu);
   memset(out, 0, sizeof(*out));
   out->fd = -1;
   hipExternalMemoryHandleDesc hd;
@@ -548,6 +565,7 @@ ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
 
 void ipcRelease(IpcImport* m) {
   if (!m->ptr) return;
+  std::lock_guard<std::mutex> g(gMapMu);
   if (m->legacy) {
     (void)hipIpcCloseMemHandle(m->ptr);
   } else {

@@ -346,6 +346,7 @@ using namespace ncclamd;
 
 NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle) {
   NCCLCHECK(commCheck(comm, "ncclCommRegister", "comm"));
+  ipcDrainReleases(nullptr);
   if (handle == nullptr) {
     WARN("ncclCommRegister : handle argument is NULL");
     return ncclInvalidArgument;
@@ -378,6 +379,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommRegister, const ncclComm_t, void*, size_t, void
 
 NCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle) {
   NCCLCHECK(commCheck(comm, "ncclCommDeregister", "comm"));
+  ipcDrainReleases(nullptr);
   if (handle == nullptr) return ncclSuccess;  // reference commDeregister: NULL reg is a no-op
   auto it = std::find(comm->regHandles.begin(), comm->regHandles.end(), (RegHandle*)handle);
   if (it == comm->regHandles.end()) {
@@ -401,6 +403,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommDeregister, const ncclComm_t, void*)
 NCCL_EXPORT ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, size_t size, ncclWindow_t* win,
                                                 int winFlags) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowRegister", "comm"));
+  ipcDrainReleases(nullptr);
   if (win == nullptr) {
     WARN("ncclCommWindowRegister : win argument is NULL");
     return ncclInvalidArgument;
@@ -420,6 +423,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommWindowRegister, ncclComm_t, void*, size_t, nccl
 
 NCCL_EXPORT ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowDeregister", "comm"));
+  ipcDrainReleases(nullptr);
   if (win == nullptr) return ncclSuccess;
   auto it = std::find(comm->windows.begin(), comm->windows.end(), win);
   if (it == comm->windows.end() || win->comm != comm) {

@@ -49,6 +49,7 @@ ncclResult_t transportSetup(ncclComm* comm) {
   HIPCHECK(hipSetDevice(comm->device));
   if (comm->nRanks == 1) return ncclSuccess;  // nranks==1 never touches peers (onerank.cu:49-110)
   size_t sb = stagingBytes(comm), fb = flagsBytes(comm);
+  std::lock_guard<std::mutex> mapLock(ipcMapMutex());
   if (paramInt("NCCL_AMD_STAGING_PLAIN", 0))  // diagnostics only (scripts/ipc_hang_diag.py): cached staging
     HIPCHECK(hipMalloc(&comm->staging, sb));
   else
