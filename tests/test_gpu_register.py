@@ -250,9 +250,9 @@ def test_registered_allreduce_fp32_256MiB_n2(built):
 def _dereg_worker(rank, nranks, uid, q):
     """Rank 0 deregisters at once and starts its next (staged) collective; the others deregister later, while
     rank 0's kernel already waits for them. Their release requests reach rank 0's fd server, which must answer
-    without waiting for rank 0's device (the unmapping runs on its reaper thread): before that fix the server's
-    hipFree waited for rank 0's kernel, which waited for the ranks blocked on the server — a stall until the
-    spin timeout (found by scripts/fuzz_mp.py)."""
+    without waiting for rank 0's device (the unmapping waits for rank 0's next library call, ipc.cc
+    ipcDrainReleases): a server that unmapped itself waited in hipFree for rank 0's kernel, which waited for the
+    ranks blocked on the server — a stall until the spin timeout (found by scripts/fuzz_mp.py)."""
     try:
         os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "15000"
         import torch
@@ -287,3 +287,76 @@ def test_deregister_while_peers_run(built):
     bad = [e for r in sorted(res) for e in res[r][0]]
     assert not bad, "\n".join(bad[:10])
     assert all(t < 12 for _, t in res.values()), res  # three 1 s delays, no spin timeout
+
+
+def _dereg_then_new_comm_worker(rank, nranks, uid, q, uid2):
+    """bench.py's suite order of round 3 on its own: a symmetric window, then 256 MiB buffers registered with
+    ncclCommRegister, deregistered, and at once a NEW communicator allocating, exporting and importing its slab
+    and running its first AllReduce. With the peers' mappings torn down on a helper thread meanwhile this failed
+    three runs out of three on the one-GPU box (refused dma-buf export, spin timeout, illegal access); mappings are
+    now released on the caller's thread at its next library call (ipc.cc ipcDrainReleases)."""
+    try:
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "20000"
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.current_stream()
+        errs = []
+        S = 256 << 20
+        c = S // 4
+        g = torch.Generator(device="cuda")
+        want = lambda b: b * (nranks * (nranks + 1) / 2)
+        # a symmetric window over a 512 MiB torch allocation (its cached block is what torch hands out next)
+        win_t = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
+        win = comm.register_window(win_t.data_ptr(), 2 * S)
+        g.manual_seed(4321)
+        base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
+        sendw, recvw = win_t[:S].view(torch.float32), win_t[S:].view(torch.float32)
+        sendw.copy_(base * (rank + 1))
+        for _ in range(3):
+            comm.all_reduce_raw(sendw.data_ptr(), recvw.data_ptr(), c, 7, 0, s.cuda_stream)
+        torch.cuda.synchronize()
+        if not torch.equal(recvw, want(base)):
+            errs.append(f"rank {rank}: window AllReduce wrong")
+        comm.deregister_window(win)
+        del win_t, sendw, recvw, base
+        # registered buffers, deregistered
+        g.manual_seed(4322)
+        base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
+        sendr = base * (rank + 1)
+        recvr = torch.empty_like(sendr)
+        hs = [comm.register_buffer(sendr.data_ptr(), S), comm.register_buffer(recvr.data_ptr(), S)]
+        for _ in range(5):
+            comm.all_reduce_raw(sendr.data_ptr(), recvr.data_ptr(), c, 7, 0, s.cuda_stream)
+        torch.cuda.synchronize()
+        if not torch.equal(recvr, want(base)):
+            errs.append(f"rank {rank}: registered AllReduce wrong")
+        for h in hs:
+            comm.deregister_buffer(h)
+        del sendr, recvr, base
+        # at once: a new communicator and its first collectives
+        g.manual_seed(4323)
+        base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
+        xs = base * (rank + 1)
+        ys = torch.empty_like(xs)
+        cm = nccl_amd.Communicator.init(nranks, rank, uid2)
+        for _ in range(3):
+            cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, s.cuda_stream)
+        torch.cuda.synchronize()
+        if cm.async_error() or comm.async_error():
+            errs.append(f"rank {rank}: async {comm.async_error()} / {cm.async_error()}")
+        elif not torch.equal(ys, want(base)):
+            errs.append(f"rank {rank}: the new communicator's AllReduce is wrong")
+        cm.destroy()
+        comm.destroy()
+        q.put((rank, errs))
+    except Exception as e:
+        q.put((rank, [f"rank {rank} exception: {e!r}"]))
+
+
+def test_deregistration_then_new_communicator(built):
+    import nccl_amd
+    res = _spawn(_dereg_then_new_comm_worker, 4, args=(nccl_amd.get_unique_id(),), limit_s=300)
+    bad = [e for r in sorted(res) for e in res[r]]
+    assert not bad, "\n".join(bad[:10])
