@@ -228,6 +228,7 @@ struct CommTuning {
   int copyVariant;          // NCCL_AMD_COPY_VARIANT (nRanks == 1 copy kernel, diagnostics)
   int64_t copyGrid;         // NCCL_AMD_COPY_GRID (cap on its workgroups; default: one per 16 KiB tile)
   int64_t ringChunkBytes;   // NCCL_ALGO=RING AllReduce chunk: NCCL_BUFFSIZE / NCCL_STEPS * ALLREDUCE_CHUNKSTEPS
+  int refOrder;             // NCCL_AMD_REF_ORDER: AllReduce on the direct kernel in the reference's ring partition
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
 void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known

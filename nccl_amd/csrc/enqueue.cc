@@ -146,6 +146,9 @@ void loadTuning(CommTuning* t) {
   t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);
   // the reference's RING/SIMPLE chunk: stepSize (NCCL_BUFFSIZE / NCCL_STEPS) x ALLREDUCE_CHUNKSTEPS (NCCL_STEPS / 2),
   // in 512-byte grains (enqueue.cc:2222-2225, 2321; collectives.h:19-20; default NCCL_BUFFSIZE 4 MiB, init.cc:813)
+  // NCCL_AMD_REF_ORDER=1: every AllReduce folds in the reference's RING/SIMPLE order at any size, on the fast
+  // direct kernel (planColl below)
+  t->refOrder = (int)paramInt("NCCL_AMD_REF_ORDER", 0);
   const int64_t buff = paramInt("NCCL_BUFFSIZE", 4 << 20);
   t->ringChunkBytes = buff / 8 * 4 / 512 * 512;
   if (t->ringChunkBytes < 512) t->ringChunkBytes = 512;
@@ -460,6 +463,10 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
                                              : ((size_t)2 << 20) / n;
     oneShot = comm->tune.algo == FORCE_ONESHOT || (comm->tune.algo == FORCE_NONE && bytes <= lim);
   }
+  // NCCL_AMD_REF_ORDER: AllReduce always on the direct kernel in the reference's partition (below)
+  const bool refOrder = comm->tune.refOrder && info.func == FUNC_ALLREDUCE && comm->tune.algo != FORCE_RING &&
+                        comm->tune.algo != FORCE_TREE;
+  if (refOrder) oneShot = false;
   int tunedNch = 0;
   if (comm->tunerLoaded) {  // external tuner plugin: one-shot (TREE/SIMPLE) vs direct (RING/SIMPLE), channels
     int tuned = TUNE_DEFAULT;
@@ -471,7 +478,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   const bool oneShotAR = oneShot;
   // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce / ReduceScatter / AllGather /
   // Reduce, one launch, no fences
-  if (llPlan(info, &p.ll.ops[0])) {
+  if (!refOrder && llPlan(info, &p.ll.ops[0])) {
     p.algo = ALGO_LL;
     p.ll.comm = comm->devComm;
     p.ll.redArg = p.args.redArg;
@@ -526,6 +533,24 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
             p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps);
       return ncclSuccess;
     }
+  }
+  if (refOrder) {
+    // The reference's RING/SIMPLE partition (ringParts: channel parts, NCCL_BUFFSIZE chunks, loops) walked by the
+    // direct scatter-reduce-gather kernel: in each loop chunk q is finalised by rank q, as in the reference's ring,
+    // so every element folds in its order — at the direct kernel's n-1 links instead of the ring's one (kernels.h
+    // Channel::refPart). All channels of the communicator's cap, no CU budget: the partition is the reference's.
+    const RingParts r = ringParts(count, ts, comm->chanCap);
+    p.nChannels = r.nch;
+    p.args.cbdLo = r.lo;
+    p.args.part = r.mid;
+    p.args.cbdHi = r.hi;
+    p.args.chunk = (uint64_t)comm->tune.ringChunkBytes / ts;
+    p.args.slice = std::min<uint64_t>(p.args.chunk, comm->slotBytes / ts / epp * epp);
+    p.args.nSteps = 0;  // per channel (kernels.h Channel::refSteps)
+    TRACE("%s: direct in the reference's partition, nch %d parts %lu/%lu/%lu chunk %lu slice %lu", info.opName,
+          p.nChannels, (unsigned long)r.lo, (unsigned long)r.mid, (unsigned long)r.hi, (unsigned long)p.args.chunk,
+          (unsigned long)p.args.slice);
+    return ncclSuccess;
   }
   // Zero-copy kernels (kernels.h symKernel): buffers in NCCL_WIN_COLL_SYMMETRIC windows (reference: symmetric
   // kernels, src/enqueue.cc ncclSymkAvailable / src/device/symmetric/*), or registered with ncclCommRegister /
@@ -677,6 +702,7 @@ bool batchable(const std::vector<PlannedColl>& run, const PlannedColl& b) {
       if (x.info.func != FUNC_ALLGATHER && !sameRedOp(x.p, b.p)) return false;
     return true;
   }
+  if (a.p.args.cbdLo || b.p.args.cbdLo) return false;  // the reference's partition (NCCL_AMD_REF_ORDER): alone
   if (a.p.algo == ALGO_DIRECT || a.p.algo == ALGO_ONESHOT)
     return run.size() < (size_t)kMaxCollBatch && a.info.func == b.info.func && sameRedOp(a.p, b.p) &&
            a.p.args.protoFlags == b.p.args.protoFlags;

@@ -417,7 +417,7 @@ __device__ __forceinline__ void foldFp8Packs(const Red<T, OP>& fn, int n, const 
 // per batch and walks the sources with the next source's loads in flight while it reduces the
 // current one (U*16 B x 2 per lane outstanding), so memory parallelism does not depend on n and the
 // per-source loop needs no predication.
-template <typename T, int OP>
+template <typename T, int OP, int UMAX = 64>
 __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const char* const* src, uint64_t nelem,
                                           char* dstLocal, char* const* dstPush, int nPush, bool aligned) {
   constexpr int EPP = 16 / sizeof(T);
@@ -429,7 +429,8 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
   constexpr bool kSwarDiv = std::is_same<T, uint8_t>::value && OP == DEV_SUMPOSTDIV;
   constexpr bool kSwar = std::is_same<T, uint8_t>::value && (Swar8<OP>::ok || kSwarDiv);
   constexpr int kSwarOp = kSwarDiv ? DEV_SUM : OP;
-  constexpr int U = sizeof(T) > 1 ? kFoldUnroll : kSwar ? kFoldUnrollSwar : kFoldUnroll1B;
+  constexpr int U0 = sizeof(T) > 1 ? kFoldUnroll : kSwar ? kFoldUnrollSwar : kFoldUnroll1B;
+  constexpr int U = U0 < UMAX ? U0 : UMAX;
   uint32_t swarMask = 0, divMagic = 0;
   if constexpr (kSwar && !kSwarDiv) swarMask = (uint32_t)(uint8_t)fn.arg * 0x01010101u;
   if constexpr (kSwarDiv) divMagic = swarDivMagic(fn.divisor);
@@ -520,7 +521,9 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
 // COLL_AR1 = one-shot AllReduce for small buffers: every rank publishes its whole channel portion to
 // every peer and folds all n contributions itself (one handshake instead of three; (n-1)*S link bytes
 // instead of 2(n-1)/n*S). Same fold order as the two-shot path, so results are identical.
-enum Coll { COLL_AR = 0, COLL_RS = 1, COLL_AG = 2, COLL_REDUCE = 3, COLL_AR1 = 4 };
+// COLL_ARREF = the direct AllReduce on the reference's ring partition (NCCL_AMD_REF_ORDER, Channel::refPart): its
+// own instantiation, so the default AllReduce kernel carries none of its indexing.
+enum Coll { COLL_AR = 0, COLL_RS = 1, COLL_AG = 2, COLL_REDUCE = 3, COLL_AR1 = 4, COLL_ARREF = 5 };
 
 // Element range [lo,hi) of a block handled by channel c at pipeline step s (offsets inside the block).
 __device__ __forceinline__ void sliceRange(const CollArgs& a, int c, int s, uint64_t blockLen, uint64_t& lo,
@@ -530,9 +533,16 @@ __device__ __forceinline__ void sliceRange(const CollArgs& a, int c, int s, uint
   hi = min(lo + a.slice, pEnd);
 }
 
+// COLL_ARREF channel geometry (Channel::refInit): region offset, loop length, full loops, the last loop's length
+// and chunk, steps per full loop, steps in all.
+struct RefGeom {
+  uint64_t off, loop, rem, ckLast;
+  uint32_t full, perFull, steps;
+};
 // Per-workgroup (channel) LDS scratch for the handshake arrays.
 struct Shared {
   ChanState st;
+  RefGeom ref;
   const char* srcPtr[NCCL_AMD_MAX_RANKS];   // phase-B fold sources, in fold order
   char* pushPtr[NCCL_AMD_MAX_RANKS];        // phase-B remote destinations
   int nPush;
@@ -564,22 +574,71 @@ struct Channel {
   // whose staging, flags and credits carry it. They differ only inside a group batch (collBatchKernel).
   int cl;
   static constexpr uint64_t ts = sizeof(T);
+  static constexpr bool kAR = COLL == COLL_AR || COLL == COLL_ARREF;
 
   __device__ uint64_t blockLen(int q) const {
-    if (COLL == COLL_AR || COLL == COLL_REDUCE) {
+    if (kAR || COLL == COLL_REDUCE) {
       uint64_t b = (uint64_t)q * a.chunk;
       return b >= a.count ? 0 : min(a.chunk, a.count - b);
     }
     return a.chunk;
   }
   __device__ uint64_t& ctr(int k, int r) const { return sh.st.ctr[k][r]; }
+  // NCCL_AMD_REF_ORDER (COLL_ARREF): the reference's ring partition instead of rank blocks cut into
+  // channel parts. This channel walks its part (ncclCollCbdPart, device.h:337-361: cbdLo / part / cbdHi) in loops
+  // of n chunks of a.chunk elements, the last loop's chunk re-cut to alignUp(divUp(rem, n), 16 / sizeof(T))
+  // (all_reduce.h:34-38); chunk q of a loop is "block" q, owned and finalised by rank q, so every element folds
+  // q+1, ..., q as in the reference's ring. Step s = slice j of loop l (a.slice elements per chunk and step).
+  static constexpr bool refPart() { return COLL == COLL_ARREF; }
+  // this channel's region and loop geometry, computed once per launch (refInit) into LDS (Shared::ref): the 64-bit
+  // divisions stay out of the per-step code and the values out of the registers the fold needs
+  __device__ void refInit() {
+    constexpr uint64_t EPP = 16 / sizeof(T);
+    if (threadIdx.x == 0) {
+      const int nch = (int)gridDim.x;  // never batched: the grid is the op's channels
+      uint64_t off, cnt;
+      if (cl == 0) off = 0, cnt = a.cbdLo;
+      else if (cl == nch - 1) off = a.cbdLo + (uint64_t)(nch - 2) * a.part, cnt = a.cbdHi;
+      else off = a.cbdLo + (uint64_t)(cl - 1) * a.part, cnt = a.part;
+      RefGeom& g = sh.ref;
+      g.off = off;
+      g.loop = (uint64_t)n * a.chunk;
+      g.full = (uint32_t)(cnt / g.loop);
+      g.rem = cnt - (uint64_t)g.full * g.loop;
+      g.ckLast = g.rem ? ((g.rem + n - 1) / n + EPP - 1) / EPP * EPP : 0;
+      g.perFull = (uint32_t)((a.chunk + a.slice - 1) / a.slice);
+      g.steps = g.full * g.perFull + (uint32_t)((g.ckLast + a.slice - 1) / a.slice);
+    }
+    __syncthreads();
+  }
+  // Block b's slice at pipeline step `step`: elements [off, off + len) of the buffer.
+  __device__ void blockSlice(int step, int b, uint64_t& off, uint64_t& len) const {
+    uint64_t lo, hi;
+    if (!refPart()) {
+      sliceRange(a, cl, step, blockLen(b), lo, hi);
+      off = (uint64_t)b * a.chunk + lo;
+      len = hi - lo;
+      return;
+    }
+    const RefGeom& g = sh.ref;
+    const uint32_t st = (uint32_t)step, inFull = g.full * g.perFull;
+    uint32_t l, j;
+    uint64_t ck, rem;
+    if (st < inFull) l = st / g.perFull, j = st - l * g.perFull, ck = a.chunk, rem = g.loop;
+    else l = g.full, j = st - inFull, ck = g.ckLast, rem = g.rem;
+    const uint64_t bb = (uint64_t)b * ck, blen = bb >= rem ? 0 : min(ck, rem - bb);
+    lo = min((uint64_t)j * a.slice, blen);
+    hi = min(lo + a.slice, blen);
+    off = g.off + (uint64_t)l * g.loop + bb + lo;
+    len = hi - lo;
+  }
   // k-th peer (k = 1..n-1) this channel sends to. Staggered by channel: every channel starting with the
   // same peer would put all of a rank's scatter traffic on ONE xGMI link at a time; rotating the start
   // spreads the channels evenly over the n-1 links (data placement and fold order are unaffected).
   __device__ int peerAt(int k) const { return (me + 1 + (k - 1 + c) % (n - 1)) % n; }
   __device__ const uint64_t* myFlags(int kind) const { return dc.flags[me] + flagIndex(c, kind, 0); }
   __device__ bool pushesTo(int p) const {
-    if (COLL == COLL_AR || COLL == COLL_AG) return true;
+    if (kAR || COLL == COLL_AG) return true;
     return COLL == COLL_REDUCE && !isRoot && p == a.root;
   }
   // Reduce over n >= 3 ranks: the root owns no block — the buffer is cut into n-1 blocks owned by the other
@@ -603,13 +662,13 @@ struct Channel {
       int p = peerAt(k);
       if (!owns(p)) continue;
       const int b = blockOf(p);
-      uint64_t lo, hi;
-      sliceRange(a, cl, step, blockLen(b), lo, hi);
+      uint64_t off, len;
+      blockSlice(step, b, off, len);
       int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
       char* dst = rsPull ? dc.staging[me] + stagingOffset(dc, c, STG_RS, slot, p)   // my slab, area for p
                          : dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me);
-      const char* src = (const char*)a.sendbuff + ((uint64_t)b * a.chunk + lo) * ts;
-      copyRange<T, true>(dst, src, (hi - lo) * ts, aligned);
+      const char* src = (const char*)a.sendbuff + off * ts;
+      copyRange<T, true>(dst, src, len * ts, aligned);
     }
     if (tid < NCCL_AMD_MAX_RANKS) {
       bool act = tid < n && tid != me && owns(tid);
@@ -627,7 +686,7 @@ struct Channel {
   __device__ bool phaseB(int step) {
     if (rootless() && isRoot) return true;  // the root owns no block
     int tid = threadIdx.x;
-    const bool push = (COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && !isRoot));
+    const bool push = (kAR || COLL == COLL_AG || (COLL == COLL_REDUCE && !isRoot));
     if (COLL != COLL_AG) {
       if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
       __syncthreads();
@@ -646,7 +705,8 @@ struct Channel {
     const int myB = blockOf(me);
     uint64_t lo, hi;
     sliceRange(a, cl, step, blockLen(myB), lo, hi);
-    const uint64_t nelem = hi - lo;
+    uint64_t myOff = (uint64_t)myB * a.chunk + lo, nelem = hi - lo;  // my block's slice in the buffer
+    if (refPart()) blockSlice(step, myB, myOff, nelem);
     if (tid == 0) {
       int np = 0;
       if (agPull) {  // one copy in my own AG staging, at this channel's publication sequence
@@ -664,7 +724,7 @@ struct Channel {
       for (int k = 0; k < n; k++) {
         int q = (first + k) % n;
         const int rslot = (int)(ctr(CTR_RECV_RS, q) % nSlots);
-        sh.srcPtr[k] = q == me ? (const char*)a.sendbuff + ((uint64_t)myB * a.chunk + lo) * ts
+        sh.srcPtr[k] = q == me ? (const char*)a.sendbuff + myOff * ts
                      : rsPull  ? dc.staging[q] + stagingOffset(dc, c, STG_RS, rslot, me)  // q's slab, remote
                                : dc.staging[me] + stagingOffset(dc, c, STG_RS, rslot, q);
       }
@@ -678,8 +738,11 @@ struct Channel {
     } else {
       char* dstLocal = nullptr;
       if (COLL == COLL_RS) dstLocal = (char*)a.recvbuff + lo * ts;
-      else if (COLL == COLL_AR || isRoot) dstLocal = (char*)a.recvbuff + ((uint64_t)myB * a.chunk + lo) * ts;
-      foldRange<T, OP>(fn, n, sh.srcPtr, nelem, dstLocal, sh.pushPtr, sh.nPush, aligned);
+      else if (kAR || isRoot) dstLocal = (char*)a.recvbuff + myOff * ts;
+      // (the reference-order kernel's extra indexing leaves the widest folds — 1-byte unpacked, 8-byte — fewer
+      // packs in flight within the 128-VGPR co-residency budget)
+      constexpr int kUMax = COLL != COLL_ARREF ? 64 : sizeof(T) == 1 ? 1 : sizeof(T) == 8 ? 2 : 64;
+      foldRange<T, OP, kUMax>(fn, n, sh.srcPtr, nelem, dstLocal, sh.pushPtr, sh.nPush, aligned);
     }
     // one release covers both: AG data ready at each destination; RS slots consumed (ack to senders)
     if (tid < NCCL_AMD_MAX_RANKS) {
@@ -780,13 +843,13 @@ struct Channel {
     for (int k = 1; k < n; k++) {
       int q = (me + n - k) % n;
       const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
-      uint64_t lo, hi;
-      sliceRange(a, cl, step, blockLen(b), lo, hi);
+      uint64_t off, len;
+      blockSlice(step, b, off, len);
       const int slot = (int)(ctr(recvKind, q) % nSlots);
       const char* src = agPull ? dc.staging[q] + stagingOffset(dc, c, STG_AG, slot, q)  // q's own copy, remote
                                : dc.staging[me] + stagingOffset(dc, c, STG_AG, slot, q);
-      char* dst = (char*)a.recvbuff + ((uint64_t)b * a.chunk + lo) * ts;
-      copyRange<T, false>(dst, src, (hi - lo) * ts, aligned);
+      char* dst = (char*)a.recvbuff + off * ts;
+      copyRange<T, false>(dst, src, len * ts, aligned);
     }
     if (tid < NCCL_AMD_MAX_RANKS) {
       bool peer = tid < n && tid != me;
@@ -840,23 +903,25 @@ __device__ __forceinline__ bool runChannel(const CollArgs& a, const DevComm& dc,
   Channel<T, OP, COLL> ch{a, dc, sh, fn, c, dc.rank, dc.nRanks, dc.nSlots, a.aligned != 0,
                           (COLL != COLL_REDUCE) || dc.rank == a.root, (a.protoFlags & 1) != 0,
                           (a.protoFlags & 2) != 0, (a.protoFlags & 8) != 0, (a.protoFlags & 64) != 0,
-                          (COLL == COLL_AR || COLL == COLL_AG) && (a.protoFlags & 16) != 0,
-                          (COLL == COLL_AR || COLL == COLL_RS) && (a.protoFlags & 32) != 0, cl};
+                          (COLL == COLL_AR || COLL == COLL_ARREF || COLL == COLL_AG) && (a.protoFlags & 16) != 0,
+                          (COLL == COLL_AR || COLL == COLL_ARREF || COLL == COLL_RS) && (a.protoFlags & 32) != 0, cl};
   if (COLL == COLL_AR1) {
     bool ok = true;
     for (int s = 0; ok && s < a.nSteps; s++) ok = ch.oneShotA(s) && ch.oneShotB(s);
     return ok;
   }
   constexpr bool hasA = COLL != COLL_AG;
-  const bool hasC = COLL == COLL_AR || COLL == COLL_AG || (COLL == COLL_REDUCE && ch.isRoot);
+  const bool hasC = COLL == COLL_AR || COLL == COLL_ARREF || COLL == COLL_AG || (COLL == COLL_REDUCE && ch.isRoot);
   // Pipeline: A(0); for s: B(s); A(s+1); C(s). Hoisting A(s+1) above C(s) lets the owners start
   // reducing step s+1 while this rank still drains step s (they are independent).
-  bool ok = !hasA || a.nSteps == 0 || ch.phaseA(0);
+  if constexpr (Channel<T, OP, COLL>::refPart()) ch.refInit();
+  const int nSteps = ch.refPart() ? (int)sh.ref.steps : a.nSteps;
+  bool ok = !hasA || nSteps == 0 || ch.phaseA(0);
   const bool cFirst = (a.protoFlags & 4) != 0;
-  for (int s = 0; ok && s < a.nSteps; s++) {
+  for (int s = 0; ok && s < nSteps; s++) {
     ok = ch.phaseB(s);
     if (ok && hasC && cFirst) ok = ch.phaseC(s);
-    if (ok && hasA && s + 1 < a.nSteps) ok = ch.phaseA(s + 1);
+    if (ok && hasA && s + 1 < nSteps) ok = ch.phaseA(s + 1);
     if (ok && hasC && !cFirst) ok = ch.phaseC(s);
   }
   return ok;
@@ -1580,10 +1645,13 @@ inline void launchLL(const LaunchPlan& p) {
 // the staged kernel: one op, or a group batch (collBatchKernel)
 template <typename T, int OP, int COLL>
 inline void launchColl(const LaunchPlan& p) {
-  if (p.batch.nOps > 1)
-    NCCL_AMD_LAUNCH((collBatchKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.batch);
-  else
-    NCCL_AMD_LAUNCH((collKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
+  if constexpr (COLL != COLL_ARREF) {  // reference-order AllReduces are never batched (enqueue.cc batchable)
+    if (p.batch.nOps > 1) {
+      NCCL_AMD_LAUNCH((collBatchKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.batch);
+      return;
+    }
+  }
+  NCCL_AMD_LAUNCH((collKernel<T, OP, COLL>), dim3(p.nChannels), dim3(kThreads), 0, p.stream, p.args);
 }
 
 template <typename T, int OP>
@@ -1615,6 +1683,7 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
     case FUNC_ALLREDUCE:
       if (p.algo == ALGO_LL) launchLL<T, OP>(p);
       else if (p.algo == ALGO_ONESHOT) launchColl<T, OP, COLL_AR1>(p);
+      else if (p.args.cbdLo) launchColl<T, OP, COLL_ARREF>(p);  // NCCL_AMD_REF_ORDER (planColl)
       else launchColl<T, OP, COLL_AR>(p);
       break;
     case FUNC_REDUCESCATTER:

@@ -77,6 +77,14 @@ def ring_runs(n: int) -> bool:
     return _env_int("NCCL_AMD_NSLOTS", 2) >= 2
 
 
+def ref_order_runs(n: int) -> bool:
+    """Whether NCCL_AMD_REF_ORDER=1 (from the communicator's environment) puts AllReduce on the reference's ring
+    partition (the direct kernel in that order; enqueue.cc planColl): any size and protocol, unless
+    NCCL_ALGO=TREE / RING takes the reference's own chain / ring instead."""
+    return n >= 2 and _env_int("NCCL_AMD_REF_ORDER", 0) != 0 and \
+        os.environ.get("NCCL_ALGO", "").upper() not in ("TREE", "RING")
+
+
 def expected(coll: str, inputs, dtype: int, op: int, root: int = 0, algo: str = ""):
     if coll == "allreduce":
         # NCCL_ALGO=TREE folds every element in the chain's order; NCCL_ALGO=RING in the reference's ring order
@@ -86,7 +94,7 @@ def expected(coll: str, inputs, dtype: int, op: int, root: int = 0, algo: str = 
         algo = algo or os.environ.get("NCCL_ALGO", "").upper()
         if algo == "TREE":
             out = oracle.all_reduce_chain(inputs, dtype, op)
-        elif algo == "RING" and ring_runs(n):
+        elif (algo == "RING" and ring_runs(n)) or ref_order_runs(n):
             out = oracle.all_reduce_ring_nccl(inputs, dtype, op, ring_channels(n), _env_int("NCCL_BUFFSIZE", 0))
         else:
             out = oracle.all_reduce(inputs, dtype, op)

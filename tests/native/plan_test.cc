@@ -162,7 +162,8 @@ int main(int argc, char** argv) {
            p.nChannels, (unsigned long)p.ll.ops[0].part,
            (unsigned long)p.ll.ops[0].chunk);
   else
-    printf("algo=%s nch=%d part=%lu slice=%lu steps=%d chunk=%lu\n", names[p.algo], p.nChannels,
-           (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps, (unsigned long)p.args.chunk);
+    printf("algo=%s nch=%d part=%lu slice=%lu steps=%d chunk=%lu cbdlo=%lu cbdhi=%lu\n", names[p.algo], p.nChannels,
+           (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps, (unsigned long)p.args.chunk,
+           (unsigned long)p.args.cbdLo, (unsigned long)p.args.cbdHi);
   return 0;
 }

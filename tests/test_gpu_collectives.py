@@ -98,8 +98,11 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (3, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
             (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}),
             (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"}),
-            # the reference's ring partition with many channel parts and loops at test sizes (small chunks)
+            # the reference's ring partition with many channel parts and loops at test sizes (small chunks): the
+            # ring itself, and the direct kernel walking the same partition (NCCL_AMD_REF_ORDER)
             (3, {"NCCL_ALGO": "RING", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "5"}),
+            (3, {"NCCL_AMD_REF_ORDER": "1", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "5"}),
+            (4, {"NCCL_AMD_REF_ORDER": "1", "NCCL_AMD_SLOT_BYTES": "4096"}),
             # cross-process memory: every dma-buf import refused -> the hipIpc handle fallback (ipc.cc); legacy
             # handles only (NCCL_AMD_IPC=legacy) run where the runtime is 7.2+, see test_legacy_ipc_runtime_gate
             (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}),

@@ -206,6 +206,7 @@ def test_c3_reducescatter_allgather_bf16_1GiB_n8(built):
 C4_SIZES = [8, 4096 + 2, 64 << 10, (1 << 20) + 6, 16 << 20, 256 << 20]
 C4_ALGOS = {"LL": {"NCCL_PROTO": "LL"}, "ONESHOT": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
             "DIRECT": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"}, "RING": {"NCCL_ALGO": "RING", "NCCL_MAX_CTAS": "32"},
+            "REFORDER": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32"},
             "TREE": {"NCCL_ALGO": "TREE"}}
 
 
@@ -218,7 +219,7 @@ def _c4_worker(rank, nranks, uid, q, uids):
         s = torch.cuda.Stream()
         comms = {}
         for k, (name, env) in enumerate(C4_ALGOS.items()):  # knobs are read at init: one comm per column
-            for key in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MAX_CTAS"):
+            for key in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MAX_CTAS", "NCCL_AMD_REF_ORDER"):
                 os.environ.pop(key, None)
             os.environ.update(env)
             comms[name] = nccl_amd.Communicator.init(nranks, rank, uids[k])
@@ -240,7 +241,7 @@ def _c4_worker(rank, nranks, uid, q, uids):
                     errs.append(f"{name} {nbytes} B rank {rank}: async {cm.async_error()}")
                     break
                 errs += _cmp(f"C4 {name} {nbytes} B rank {rank}", recv.cpu().numpy().view(np.uint16),
-                             want["chain" if name == "TREE" else "ring" if name == "RING" else "direct"], 6)
+                             want["chain" if name == "TREE" else "ring" if name in ("RING", "REFORDER") else "direct"], 6)
             if errs:
                 break
         for cm in comms.values():

@@ -20,7 +20,7 @@ FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
 # protocol settings, each its own communicator (tuning knobs are read at init)
 SETTINGS = [{}, {"NCCL_PROTO": "LL"}, {"NCCL_PROTO": "^LL", "NCCL_ALGO": "ONESHOT"},
             {"NCCL_PROTO": "^LL", "NCCL_ALGO": "DIRECT"}]
-KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_MAX_CTAS", "NCCL_BUFFSIZE")
+KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_MAX_CTAS", "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER")
 
 
 def _fixtures(n):
@@ -32,11 +32,12 @@ def _fixtures(n):
     return out
 
 
-def _ring_setting(z):
-    """NCCL_ALGO=RING fixtures (the reference's full-size ring partition) run on a ring communicator of the
-    fixture's channel count and NCCL_BUFFSIZE only."""
-    return {"NCCL_ALGO": "RING", "NCCL_PROTO": "Simple", "NCCL_MAX_CTAS": str(int(z["nchannels"])),
-            "NCCL_BUFFSIZE": str(int(z["buffsize"]))}
+def _ring_settings(z):
+    """NCCL_ALGO=RING fixtures (the reference's full-size ring partition) run on communicators of the fixture's
+    channel count and NCCL_BUFFSIZE only: the ring kernel, and the direct kernel on the same partition
+    (NCCL_AMD_REF_ORDER=1)."""
+    common = {"NCCL_MAX_CTAS": str(int(z["nchannels"])), "NCCL_BUFFSIZE": str(int(z["buffsize"]))}
+    return [dict(common, NCCL_ALGO="RING", NCCL_PROTO="Simple"), dict(common, NCCL_AMD_REF_ORDER="1")]
 
 
 def _worker(rank, n, uids, q):
@@ -50,7 +51,7 @@ def _worker(rank, n, uids, q):
         errs = []
         fixtures = _fixtures(n)
         runs = [(setting, [f for f in fixtures if str(f[1]["coll"]) != "allreduce_ring"]) for setting in SETTINGS]
-        runs += [(_ring_setting(z), [(name, z)]) for name, z in fixtures if str(z["coll"]) == "allreduce_ring"]
+        runs += [(st, [(name, z)]) for name, z in fixtures if str(z["coll"]) == "allreduce_ring" for st in _ring_settings(z)]
         for (setting, fx), uid in zip(runs, uids):
             for k in KNOBS:
                 os.environ.pop(k, None)
@@ -93,7 +94,7 @@ def test_golden_fixtures(built, n):
     import torch
     assert torch.cuda.is_available(), "GPU test on a box without a GPU"
     import nccl_amd
-    nring = sum(str(z["coll"]) == "allreduce_ring" for _, z in _fixtures(n))
+    nring = 2 * sum(str(z["coll"]) == "allreduce_ring" for _, z in _fixtures(n))
     uids = [nccl_amd.get_unique_id() for _ in range(len(SETTINGS) + nring)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -257,6 +257,26 @@ def test_link_channel_budget(exe, n, want):
         assert plan(exe, n, "ar", 7, (256 << 20) // 4, chancap=24)["nch"] == 24
 
 
+def test_reference_order_direct_allreduce(exe, built):
+    """NCCL_AMD_REF_ORDER=1: every AllReduce — the smallest included, no LL / one-shot — runs the direct kernel on the
+    reference's ring partition (the same parts and chunk as NCCL_ALGO=RING), other collectives keep their plans."""
+    import oracle
+    for n, dt, count, k, buff in ((2, 7, 1, 256, None), (2, 7, 1000, 256, None), (3, 6, 100_003, 7, 16384),
+                                  (8, 9, 1 << 27, 32, None), (4, 0, 5_000_000, 64, 65536), (8, 7, 1 << 22, 1, None)):
+        env = {"NCCL_AMD_REF_ORDER": 1}
+        if buff:
+            env["NCCL_BUFFSIZE"] = buff
+        p = plan(exe, n, "ar", dt, count, chancap=k, **env)
+        want = oracle.ring_nccl_plan(count, SIZES[dt], n, k, buff or 0)
+        assert p["algo"] == "direct", p
+        assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (n, dt, count, k, buff, p)
+        assert 0 < p["slice"] <= p["chunk"]
+    assert plan(exe, 8, "rs", 7, 8 << 20, NCCL_AMD_REF_ORDER=1)["cbdlo"] == 0
+    assert plan(exe, 2, "ar", 7, 1000, NCCL_AMD_REF_ORDER=1, NCCL_ALGO="TREE")["algo"] == "chain"
+    # ref-order AllReduces launch alone (never batched)
+    assert [l["ops"] for l in batch(exe, 2, *(["ar:7:1000000"] * 3), NCCL_AMD_REF_ORDER=1)] == [1, 1, 1]
+
+
 def test_ring_allreduce_takes_the_reference_partition(exe, built):
     """NCCL_ALGO=RING AllReduce is planned on the reference's own channel parts and chunk (enqueue.cc ringParts;
     reference enqueue.cc:576-757, 2091-2097, 2222-2321), identical to the C oracle's restatement over a sweep
