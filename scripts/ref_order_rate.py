@@ -1,0 +1,59 @@
+"""One-GPU rehearsal of the AllReduce rate with the default direct kernel, the direct kernel on the reference's
+ring partition (NCCL_AMD_REF_ORDER=1) and the ring (NCCL_ALGO=RING), all ranks in one process, 256 MiB per rank.
+Prints one JSON line per (n, dtype, mode). usage: python scripts/ref_order_rate.py [MIB] [ITERS]"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+import torch  # noqa: E402
+
+import nccl_amd  # noqa: E402
+
+MODES = {"direct": {}, "ref_order": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32"},
+         "ref_order_cap": {"NCCL_AMD_REF_ORDER": "1"}, "ring": {"NCCL_ALGO": "RING", "NCCL_MAX_CTAS": "32"}}
+
+
+def main():
+    mib = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+    iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    torch.cuda.set_device(0)
+    for n in (2, 4):
+        for dt, tdt, es in ((7, torch.float32, 4), (9, torch.bfloat16, 2)):
+            count = (mib << 20) // es
+            bufs = [(torch.empty(count, dtype=tdt, device="cuda").uniform_(-1, 1), torch.empty(count, dtype=tdt, device="cuda"))
+                    for _ in range(n)]
+            for mode, env in MODES.items():
+                for k in ("NCCL_AMD_REF_ORDER", "NCCL_MAX_CTAS", "NCCL_ALGO"):
+                    os.environ.pop(k, None)
+                os.environ.update(env)
+                comms = nccl_amd.Communicator.init_all([0] * n)
+                streams = [torch.cuda.Stream() for _ in range(n)]
+
+                def step():
+                    with nccl_amd.group():
+                        for c, s, (x, y) in zip(comms, streams, bufs):
+                            c.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, dt, 0, s.cuda_stream)
+                for _ in range(3):
+                    step()
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(iters):
+                    step()
+                for s in streams:
+                    torch.cuda.current_stream().wait_stream(s)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / iters
+                print(json.dumps({"n": n, "dtype": dt, "mode": mode, "ms": round(ms, 4),
+                                  "GBps_per_rank": round((mib << 20) / (ms * 1e-3) / 1e9, 1),
+                                  "async": [c.async_error() for c in comms]}), flush=True)
+                for c in comms:
+                    c.destroy()
+            del bufs
+
+
+if __name__ == "__main__":
+    main()
