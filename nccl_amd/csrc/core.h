@@ -229,6 +229,8 @@ struct CommTuning {
   int64_t copyGrid;         // NCCL_AMD_COPY_GRID (cap on its workgroups; default: one per 16 KiB tile)
   int64_t ringChunkBytes;   // NCCL_ALGO=RING AllReduce chunk: NCCL_BUFFSIZE / NCCL_STEPS * ALLREDUCE_CHUNKSTEPS
   int refOrder;             // NCCL_AMD_REF_ORDER: AllReduce on the direct kernel in the reference's ring partition
+  int refProto;             // ... of this protocol (NCCL_PROTO_LL 0, LL128 1, SIMPLE 2: the one NCCL_PROTO names)
+  int64_t refChunkBytes;    // that protocol's ring chunk (NCCL_BUFFSIZE / NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE)
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
 void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known

@@ -152,6 +152,21 @@ void loadTuning(CommTuning* t) {
   const int64_t buff = paramInt("NCCL_BUFFSIZE", 4 << 20);
   t->ringChunkBytes = buff / 8 * 4 / 512 * 512;
   if (t->ringChunkBytes < 512) t->ringChunkBytes = 512;
+  // The partition REF_ORDER walks is the reference's ring partition of the protocol NCCL_PROTO names alone (LL or
+  // LL128; Simple otherwise), with that protocol's chunk: stepSize = buffer / NCCL_STEPS, Simple x 4 in 512-byte
+  // grains, LL / 2 in 16-byte grains, LL128 x 15/16 in 1920-byte grains (enqueue.cc:2222-2227, 2321; buffers
+  // init.cc:810-827: 4 MiB, 8 x 512 x 8 x 16 B, 120 x 640 x 8 x 8 B). A chunk below one grain (which never
+  // advances in the reference) is raised to one grain.
+  t->refProto = t->llOn && !t->simpleOn && !t->ll128On ? 0 : t->ll128On && !t->llOn && !t->simpleOn ? 1 : 2;
+  if (t->refProto == 2) {
+    t->refChunkBytes = t->ringChunkBytes;
+  } else if (t->refProto == 0) {
+    t->refChunkBytes = paramInt("NCCL_LL_BUFFSIZE", 8 * 512 * 8 * 16) / 8 / 2 / 16 * 16;
+    if (t->refChunkBytes < 16) t->refChunkBytes = 16;
+  } else {
+    t->refChunkBytes = paramInt("NCCL_LL128_BUFFSIZE", 120 * 640 * 8 * 8) / 8 / 16 * 15 / 1920 * 1920;
+    if (t->refChunkBytes < 1920) t->refChunkBytes = 1920;
+  }
 }
 
 // CU budget of the large staged and zero-copy plans at n >= 3 (reference: channels and threads shrink below
@@ -255,24 +270,29 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
 // NCCL_ALGO=RING AllReduce: the reference's own partition, so that every element is finalised by the same ring
 // position as in the reference's RING/SIMPLE AllReduce on a communicator of K channels (here K = chanCap, i.e.
 // NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS = K there) with the same NCCL_BUFFSIZE — bit-identical results, floats
-// included. For one task, starting on channel 0 with no traffic planned yet:
-//  * channels: K shrunk while the bytes are below K x 512 threads x 64 (topoGetAlgoInfo, enqueue.cc:2091-2097;
-//    NCCL_SIMPLE_MAX_NTHREADS and NCCL_SIMPLE_THREAD_THRESHOLD, tuning.cc:246, 591);
-//  * channel parts over 16 KiB cells (32 KiB of AllReduce traffic): a first part sized to the traffic per
-//    channel, equal middle parts, a remainder part (scheduleCollTasksToPlan, enqueue.cc:576-757);
-//  * each part walked in loops of n chunks of tune.ringChunkBytes, the last loop re-cut (kernel, pipe.h).
+// included. NCCL_AMD_REF_ORDER walks the same partition, or the one of RING/LL or RING/LL128
+// (`proto` 0 / 1). For one task, starting on channel 0 with no traffic planned yet:
+//  * channels: K shrunk while the bytes are below K x threads x threshold — 512 x 64 (Simple), 512 x 8n (LL),
+//    640 x 8 (LL128) (topoGetAlgoInfo, enqueue.cc:2091-2097; tuning.cc:244-257, 589-593);
+//  * channel parts over cells of 32 KiB of traffic (AllReduce: 2 bytes of traffic per byte, 8 under LL,
+//    enqueue.cc:461, 658): a first part sized to the traffic per channel, equal middle parts, a remainder part
+//    (scheduleCollTasksToPlan, enqueue.cc:576-757);
+//  * each part walked in loops of n chunks of tune.ringChunkBytes / refChunkBytes, the last loop re-cut (kernel,
+//    pipe.h).
 struct RingParts {
   int nch;
   uint64_t lo, mid, hi;
 };
-static RingParts ringParts(uint64_t count, int ts, int K) {
+static RingParts ringParts(uint64_t count, int ts, int K, int n, int proto) {
   const uint64_t bytes = count * (uint64_t)ts;
+  const uint64_t threads = proto == 1 ? 640 : 512, threshold = proto == 0 ? 8 * (uint64_t)n : proto == 1 ? 8 : 64;
   int nc = K;
-  while (nc >= 2 && bytes < (uint64_t)nc * 512 * 64) nc--;
-  const uint64_t cell = 16 << 10, trafficCell = 2 * cell;  // AllReduce moves 2 bytes of traffic per byte
+  while (nc >= 2 && bytes < (uint64_t)nc * threads * threshold) nc--;
+  const uint64_t tpb = proto == 0 ? 8 : 2;  // traffic bytes per AllReduce byte
+  const uint64_t cell = ((32 << 10) / tpb + 15) / 16 * 16, trafficCell = tpb * cell;
   const uint64_t eltsPerCell = cell / ts;
   const uint64_t cells = (bytes + cell - 1) / cell;
-  const uint64_t traffic = std::max<uint64_t>(32 << 10, 2 * bytes);
+  const uint64_t traffic = std::max<uint64_t>(32 << 10, tpb * bytes);
   const uint64_t perChannel = (traffic / nc + 15) / 16 * 16;
   const uint64_t perChannelCells = (perChannel + trafficCell - 1) / trafficCell;
   uint64_t cellsPerCh = std::min(cells, perChannelCells);
@@ -520,7 +540,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       const size_t span = chain ? count * ts : blockElems * ts;
       planChannels(comm, span, ts, p, (size_t)comm->tune.minChannelBytes, comm->chanCap);
       if (kind == PIPE_RING_AR) {  // the reference's channel parts and loop chunk (ringParts above)
-        const RingParts r = ringParts(count, ts, comm->chanCap);
+        const RingParts r = ringParts(count, ts, comm->chanCap, n, 2);
         p.nChannels = r.nch;
         p.args.cbdLo = r.lo;
         p.args.part = r.mid;
@@ -535,16 +555,16 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     }
   }
   if (refOrder) {
-    // The reference's RING/SIMPLE partition (ringParts: channel parts, NCCL_BUFFSIZE chunks, loops) walked by the
-    // direct scatter-reduce-gather kernel: in each loop chunk q is finalised by rank q, as in the reference's ring,
+    // The reference's ring partition of the protocol NCCL_PROTO names (ringParts: channel parts, the protocol's
+    // chunks, loops; Simple unless NCCL_PROTO is LL or LL128 alone) walked by the direct scatter-reduce-gather kernel: in each loop chunk q is finalised by rank q, as in the reference's ring,
     // so every element folds in its order — at the direct kernel's n-1 links instead of the ring's one (kernels.h
     // Channel::refPart). All channels of the communicator's cap, no CU budget: the partition is the reference's.
-    const RingParts r = ringParts(count, ts, comm->chanCap);
+    const RingParts r = ringParts(count, ts, comm->chanCap, n, comm->tune.refProto);
     p.nChannels = r.nch;
     p.args.cbdLo = r.lo;
     p.args.part = r.mid;
     p.args.cbdHi = r.hi;
-    p.args.chunk = (uint64_t)comm->tune.ringChunkBytes / ts;
+    p.args.chunk = (uint64_t)comm->tune.refChunkBytes / ts;
     p.args.slice = std::min<uint64_t>(p.args.chunk, comm->slotBytes / ts / epp * epp);
     p.args.nSteps = 0;  // per channel (kernels.h Channel::refSteps)
     TRACE("%s: direct in the reference's partition, nch %d parts %lu/%lu/%lu chunk %lu slice %lu", info.opName,

@@ -36,6 +36,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_all_reduce_chain.argtypes = [I, I, U64, I, PP, S, P]
         L.oracle_all_reduce_ring_nccl.argtypes = [I, I, U64, I, PP, S, P, I, S]
         L.oracle_ring_nccl_plan.argtypes = [S, I, I, I, S, ctypes.POINTER(U64)]
+        L.oracle_all_reduce_ring_nccl_proto.argtypes = [I, I, U64, I, PP, S, P, I, I, S]
+        L.oracle_ring_nccl_plan_proto.argtypes = [S, I, I, I, I, S, ctypes.POINTER(U64)]
         L.oracle_reduce_scatter.argtypes = [I, I, U64, I, PP, S, PP]
         L.oracle_reduce.argtypes = [I, I, U64, I, I, PP, S, P]
         L.oracle_fill.argtypes = [I, U64, S, P, I]
@@ -98,25 +100,32 @@ def all_reduce_chain(inputs: Sequence[np.ndarray], dtype: int, op: int = 0):
     return out
 
 
-def ring_nccl_plan(count: int, type_size: int, nranks: int, nchannels: int, buffsize: int = 0):
-    """The reference's RING/SIMPLE AllReduce partition of `count` elements on a communicator of `nchannels`
-    channels (nccl_oracle.c oracle_ring_nccl_plan): (channels, countLo, countMid, countHi, chunk elements)."""
+PROTO_LL, PROTO_LL128, PROTO_SIMPLE = 0, 1, 2  # NCCL_PROTO_* ids (reference device.h)
+
+
+def ring_nccl_plan(count: int, type_size: int, nranks: int, nchannels: int, buffsize: int = 0,
+                   proto: int = PROTO_SIMPLE):
+    """The reference's RING AllReduce partition of `count` elements on a communicator of `nchannels` channels
+    under protocol `proto` with that protocol's buffer size (0 = its default; nccl_oracle.c
+    oracle_ring_nccl_plan_proto): (channels, countLo, countMid, countHi, chunk elements)."""
     plan = (ctypes.c_uint64 * 5)()
-    rc = lib().oracle_ring_nccl_plan(count, type_size, nranks, nchannels, buffsize, plan)
+    rc = lib().oracle_ring_nccl_plan_proto(count, type_size, nranks, nchannels, proto, buffsize, plan)
     if rc:
         raise ValueError("invalid ring plan arguments")
     return tuple(int(x) for x in plan)
 
 
-def all_reduce_ring_nccl(inputs: Sequence[np.ndarray], dtype: int, op: int, nchannels: int, buffsize: int = 0):
-    """ncclAllReduce with NCCL_ALGO=RING, NCCL_PROTO=Simple in the reference's full-size order: channel parts,
-    loops of n chunks, last loop re-cut (all_reduce.h:21-81) on a communicator of `nchannels` channels."""
+def all_reduce_ring_nccl(inputs: Sequence[np.ndarray], dtype: int, op: int, nchannels: int, buffsize: int = 0,
+                         proto: int = PROTO_SIMPLE):
+    """ncclAllReduce with NCCL_ALGO=RING in the reference's full-size order for protocol `proto` (Simple by
+    default): channel parts, loops of n chunks, last loop re-cut (all_reduce.h:21-81) on a communicator of
+    `nchannels` channels."""
     n = len(inputs)
     d, arg = dev_op(op, dtype, n)
     ins = [np.ascontiguousarray(x) for x in inputs]
     out = np.empty_like(ins[0])
-    rc = lib().oracle_all_reduce_ring_nccl(dtype, d, arg, n, _ptrs(ins), ins[0].size, out.ctypes.data, nchannels,
-                                           buffsize)
+    rc = lib().oracle_all_reduce_ring_nccl_proto(dtype, d, arg, n, _ptrs(ins), ins[0].size, out.ctypes.data,
+                                                 nchannels, proto, buffsize)
     assert rc == 0
     return out
 

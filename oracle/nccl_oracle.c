@@ -345,38 +345,49 @@ int oracle_all_reduce(int dt, int devop, uint64_t arg, int n, const void* const*
   return 0;
 }
 
-/* ---- the reference's RING/SIMPLE AllReduce partition at full size (more than one channel and loop) ----
+/* ---- the reference's RING AllReduce partition at full size (more than one channel and loop) ----
  * NCCL cuts a large AllReduce into channel parts and each part into loops of n chunks; a chunk's elements are
  * finalised by the ring position of the chunk INSIDE ITS LOOP, so which rank's input an element's fold starts
- * from depends on this partition. Restated for ONE task on a communicator of `nchannels` channels with an
- * NCCL_BUFFSIZE of `buffsize` bytes (0 = the 4 MiB default, src/init.cc:813):
- *   channel count   topoGetAlgoInfo, RING/SIMPLE: nc = nchannels, decremented while
- *                   nBytes < nc * nt * threshold with nt = 512 (NCCL_SIMPLE_MAX_NTHREADS, tuning.cc:244-247,
- *                   NVLink-class bandwidth) and threshold 64 (NCCL_SIMPLE_THREAD_THRESHOLD, tuning.cc:591):
- *                   src/enqueue.cc:2070-2097
- *   parts (CBD)     scheduleCollTasksToPlan for a lone task (channelId 0, no traffic yet): 16 KiB cells
- *                   (32 KiB of traffic at 2 bytes per byte for AllReduce), lo / mid / hi channel parts:
- *                   src/enqueue.cc:576-757, trafficPerByte :91-94; the part of channel c: device.h:337-361
- *   chunk           calcCollChunking, RING/SIMPLE: buffsize / NCCL_STEPS (8) * ALLREDUCE_CHUNKSTEPS (4),
- *                   in 512-byte grains: src/enqueue.cc:2222-2225, 2321; collectives.h:19-20; device.h:328-334
+ * from depends on this partition. The three protocols run the same ring (runRing<T, RedOp, Proto>,
+ * src/device/all_reduce.h:13-83, 229-233, 763-781) on different partitions. Restated for ONE task on a
+ * communicator of `nchannels` channels, protocol `proto` (0 LL, 1 LL128, 2 SIMPLE: NCCL_PROTO_* ids) with that
+ * protocol's buffer of `buffsize` bytes (0 = its default: NCCL_LL_BUFFSIZE 8 lines x 512 threads x 8 steps x
+ * 16 B = 512 KiB, NCCL_LL128_BUFFSIZE 120 x 640 x 8 x 8 B, NCCL_BUFFSIZE 4 MiB; src/init.cc:810-827):
+ *   channel count   topoGetAlgoInfo, RING: nc = nchannels, decremented while nBytes < nc * nt * threshold
+ *                   (src/enqueue.cc:2070-2097) with nt / threshold = 512 / 64 (SIMPLE, NVLink-class bandwidth,
+ *                   tuning.cc:244-247, 591), 512 / 8 x nranks (LL, tuning.cc:253-254, 589, 593), 640 / 8
+ *                   (LL128, tuning.cc:255-257, 590)
+ *   parts (CBD)     scheduleCollTasksToPlan for a lone task (channelId 0, no traffic yet): AllReduce moves 2 bytes
+ *                   of traffic per byte, 8 under LL (enqueue.cc:461, 658); cells of 32 KiB of traffic (16 KiB of
+ *                   data, 4 KiB under LL), lo / mid / hi channel parts: src/enqueue.cc:576-757, trafficPerByte
+ *                   :91-94; the part of channel c: device.h:337-361
+ *   chunk           calcCollChunking, RING: stepSize = buffsize / NCCL_STEPS (8); SIMPLE x ALLREDUCE_CHUNKSTEPS
+ *                   (4) in 512-byte grains, LL / 2 in 16-byte grains, LL128 x 15/16 (data elements per 128-byte
+ *                   line) in 1920-byte grains: src/enqueue.cc:2222-2227, 2321; collectives.h:19-20;
+ *                   device.h:328-334, 97-117
  *   loops           runRing: loopCount = n * chunkCount; the last loop re-cuts chunkCount to
  *                   alignUp(divUp(rem, n), 16 / sizeof(T)): src/device/all_reduce.h:21-38
  * plan[0..4] = {channels, countLo, countMid, countHi, chunk elements}. */
 static size_t div_up(size_t a, size_t b) { return (a + b - 1) / b; }
 
-int oracle_ring_nccl_plan(size_t count, int ts, int nranks, int nchannels, size_t buffsize, uint64_t* plan) {
-  if (ts <= 0 || nranks <= 0 || nchannels <= 0 || count == 0) return 4;
-  if (buffsize == 0) buffsize = (size_t)1 << 22;
+int oracle_ring_nccl_plan_proto(size_t count, int ts, int nranks, int nchannels, int proto, size_t buffsize,
+                                uint64_t* plan) {
+  if (ts <= 0 || nranks <= 0 || nchannels <= 0 || count == 0 || proto < 0 || proto > 2) return 4;
+  static const size_t defBuff[3] = {(size_t)8 * 512 * 8 * 16, (size_t)120 * 640 * 8 * 8, (size_t)1 << 22};
+  static const size_t grain[3] = {16, 1920, 512};
+  if (buffsize == 0) buffsize = defBuff[proto];
   /* channel count (enqueue.cc:2093-2096) */
   const size_t nBytes = count * (size_t)ts;
+  const size_t nt = proto == 1 ? 640 : 512;
+  const size_t thr = proto == 0 ? (size_t)8 * nranks : proto == 1 ? 8 : 64;
   int nc = nchannels;
-  while (nBytes < (size_t)nc * 512 * 64) {
+  while (nBytes < (size_t)nc * nt * thr) {
     if (nc >= 2) nc--;
     else break;
   }
   /* CBD (enqueue.cc:580-604, 617-620, 657-701) */
   const size_t minTraffic = (size_t)32 << 10;
-  const size_t trafficPerByte = 2;
+  const size_t trafficPerByte = proto == 0 ? 8 : 2;
   size_t trafficBytes = count * (size_t)ts * trafficPerByte;
   if (trafficBytes < minTraffic) trafficBytes = minTraffic;
   const size_t trafficPerChannel = div_up(trafficBytes / (size_t)nc, 16) * 16;
@@ -414,28 +425,34 @@ int oracle_ring_nccl_plan(size_t count, int ts, int nranks, int nchannels, size_
   if (countHi != 0) countHi -= excess;
   else countLo -= excess;
   used = (countLo != 0) + nMid + (cellsHi != 0);
-  /* chunk (enqueue.cc:2222-2225, 2321): SIMPLE grain 512 bytes */
-  size_t chunkBytes = buffsize / 8 * 4;
-  chunkBytes = chunkBytes / 512 * 512;
+  /* chunk (enqueue.cc:2222-2227, 2321), in grains; the device's chunkCount = grains x grain / sizeof(T) */
+  const size_t step = buffsize / 8;
+  size_t chunkBytes = proto == 2 ? step * 4 : proto == 0 ? step / 2 : step / 16 * 15;
+  const size_t grains = chunkBytes / grain[proto];
+  if (grains == 0) return 4; /* a zero chunk never advances (the reference loops forever) */
   plan[0] = (uint64_t)used;
   plan[1] = countLo;
   plan[2] = countMid;
   plan[3] = countHi;
-  plan[4] = chunkBytes / (size_t)ts;
+  plan[4] = grains * (grain[proto] / (size_t)ts);
   return 0;
 }
 
-/* AllReduce in the reference's RING/SIMPLE order at full size: element e of channel part [off, off + cnt) in
- * loop l = (e - off) / (n * chunk) lies in chunk q of that loop and is finalised by ring position q, i.e. folded
- * from q + 1 (all_reduce.h:42-81; ring index = rank). */
-int oracle_all_reduce_ring_nccl(int dt, int devop, uint64_t arg, int n, const void* const* in, size_t count,
-                                void* out, int nchannels, size_t buffsize) {
+int oracle_ring_nccl_plan(size_t count, int ts, int nranks, int nchannels, size_t buffsize, uint64_t* plan) {
+  return oracle_ring_nccl_plan_proto(count, ts, nranks, nchannels, 2, buffsize, plan);
+}
+
+/* AllReduce in the reference's RING order at full size: element e of channel part [off, off + cnt) in loop
+ * l = (e - off) / (n * chunk) lies in chunk q of that loop and is finalised by ring position q, i.e. folded from
+ * q + 1 (all_reduce.h:42-81; ring index = rank). */
+int oracle_all_reduce_ring_nccl_proto(int dt, int devop, uint64_t arg, int n, const void* const* in, size_t count,
+                                      void* out, int nchannels, int proto, size_t buffsize) {
   int ts = oracle_type_size(dt);
   if (ts <= 0 || n <= 0) return 4;
   if (count == 0) return 0;
   if (n == 1) return oracle_all_reduce(dt, devop, arg, n, in, count, out);
   uint64_t plan[5];
-  if (oracle_ring_nccl_plan(count, ts, n, nchannels, buffsize, plan)) return 4;
+  if (oracle_ring_nccl_plan_proto(count, ts, n, nchannels, proto, buffsize, plan)) return 4;
   const int nch = (int)plan[0];
   const size_t epp = (size_t)(16 / ts);
   for (int c = 0; c < nch; c++) {
@@ -458,6 +475,11 @@ int oracle_all_reduce_ring_nccl(int dt, int devop, uint64_t arg, int n, const vo
     }
   }
   return 0;
+}
+
+int oracle_all_reduce_ring_nccl(int dt, int devop, uint64_t arg, int n, const void* const* in, size_t count,
+                                void* out, int nchannels, size_t buffsize) {
+  return oracle_all_reduce_ring_nccl_proto(dt, devop, arg, n, in, count, out, nchannels, 2, buffsize);
 }
 
 /* AllReduce over the reference's intra-node TREE (NCCL_ALGO=TREE): a chain with root 0 and leaf n-1

@@ -19,7 +19,7 @@ from tests import gpu_cases as G  # noqa: E402
 KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_AG_PULL",
          "NCCL_AMD_RS_PULL", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_LL_CHANNEL_BYTES", "NCCL_AMD_LL128",
          "NCCL_AMD_LL128_CHANNEL_BYTES", "NCCL_AMD_SYM_WT", "NCCL_AMD_P2P_FENCE", "NCCL_AMD_LINK_CHANNELS",
-         "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER")
+         "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER", "NCCL_LL_BUFFSIZE", "NCCL_LL128_BUFFSIZE")
 
 
 def settings(rng):
@@ -58,6 +58,10 @@ def settings(rng):
         env["NCCL_AMD_REF_ORDER"] = "1"
     if rng.random() < 0.2:  # the reference's knob: slot size here, and the ring's chunk (many ring loops)
         env["NCCL_BUFFSIZE"] = str(rng.choice([8192, 16384, 65536]))
+    if rng.random() < 0.15:  # the LL / LL128 ring chunks REF_ORDER walks when NCCL_PROTO names that protocol alone
+        env["NCCL_LL_BUFFSIZE"] = str(rng.choice([4096, 65536, 524288]))
+    if rng.random() < 0.15:
+        env["NCCL_LL128_BUFFSIZE"] = str(rng.choice([32768, 262144]))
     return env
 
 

@@ -120,19 +120,26 @@ def allreduce(kind, dtype, ins):
     return out
 
 
-def ring_parts(count, esize, n, nchannels, buffsize):
-    """The reference's RING/SIMPLE AllReduce partition of one task on a communicator of `nchannels` channels
-    (restated from src/enqueue.cc:2091-2097 channel shrink, :576-757 continuous-byte-distribution over 16 KiB
-    cells with the first channel's part sized to the traffic per channel, :2222-2321 chunk = buffsize / 8 * 4 in
-    512-byte grains): returns the element counts of the channel parts, in channel order, and the chunk."""
+def ring_parts(count, esize, n, nchannels, buffsize, proto="simple"):
+    """The reference's RING AllReduce partition of one task on a communicator of `nchannels` channels under
+    protocol `proto` ("simple", "ll", "ll128") with that protocol's buffer size (0 = its default), restated from
+    src/enqueue.cc:2091-2097 (channel shrink: threads x threshold 512 x 64, 512 x 8n, 640 x 8 with tuning.cc
+    :244-257, 589-593), :576-757 (continuous-byte-distribution over cells of 32 KiB of traffic, AllReduce moving
+    2 bytes of traffic per byte, 8 under LL, :461/:658; the first channel's part sized to the traffic per channel)
+    and :2222-2321 (chunk: buffsize / 8 x 4 in 512-byte grains, / 8 / 2 in 16-byte grains, / 8 / 16 x 15 in
+    1920-byte grains): returns the element counts of the channel parts, in channel order, and the chunk."""
+    default = {"ll": 8 * 512 * 8 * 16, "ll128": 120 * 640 * 8 * 8, "simple": 1 << 22}[proto]
+    buffsize = buffsize or default
+    threads, threshold = {"simple": (512, 64), "ll": (512, 8 * n), "ll128": (640, 8)}[proto]
+    tpb = 8 if proto == "ll" else 2           # traffic bytes per AllReduce byte
     nbytes = count * esize
     nc = nchannels
-    while nc > 1 and nbytes < nc * 512 * 64:
+    while nc > 1 and nbytes < nc * threads * threshold:
         nc -= 1
-    cell = 16384                              # 32 KiB minimum traffic / 2 traffic bytes per AllReduce byte
+    cell = -(-(32768 // tpb) // 16) * 16      # 32 KiB minimum traffic per channel, in data bytes
     ncells = -(-nbytes // cell)
-    per_channel = -(-(max(32768, 2 * nbytes) // nc) // 16) * 16
-    per = -(-per_channel // (2 * cell))       # cells of traffic per channel
+    per_channel = -(-(max(32768, tpb * nbytes) // nc) // 16) * 16
+    per = -(-per_channel // (tpb * cell))     # cells of traffic per channel
     step = min(ncells, per)
     first = ncells if nchannels == 1 else min(ncells, per)
     mids, last = divmod(ncells - first, step)
@@ -145,14 +152,17 @@ def ring_parts(count, esize, n, nchannels, buffsize):
     cells = [first] + [step] * mids + ([last] if last else [])
     parts = [c * cell // esize for c in cells]
     parts[-1] -= ncells * cell // esize - count
-    chunk = (buffsize // 8 * 4) // 512 * 512 // esize
+    stepsize = buffsize // 8
+    chunk_bytes, grain = {"simple": (stepsize * 4, 512), "ll": (stepsize // 2, 16),
+                          "ll128": (stepsize // 16 * 15, 1920)}[proto]
+    chunk = chunk_bytes // grain * (grain // esize)
     return parts, chunk
 
 
-def ring_owners(count, esize, n, nchannels, buffsize):
+def ring_owners(count, esize, n, nchannels, buffsize, proto="simple"):
     """Ring position that finalises each element: inside each channel part, loops of n chunks; the last loop's
     chunk is re-cut to alignUp(divUp(rem, n), 16 / esize) (src/device/all_reduce.h:34-38)."""
-    parts, chunk = ring_parts(count, esize, n, nchannels, buffsize)
+    parts, chunk = ring_parts(count, esize, n, nchannels, buffsize, proto)
     epp = 16 // esize
     owner = np.empty(count, dtype=np.int64)
     base = 0
@@ -167,9 +177,9 @@ def ring_owners(count, esize, n, nchannels, buffsize):
     return owner
 
 
-def allreduce_ring(kind, dtype, ins, nchannels, buffsize):
+def allreduce_ring(kind, dtype, ins, nchannels, buffsize, proto="simple"):
     n, count = len(ins), ins[0].size
-    owner = ring_owners(count, ESIZE[dtype], n, nchannels, buffsize)
+    owner = ring_owners(count, ESIZE[dtype], n, nchannels, buffsize, proto)
     out = np.empty_like(ins[0])
     for c in range(n):
         idx = np.nonzero(owner == c)[0]
@@ -208,6 +218,13 @@ RING_CASES = [
     ("max", "f32", 5, 30011, 6, 8192), ("avg", "f32", 8, 40000, 5, 16384), ("sum", "i32", 3, 9000, 2, 8192),
     ("sum", "f32", 2, 120_000, 7, 65536),
 ]
+# the same ring on the LL and LL128 partitions (protocol buffer sizes NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE; 0 =
+# the reference's default): several channel parts and loops each
+RING_PROTO_CASES = [
+    ("sum", "f32", 3, 20000, 4, 65536, "ll"), ("sum", "bf16", 4, 30001, 5, 32768, "ll"),
+    ("sum", "f16", 5, 60000, 6, 65536, "ll128"), ("max", "f32", 2, 25013, 3, 131072, "ll128"),
+    ("sum", "f32", 8, 3000, 256, 0, "ll"), ("sum", "bf16", 3, 200_000, 4, 0, "ll128"),
+]
 
 
 def main():
@@ -241,7 +258,17 @@ def main():
         d["out"] = allreduce_ring(kind, dtype, ins, nch, buffsize)
         name = f"{len(CASES) + j:02d}_allreduce_ring_{kind}_{dtype}_n{n}_k{nch}"
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
-    print(f"wrote {len(CASES) + len(RING_CASES)} fixtures to {HERE}")
+    base = len(CASES) + len(RING_CASES)
+    for j, (kind, dtype, n, count, nch, buffsize, proto) in enumerate(RING_PROTO_CASES):
+        ins = gen_inputs(rng, dtype, n, count)
+        d = {"coll": "allreduce_ring", "dtype": NCCL_DT[dtype], "op": NCCL_OP[kind], "n": n, "nchannels": nch,
+             "buffsize": buffsize, "proto": proto}
+        for r, x in enumerate(ins):
+            d[f"in{r}"] = x
+        d["out"] = allreduce_ring(kind, dtype, ins, nch, buffsize, proto)
+        name = f"{base + j:02d}_allreduce_ring_{proto}_{kind}_{dtype}_n{n}_k{nch}"
+        np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+    print(f"wrote {base + len(RING_PROTO_CASES)} fixtures to {HERE}")
 
 
 if __name__ == "__main__":

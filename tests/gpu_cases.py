@@ -85,6 +85,24 @@ def ref_order_runs(n: int) -> bool:
         os.environ.get("NCCL_ALGO", "").upper() not in ("TREE", "RING")
 
 
+def ref_proto() -> tuple[int, int]:
+    """The protocol whose ring partition NCCL_AMD_REF_ORDER walks and that protocol's buffer size (0 = default):
+    LL or LL128 when NCCL_PROTO enables that one protocol alone, Simple otherwise (enqueue.cc loadTuning)."""
+    proto = os.environ.get("NCCL_PROTO", "")
+    on = {"ll": True, "simple": True, "ll128": _env_int("NCCL_AMD_LL128", 0) != 0}
+    if proto:
+        excl = proto.startswith("^")
+        toks = {t.strip().lower() for t in proto.lstrip("^").split(",")}
+        on = {k: ((k not in toks) and (on[k] if k == "ll128" else True)) if excl else (k in toks) for k in on}
+        if not any(on.values()):
+            on["simple"] = True
+    if on["ll"] and not on["simple"] and not on["ll128"]:
+        return oracle.PROTO_LL, _env_int("NCCL_LL_BUFFSIZE", 0)
+    if on["ll128"] and not on["ll"] and not on["simple"]:
+        return oracle.PROTO_LL128, _env_int("NCCL_LL128_BUFFSIZE", 0)
+    return oracle.PROTO_SIMPLE, _env_int("NCCL_BUFFSIZE", 0)
+
+
 def expected(coll: str, inputs, dtype: int, op: int, root: int = 0, algo: str = ""):
     if coll == "allreduce":
         # NCCL_ALGO=TREE folds every element in the chain's order; NCCL_ALGO=RING in the reference's ring order
@@ -94,8 +112,11 @@ def expected(coll: str, inputs, dtype: int, op: int, root: int = 0, algo: str = 
         algo = algo or os.environ.get("NCCL_ALGO", "").upper()
         if algo == "TREE":
             out = oracle.all_reduce_chain(inputs, dtype, op)
-        elif (algo == "RING" and ring_runs(n)) or ref_order_runs(n):
+        elif algo == "RING" and ring_runs(n):
             out = oracle.all_reduce_ring_nccl(inputs, dtype, op, ring_channels(n), _env_int("NCCL_BUFFSIZE", 0))
+        elif ref_order_runs(n):
+            proto, buff = ref_proto()
+            out = oracle.all_reduce_ring_nccl(inputs, dtype, op, ring_channels(n), buff, proto)
         else:
             out = oracle.all_reduce(inputs, dtype, op)
         return [out] * len(inputs)

@@ -207,7 +207,11 @@ C4_SIZES = [8, 4096 + 2, 64 << 10, (1 << 20) + 6, 16 << 20, 256 << 20]
 C4_ALGOS = {"LL": {"NCCL_PROTO": "LL"}, "ONESHOT": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
             "DIRECT": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"}, "RING": {"NCCL_ALGO": "RING", "NCCL_MAX_CTAS": "32"},
             "REFORDER": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32"},
+            # the reference's RING/LL and RING/LL128 partitions (the lower end of the curve), up to 16 MiB
+            "REFORDER_LL": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32", "NCCL_PROTO": "LL"},
+            "REFORDER_LL128": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32", "NCCL_PROTO": "LL128"},
             "TREE": {"NCCL_ALGO": "TREE"}}
+C4_PROTO_MAX = 16 << 20
 
 
 def _c4_worker(rank, nranks, uid, q, uids):
@@ -229,9 +233,14 @@ def _c4_worker(rank, nranks, uid, q, uids):
             # RING: the reference's ring partition on the RING communicator's 32 channels (enqueue.cc ringParts)
             want = {"direct": oracle.all_reduce(inputs, 6, 0), "chain": oracle.all_reduce_chain(inputs, 6, 0),
                     "ring": oracle.all_reduce_ring_nccl(inputs, 6, 0, 32)}
+            if nbytes <= C4_PROTO_MAX:
+                want["REFORDER_LL"] = oracle.all_reduce_ring_nccl(inputs, 6, 0, 32, 0, oracle.PROTO_LL)
+                want["REFORDER_LL128"] = oracle.all_reduce_ring_nccl(inputs, 6, 0, 32, 0, oracle.PROTO_LL128)
             send = _dev(torch, inputs[rank])
             for name, cm in comms.items():
                 if name == "LL" and nbytes > 512 << 10:  # beyond the LL line area the default plan runs
+                    continue
+                if name.startswith("REFORDER_") and nbytes > C4_PROTO_MAX:
                     continue
                 recv = torch.zeros_like(send)
                 torch.cuda.synchronize()
@@ -241,6 +250,7 @@ def _c4_worker(rank, nranks, uid, q, uids):
                     errs.append(f"{name} {nbytes} B rank {rank}: async {cm.async_error()}")
                     break
                 errs += _cmp(f"C4 {name} {nbytes} B rank {rank}", recv.cpu().numpy().view(np.uint16),
+                             want[name] if name in want else
                              want["chain" if name == "TREE" else "ring" if name in ("RING", "REFORDER") else "direct"], 6)
             if errs:
                 break

@@ -20,7 +20,11 @@ FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
 # protocol settings, each its own communicator (tuning knobs are read at init)
 SETTINGS = [{}, {"NCCL_PROTO": "LL"}, {"NCCL_PROTO": "^LL", "NCCL_ALGO": "ONESHOT"},
             {"NCCL_PROTO": "^LL", "NCCL_ALGO": "DIRECT"}]
-KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_MAX_CTAS", "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER")
+KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_MAX_CTAS", "NCCL_BUFFSIZE", "NCCL_LL_BUFFSIZE", "NCCL_LL128_BUFFSIZE",
+         "NCCL_AMD_REF_ORDER")
+# the protocol a ring fixture's partition belongs to: its NCCL_PROTO value and buffer-size variable
+RING_PROTO = {"simple": ("Simple", "NCCL_BUFFSIZE"), "ll": ("LL", "NCCL_LL_BUFFSIZE"),
+              "ll128": ("LL128", "NCCL_LL128_BUFFSIZE")}
 
 
 def _fixtures(n):
@@ -34,10 +38,17 @@ def _fixtures(n):
 
 def _ring_settings(z):
     """NCCL_ALGO=RING fixtures (the reference's full-size ring partition) run on communicators of the fixture's
-    channel count and NCCL_BUFFSIZE only: the ring kernel, and the direct kernel on the same partition
-    (NCCL_AMD_REF_ORDER=1)."""
-    common = {"NCCL_MAX_CTAS": str(int(z["nchannels"])), "NCCL_BUFFSIZE": str(int(z["buffsize"]))}
-    return [dict(common, NCCL_ALGO="RING", NCCL_PROTO="Simple"), dict(common, NCCL_AMD_REF_ORDER="1")]
+    channel count and protocol buffer size only. Simple-partition fixtures: the ring kernel, and the direct
+    kernel on the same partition (NCCL_AMD_REF_ORDER=1). LL / LL128-partition fixtures: the direct kernel on that
+    protocol's partition (NCCL_AMD_REF_ORDER=1 with NCCL_PROTO naming the protocol)."""
+    proto, var = RING_PROTO[str(z["proto"]) if "proto" in z else "simple"]
+    common = {"NCCL_MAX_CTAS": str(int(z["nchannels"]))}
+    if int(z["buffsize"]):
+        common[var] = str(int(z["buffsize"]))
+    ref = dict(common, NCCL_AMD_REF_ORDER="1", NCCL_PROTO=proto)
+    if proto != "Simple":
+        return [ref]
+    return [dict(common, NCCL_ALGO="RING", NCCL_PROTO="Simple"), ref]
 
 
 def _worker(rank, n, uids, q):
@@ -94,7 +105,7 @@ def test_golden_fixtures(built, n):
     import torch
     assert torch.cuda.is_available(), "GPU test on a box without a GPU"
     import nccl_amd
-    nring = 2 * sum(str(z["coll"]) == "allreduce_ring" for _, z in _fixtures(n))
+    nring = sum(len(_ring_settings(z)) for _, z in _fixtures(n) if str(z["coll"]) == "allreduce_ring")
     uids = [nccl_amd.get_unique_id() for _ in range(len(SETTINGS) + nring)]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -60,6 +60,9 @@ def _golden_files():
     return sorted(f for f in os.listdir(GOLDEN) if f.endswith(".npz"))
 
 
+PROTOS = {"ll": oracle.PROTO_LL, "ll128": oracle.PROTO_LL128, "simple": oracle.PROTO_SIMPLE}
+
+
 @pytest.mark.parametrize("fname", _golden_files())
 def test_oracle_matches_golden(built, fname):
     z = np.load(os.path.join(GOLDEN, fname), allow_pickle=False)
@@ -69,7 +72,8 @@ def test_oracle_matches_golden(built, fname):
         got = [oracle.all_reduce(ins, dtype, op)]
         want = [z["out"]]
     elif coll == "allreduce_ring":  # NCCL_ALGO=RING at full size: the reference's channel parts and loops
-        got = [oracle.all_reduce_ring_nccl(ins, dtype, op, int(z["nchannels"]), int(z["buffsize"]))]
+        proto = PROTOS[str(z["proto"])] if "proto" in z.files else oracle.PROTO_SIMPLE
+        got = [oracle.all_reduce_ring_nccl(ins, dtype, op, int(z["nchannels"]), int(z["buffsize"]), proto)]
         want = [z["out"]]
     elif coll == "reducescatter":
         got = oracle.reduce_scatter(ins, dtype, op)
@@ -147,9 +151,10 @@ def test_cpu_baseline_equals_oracle(built):
 
 
 def test_ring_partition_matches_golden_restatement(built):
-    """The C oracle's RING/SIMPLE partition (oracle_ring_nccl_plan) against the independent numpy restatement of
-    tests/golden/make_golden.py over a sweep of sizes, types, rank and channel counts and NCCL_BUFFSIZE values;
-    the parts tile [0, count) and every plan uses at most the communicator's channels."""
+    """The C oracle's RING partition (oracle_ring_nccl_plan_proto) against the independent numpy restatement of
+    tests/golden/make_golden.py over a sweep of sizes, types, rank and channel counts, protocols (Simple, LL,
+    LL128) and protocol buffer sizes; the parts tile [0, count) and every plan uses at most the communicator's
+    channels."""
     import importlib.util
     spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
     mg = importlib.util.module_from_spec(spec)
@@ -159,11 +164,20 @@ def test_ring_partition_matches_golden_restatement(built):
     for count in counts:
         for es in (1, 2, 4, 8):
             for n, k in ((2, 1), (2, 256), (3, 7), (8, 32), (8, 64), (4, 2), (5, 3)):
-                for buff in (0, 16384, 1 << 20):
-                    nch, lo, mid, hi, chunk = oracle.ring_nccl_plan(count, es, n, k, buff)
-                    parts, ck = mg.ring_parts(count, es, n, k, buff or (4 << 20))
-                    assert [lo] + [mid] * (nch - 2) + ([hi] if nch > 1 else []) == parts, (count, es, n, k, buff)
-                    assert ck == chunk and 1 <= nch <= k and sum(parts) == count and min(parts) > 0
+                for proto, buffs in (("simple", (0, 16384, 1 << 20)), ("ll", (0, 4096, 65536)),
+                                     ("ll128", (0, 32768, 1 << 20))):
+                    for buff in buffs:
+                        nch, lo, mid, hi, chunk = oracle.ring_nccl_plan(count, es, n, k, buff, PROTOS[proto])
+                        parts, ck = mg.ring_parts(count, es, n, k, buff, proto)
+                        assert [lo] + [mid] * (nch - 2) + ([hi] if nch > 1 else []) == parts, (count, es, n, k, buff,
+                                                                                               proto)
+                        assert ck == chunk and 1 <= nch <= k and sum(parts) == count and min(parts) > 0
+    # protocol-specific constants: LL's 4 KiB cells and 32 KiB chunk, LL128's 576000-byte chunk (1920-byte grains)
+    assert oracle.ring_nccl_plan(4096, 4, 2, 1, 0, oracle.PROTO_LL)[4] * 4 == 32768
+    assert oracle.ring_nccl_plan(4096, 4, 2, 1, 0, oracle.PROTO_LL128)[4] * 4 == 576000
+    assert oracle.ring_nccl_plan(1 << 20, 4, 2, 64, 0, oracle.PROTO_LL)[1] % 1024 == 0
+    with pytest.raises(ValueError):  # a chunk below one grain never advances
+        oracle.ring_nccl_plan(4096, 4, 2, 1, 1024, oracle.PROTO_LL128)
 
 
 def test_ring_order_is_the_one_loop_order_when_one_loop(built):

@@ -271,6 +271,25 @@ def test_reference_order_direct_allreduce(exe, built):
         assert p["algo"] == "direct", p
         assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (n, dt, count, k, buff, p)
         assert 0 < p["slice"] <= p["chunk"]
+    # NCCL_PROTO naming LL or LL128 alone: that protocol's ring partition (its cells, channel shrink and chunk, with
+    # NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE), still on the direct kernel (no LL kernel in this mode)
+    import numpy as np
+    rng = np.random.default_rng(11)
+    counts = [1, 1000, 100_003, 1 << 22] + [int(x) for x in rng.integers(1, 1 << 25, 6)]
+    for proto, var, pid, buffs in (("LL", "NCCL_LL_BUFFSIZE", oracle.PROTO_LL, (None, 4096, 65536)),
+                                   ("LL128", "NCCL_LL128_BUFFSIZE", oracle.PROTO_LL128, (None, 32768)),
+                                   ("^LL,LL128", "NCCL_BUFFSIZE", oracle.PROTO_SIMPLE, (None, 16384))):
+        for count in counts:
+            for n, dt, k in ((2, 7, 256), (3, 6, 7), (8, 9, 32), (4, 0, 1)):
+                for buff in buffs:
+                    env = {"NCCL_AMD_REF_ORDER": 1, "NCCL_PROTO": proto}
+                    if buff:
+                        env[var] = buff
+                    p = plan(exe, n, "ar", dt, count, chancap=k, **env)
+                    want = oracle.ring_nccl_plan(count, SIZES[dt], n, k, buff or 0, pid)
+                    assert p["algo"] == "direct", (proto, p)
+                    assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (proto, count, n, dt, k, buff, p)
+                    assert 0 < p["slice"] <= p["chunk"]
     assert plan(exe, 8, "rs", 7, 8 << 20, NCCL_AMD_REF_ORDER=1)["cbdlo"] == 0
     assert plan(exe, 2, "ar", 7, 1000, NCCL_AMD_REF_ORDER=1, NCCL_ALGO="TREE")["algo"] == "chain"
     # ref-order AllReduces launch alone (never batched)
