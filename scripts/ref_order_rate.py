@@ -19,12 +19,15 @@ def main():
     mib = int(sys.argv[1]) if len(sys.argv) > 1 else 256
     iters = int(sys.argv[2]) if len(sys.argv) > 2 else 10
     torch.cuda.set_device(0)
-    for n in (2, 4):
+    for n in [int(x) for x in os.environ.get("NS", "2,4").split(",")]:
         for dt, tdt, es in ((7, torch.float32, 4), (9, torch.bfloat16, 2)):
             count = (mib << 20) // es
             bufs = [(torch.empty(count, dtype=tdt, device="cuda").uniform_(-1, 1), torch.empty(count, dtype=tdt, device="cuda"))
                     for _ in range(n)]
-            for mode, env in MODES.items():
+            order = list(MODES.items())
+            if os.environ.get("REVERSE"):
+                order.reverse()
+            for mode, env in order:
                 for k in ("NCCL_AMD_REF_ORDER", "NCCL_MAX_CTAS", "NCCL_ALGO"):
                     os.environ.pop(k, None)
                 os.environ.update(env)
