@@ -487,6 +487,9 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   const bool refOrder = comm->tune.refOrder && info.func == FUNC_ALLREDUCE && comm->tune.algo != FORCE_RING &&
                         comm->tune.algo != FORCE_TREE;
   if (refOrder) oneShot = false;
+  // NCCL_ALGO=RING with NCCL_PROTO naming LL or LL128 alone: the reference's RING/LL or RING/LL128 AllReduce, i.e.
+  // the ring kernel on that protocol's partition (ringParts), not this engine's LL kernel (another fold order)
+  const bool ringProtoPart = info.func == FUNC_ALLREDUCE && comm->tune.algo == FORCE_RING && comm->tune.refProto != 2;
   int tunedNch = 0;
   if (comm->tunerLoaded) {  // external tuner plugin: one-shot (TREE/SIMPLE) vs direct (RING/SIMPLE), channels
     int tuned = TUNE_DEFAULT;
@@ -498,7 +501,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   const bool oneShotAR = oneShot;
   // LL protocol (reference NCCL_PROTO=LL, prims_ll.h): small AllReduce / ReduceScatter / AllGather /
   // Reduce, one launch, no fences
-  if (!refOrder && llPlan(info, &p.ll.ops[0])) {
+  if (!refOrder && !ringProtoPart && llPlan(info, &p.ll.ops[0])) {
     p.algo = ALGO_LL;
     p.ll.comm = comm->devComm;
     p.ll.redArg = p.args.redArg;
@@ -540,12 +543,12 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       const size_t span = chain ? count * ts : blockElems * ts;
       planChannels(comm, span, ts, p, (size_t)comm->tune.minChannelBytes, comm->chanCap);
       if (kind == PIPE_RING_AR) {  // the reference's channel parts and loop chunk (ringParts above)
-        const RingParts r = ringParts(count, ts, comm->chanCap, n, 2);
+        const RingParts r = ringParts(count, ts, comm->chanCap, n, comm->tune.refProto);
         p.nChannels = r.nch;
         p.args.cbdLo = r.lo;
         p.args.part = r.mid;
         p.args.cbdHi = r.hi;
-        p.args.chunk = (uint64_t)comm->tune.ringChunkBytes / ts;
+        p.args.chunk = (uint64_t)comm->tune.refChunkBytes / ts;
         p.args.slice = std::min<uint64_t>(p.args.chunk, comm->slotBytes / ts / epp * epp);
         p.args.nSteps = 0;  // per channel and loop (pipe.h)
       }

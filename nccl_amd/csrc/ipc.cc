@@ -275,6 +275,11 @@ ncclResult_t ipcServerStart(ncclComm* comm) {
     delete s;
     return ncclSystemError;
   }
+  // the server thread's first runtime call must not be the one that initialises the HIP runtime: that init
+  // may set environment variables while other threads read theirs (getenv vs setenv), so it happens here first
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipGetLastError();
   s->thread = std::thread(serverLoop, s);
   comm->fdServer = s;
   TRACE("rank %d: fd server %s", comm->rank, s->name);

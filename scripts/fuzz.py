@@ -28,8 +28,8 @@ def settings(rng):
         env["NCCL_PROTO"] = rng.choice(["LL", "^LL", "Simple", "LL,Simple", "LL128", "LL,LL128", "LL128,Simple"])
     if rng.random() < 0.3:
         env["NCCL_ALGO"] = rng.choice(["ONESHOT", "DIRECT", "RING"])
-        if env["NCCL_ALGO"] == "RING" and env.get("NCCL_PROTO") in ("LL", "LL128", "LL,LL128"):
-            env["NCCL_PROTO"] = "LL,Simple"  # the ring is a Simple-protocol kernel (tests/gpu_cases.py ring_runs)
+        if env["NCCL_ALGO"] == "RING" and env.get("NCCL_PROTO") == "LL,LL128":
+            env["NCCL_PROTO"] = "LL,Simple"  # LL kernel / ring split by capacity (tests/gpu_cases.py ring_runs)
     if rng.random() < 0.4:
         env["NCCL_AMD_SLOT_BYTES"] = str(rng.choice([4096, 8192, 16384, 65536]))
     if rng.random() < 0.3:

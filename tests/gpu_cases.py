@@ -63,16 +63,17 @@ def ring_channels(n: int, ranks_per_gpu: int | None = None) -> int:
 
 def ring_runs(n: int) -> bool:
     """Whether NCCL_ALGO=RING (from the environment the communicator was created under) runs the ring kernel for
-    an AllReduce: two staging slots are needed (enqueue.cc planColl). With only LL-class protocols enabled the LL
-    kernel takes what fits its line area and the ring the rest, a size rule this helper does not restate: the
-    tests never combine NCCL_ALGO=RING with an NCCL_PROTO that excludes Simple (ValueError)."""
+    an AllReduce: two staging slots are needed (enqueue.cc planColl). NCCL_PROTO naming LL or LL128 alone runs the
+    ring on that protocol's partition (ref_proto); with several LL-class protocols and no Simple the LL kernel
+    takes what fits its line area and the ring the rest, a size rule this helper does not restate: the tests
+    never use that combination with NCCL_ALGO=RING (ValueError)."""
     if os.environ.get("NCCL_ALGO", "").upper() != "RING" or n < 2:
         return False
     proto = os.environ.get("NCCL_PROTO", "")
     if proto:
         toks = {t.strip().lower() for t in proto.lstrip("^").split(",")}
         simple = ("simple" not in toks) if proto.startswith("^") else ("simple" in toks)
-        if not simple:
+        if not simple and ref_proto()[0] == oracle.PROTO_SIMPLE:
             raise ValueError(f"NCCL_ALGO=RING with NCCL_PROTO={proto}: the AllReduce order depends on the LL capacity")
     return _env_int("NCCL_AMD_NSLOTS", 2) >= 2
 
@@ -112,9 +113,7 @@ def expected(coll: str, inputs, dtype: int, op: int, root: int = 0, algo: str = 
         algo = algo or os.environ.get("NCCL_ALGO", "").upper()
         if algo == "TREE":
             out = oracle.all_reduce_chain(inputs, dtype, op)
-        elif algo == "RING" and ring_runs(n):
-            out = oracle.all_reduce_ring_nccl(inputs, dtype, op, ring_channels(n), _env_int("NCCL_BUFFSIZE", 0))
-        elif ref_order_runs(n):
+        elif (algo == "RING" and ring_runs(n)) or ref_order_runs(n):
             proto, buff = ref_proto()
             out = oracle.all_reduce_ring_nccl(inputs, dtype, op, ring_channels(n), buff, proto)
         else:

@@ -106,6 +106,7 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             # ... on the reference's RING/LL and RING/LL128 partitions (small protocol buffers: many parts and loops)
             (3, {"NCCL_AMD_REF_ORDER": "1", "NCCL_PROTO": "LL", "NCCL_LL_BUFFSIZE": "65536", "NCCL_MAX_CTAS": "6"}),
             (2, {"NCCL_AMD_REF_ORDER": "1", "NCCL_PROTO": "LL128", "NCCL_LL128_BUFFSIZE": "131072"}),
+            (3, {"NCCL_ALGO": "RING", "NCCL_PROTO": "LL", "NCCL_LL_BUFFSIZE": "65536", "NCCL_MAX_CTAS": "4"}),
             # cross-process memory: every dma-buf import refused -> the hipIpc handle fallback (ipc.cc); legacy
             # handles only (NCCL_AMD_IPC=legacy) run where the runtime is 7.2+, see test_legacy_ipc_runtime_gate
             (3, {"NCCL_AMD_IPC_FAIL_DMABUF": "1"}),

@@ -38,17 +38,13 @@ def _fixtures(n):
 
 def _ring_settings(z):
     """NCCL_ALGO=RING fixtures (the reference's full-size ring partition) run on communicators of the fixture's
-    channel count and protocol buffer size only. Simple-partition fixtures: the ring kernel, and the direct
-    kernel on the same partition (NCCL_AMD_REF_ORDER=1). LL / LL128-partition fixtures: the direct kernel on that
-    protocol's partition (NCCL_AMD_REF_ORDER=1 with NCCL_PROTO naming the protocol)."""
+    channel count and protocol buffer size only, with NCCL_PROTO naming the fixture's protocol: the ring kernel
+    (NCCL_ALGO=RING) and the direct kernel on the same partition (NCCL_AMD_REF_ORDER=1)."""
     proto, var = RING_PROTO[str(z["proto"]) if "proto" in z else "simple"]
     common = {"NCCL_MAX_CTAS": str(int(z["nchannels"]))}
     if int(z["buffsize"]):
         common[var] = str(int(z["buffsize"]))
-    ref = dict(common, NCCL_AMD_REF_ORDER="1", NCCL_PROTO=proto)
-    if proto != "Simple":
-        return [ref]
-    return [dict(common, NCCL_ALGO="RING", NCCL_PROTO="Simple"), ref]
+    return [dict(common, NCCL_ALGO="RING", NCCL_PROTO=proto), dict(common, NCCL_AMD_REF_ORDER="1", NCCL_PROTO=proto)]
 
 
 def _worker(rank, n, uids, q):

@@ -290,6 +290,14 @@ def test_reference_order_direct_allreduce(exe, built):
                     assert p["algo"] == "direct", (proto, p)
                     assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (proto, count, n, dt, k, buff, p)
                     assert 0 < p["slice"] <= p["chunk"]
+    # NCCL_ALGO=RING with LL or LL128 alone: the ring kernel on that protocol's partition (no LL kernel)
+    for proto, pid in (("LL", oracle.PROTO_LL), ("LL128", oracle.PROTO_LL128)):
+        for count in (1, 1000, 100_003, 1 << 22):
+            p = plan(exe, 3, "ar", 7, count, chancap=7, NCCL_ALGO="RING", NCCL_PROTO=proto)
+            assert p["algo"] == "ring", (proto, p)
+            assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == \
+                oracle.ring_nccl_plan(count, 4, 3, 7, 0, pid), (proto, count, p)
+    assert plan(exe, 3, "ar", 7, 1000, NCCL_ALGO="RING", NCCL_PROTO="LL,LL128")["algo"] == "ll"
     assert plan(exe, 8, "rs", 7, 8 << 20, NCCL_AMD_REF_ORDER=1)["cbdlo"] == 0
     assert plan(exe, 2, "ar", 7, 1000, NCCL_AMD_REF_ORDER=1, NCCL_ALGO="TREE")["algo"] == "chain"
     # ref-order AllReduces launch alone (never batched)
