@@ -183,10 +183,12 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     cols = {"ll": {"NCCL_PROTO": "LL"}, "ll128": {"NCCL_PROTO": "LL128"},
             "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
             "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
-            "ring": {"NCCL_ALGO": "RING"}, "tree": {"NCCL_ALGO": "TREE"}, "default": {}}
+            "ring": {"NCCL_ALGO": "RING"}, "tree": {"NCCL_ALGO": "TREE"}, "default": {},
+            # the reference's RING/SIMPLE partition walked by the direct kernel: its cost vs default
+            "reforder": {"NCCL_AMD_REF_ORDER": "1"}}
     limits = {"ll": 512 * 1024, "ll128": 896 * 1024, "oneshot": 64 * MIB}
     rows = {}
-    saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION")}
+    saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION", "NCCL_AMD_REF_ORDER")}
     for name, env in cols.items():  # ll128: the LL64-line protocol (64-byte lines)
         for k in saved:
             os.environ.pop(k, None)
