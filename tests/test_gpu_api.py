@@ -197,6 +197,71 @@ def test_hipgraph_mixed_sequence(two_comms):
                     assert np.array_equal(ys[r][j].cpu().numpy(), want[r]), f"replay {it} op {j} ({k}) rank {r}"
 
 
+REF_GRAPH_ENVS = [
+    {"NCCL_AMD_REF_ORDER": "1", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "6"},
+    {"NCCL_ALGO": "RING", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "6"},
+    {"NCCL_AMD_REF_ORDER": "1", "NCCL_PROTO": "LL", "NCCL_LL_BUFFSIZE": "65536", "NCCL_MAX_CTAS": "6"},
+]
+
+
+@pytest.mark.parametrize("env", REF_GRAPH_ENVS, ids=["reforder", "ring", "reforder-ll"])
+def test_hipgraph_reference_order_allreduce(built, env):
+    """The reference-partition AllReduces (NCCL_AMD_REF_ORDER's direct kernel, the ring) captured in one hipGraph per
+    rank — 3 ranks, bf16 (every hop rounds, so the fold order shows) at sizes spanning one and many channel parts
+    and loops — and replayed with fresh inputs: the per-channel loop geometry is recomputed by every launch and the
+    step counters continue across replays, bit-exact vs the reference's order every time."""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    keys = ("NCCL_AMD_REF_ORDER", "NCCL_BUFFSIZE", "NCCL_MAX_CTAS", "NCCL_ALGO", "NCCL_PROTO", "NCCL_LL_BUFFSIZE")
+    saved = {k: os.environ.get(k) for k in keys}
+    for k in keys:
+        os.environ.pop(k, None)
+    os.environ.update(env)
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    n, counts, dt = 3, (3000, 100_003, 1 << 20), 9
+    comms = []
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        comms = nccl_amd.Communicator.init_all([0] * n)
+        streams = [nccl_amd.dedicated_stream(0) for _ in range(n)]
+        bufs = [[(G.to_device(np.zeros(c, np.uint16), dev)[1], G.to_device(np.zeros(c, np.uint16), dev)[1])
+                 for c in counts] for _ in range(n)]
+        graphs = [torch.cuda.CUDAGraph() for _ in range(n)]
+        torch.cuda.synchronize()
+        for r in range(n):
+            with torch.cuda.graph(graphs[r], stream=streams[r]):
+                for c, (x, y) in zip(counts, bufs[r]):
+                    comms[r].all_reduce_raw(x.data_ptr(), y.data_ptr(), c, dt, 0, streams[r].cuda_stream)
+        for it in range(3):
+            ins = [G.make_inputs(n, dt, c, seed=700 + 10 * it + j) for j, c in enumerate(counts)]
+            for r in range(n):
+                for j, (x, _) in enumerate(bufs[r]):
+                    x.copy_(torch.from_numpy(ins[j][r].view(np.uint8).copy()))
+            torch.cuda.synchronize()
+            for r in range(n):
+                with torch.cuda.stream(streams[r]):
+                    graphs[r].replay()
+            torch.cuda.synchronize()
+            assert all(c.async_error() == 0 for c in comms)
+            for j, c in enumerate(counts):
+                want = G.expected("allreduce", ins[j], dt, 0)[0]
+                assert not np.array_equal(want, G.oracle.all_reduce(ins[j], dt, 0)) or c == 3000, \
+                    "inputs do not tell the reference order from the one-loop order"
+                for r in range(n):
+                    got = G.from_device(bufs[r][j][1], np.uint16)
+                    assert G.same_bits(got, want, dt), f"{env} replay {it} count {c} rank {r}"
+    finally:
+        for cm in comms:
+            if cm.ptr:
+                cm.destroy()
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+
+
 def test_init_rank_in_group_single_thread(built):
     import torch
     import nccl_amd
