@@ -38,10 +38,11 @@ $(BUILD)/%.o: $(SRCDIR)/%.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -Rpass-analysis=kernel-resource-usage -c $< -o $@ 2> $(BUILD)/$*.usage; \
 	  st=$$?; grep -E "warning|error" $(BUILD)/$*.usage >&2; exit $$st
 
-$(LIBDIR)/libnccl.so: $(HOSTOBJ) $(DEVOBJ)
+# -Wl,--version-script: export exactly nccl* / pnccl* (reference src/libnccl.map:13-19)
+$(LIBDIR)/libnccl.so: $(HOSTOBJ) $(DEVOBJ) $(SRCDIR)/libnccl.map
 	@mkdir -p $(LIBDIR)
 	$(HIPCC) -shared -fPIC --offload-arch=$(ARCH) -Wl,-soname,libnccl.so.2 -Wl,-Bsymbolic \
-	  -o $@ $^ -lpthread -ldl
+	  -Wl,--version-script=$(SRCDIR)/libnccl.map -o $@ $(HOSTOBJ) $(DEVOBJ) -lpthread -ldl
 	ln -sf libnccl.so $(LIBDIR)/libnccl.so.2
 
 oracle: oracle/_build/liboracle.so

@@ -10,9 +10,11 @@ Workload (BASELINE.json metric: 256 MiB fp32 at 1/2/4/8 GPUs):
   N == 1: 256 MiB fp32, world_size 1 (the reference's nranks==1 out-of-place copy,
           src/device/onerank.cu:52-56). busBW is 0 by definition at n=1, so `value` is the HBM rate
           2*S/t (read S + write S), as BASELINE.md §2 prescribes; configs[0] (64 MiB) is reported beside.
-  N >= 2: the metric's 256 MiB fp32 per rank (configs[1] at N=2). `value` = whole-job bus bytes / time
-          = N * busBW, busBW = algBW * 2(n-1)/n (reference plugins/profiler/inspector/inspector.cc:1450-1492).
-          Per-rank busBW (the nccl-tests figure) is printed as `busbw_GBps`.
+  N >= 2: the metric's 256 MiB fp32 per rank (configs[1] at N=2). `value` = busBW, the metric's own figure:
+          algBW * 2(n-1)/n with algBW = S / t (reference plugins/profiler/inspector/inspector.cc:1450-1492, the
+          nccl-tests number; t is the max over ranks, so it is the slowest rank's). It equals `busbw_GBps`, and
+          `roofline.frac` is this figure (per launch) over the link peak. The whole-job sum N * busBW is printed
+          beside it as `busbw_sum_GBps`.
 Harness collectives (unique-id broadcast, barrier, max-over-ranks) use torch.distributed over gloo;
 the measured AllReduce is this repo's libnccl.so (no RCCL anywhere on the data path).
 """
@@ -71,10 +73,11 @@ def max_over_ranks(dist, values):
 
 
 def rates(n: int, S: int, ms_per_step: float):
-    """(value, algBW, busBW) in GB/s for one AllReduce of S bytes per rank taking ms_per_step."""
+    """(value, algBW, busBW) in GB/s for one AllReduce of S bytes per rank taking ms_per_step. value = busBW at
+    n >= 2 (the metric, inspector.cc:1450-1492); at n = 1 busBW is 0 by definition, so value = the HBM rate 2S/t."""
     algbw = S / (ms_per_step * 1e-3) / 1e9
     busbw = algbw * bus_factor("allreduce", n)
-    value = 2 * S / (ms_per_step * 1e-3) / 1e9 if n == 1 else n * busbw
+    value = 2 * S / (ms_per_step * 1e-3) / 1e9 if n == 1 else busbw
     return value, algbw, busbw
 
 
@@ -775,8 +778,11 @@ def main(argv=None):
             "data": "synthetic: uniform[-1,1) fp32 per rank generated on device (torch RNG)",
             "config": {"workload": workload, "collective": "ncclAllReduce", "op": "sum", "bytes_per_rank": S,
                        "count": count, "n_ranks": n, "out_of_place": True,
-                       "value_definition": "HBM GB/s = 2S/t (n=1)" if n == 1 else "N x busBW (whole job)"},
+                       "value_definition": ("HBM GB/s = 2S/t (n=1: busBW = algBW x 2(n-1)/n is 0 by definition)"
+                                            if n == 1 else "busBW = S/t x 2(n-1)/n, t = slowest rank (inspector.cc:"
+                                            "1450-1492, the nccl-tests figure); busbw_sum_GBps = N x busBW")},
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
+            **({"busbw_sum_GBps": round(n * busbw, 2)} if n > 1 else {}),
             "roofline": roof, "cpu_baseline": cpu, "check": "pass" if ok else "FAIL", **extra,
         }
 

@@ -122,9 +122,10 @@ struct IpcImport {  // one mapping of a peer's allocation in this process
 };
 struct FdServer;
 bool ipcLegacy();
-// Release peers' mappings whose owner deregistered them (ipc.cc): called on the caller's thread at library entry
-// points (not inside a stream capture of `stream`); a no-op unless a RELEASE request arrived.
-void ipcDrainReleases(hipStream_t stream);
+const char* ipcServerName(const ncclComm* comm);  // "" without an fd server
+// Release peers' mappings whose owner deregistered them (ipc.cc): called on the caller's thread at the blocking entry
+// points only (init, finalize, destroy, (de)registration), never in a collective; a no-op unless a RELEASE arrived.
+void ipcDrainReleases();
 // Held around this library's device allocations, imports and releases (ipc.cc gMapMu): no allocation of ours can
 // interleave with a mapping being torn down on another thread (a non-blocking init runs on its own thread).
 std::mutex& ipcMapMutex();
@@ -162,6 +163,9 @@ struct PeerInfo {  // exchanged once at init (reference: struct ncclPeerInfo, sr
   IpcDesc flagsDesc;
   uint64_t stagingPtr;  // raw pointers, valid only inside the same process
   uint64_t flagsPtr;
+  // this rank's fd server (ipc.cc), published on its own: a slab exported by the hipIpc fallback carries no server
+  // name in its descriptor, yet the server still maps peers' registered buffers (register.cc)
+  char fdServer[40];
 };
 
 struct UserRedOp {  // ncclRedOpCreatePreMulSum state (reference src/enqueue.cc:2560-2576)
@@ -306,6 +310,9 @@ struct ncclComm {
   std::thread initThread;  // non-blocking ncclCommInitRankConfig (config.blocking = 0)
   uint64_t opCount = 0;
   uint32_t warnedAlgo = 0;  // NCCL_ALGO forced but unavailable for a collective: warned once per CollFunc
+  // every rank can map every other-process peer's registered buffers (each such peer runs an fd server): derived
+  // from the shared peer table at init, so every rank takes the same registered / staged decision (register.cc)
+  bool regIpcAll = false;
   uint64_t endMagic;
 };
 
@@ -407,7 +414,8 @@ ncclWindow_vidmem* findSymWindow(ncclComm* comm, const void* p, size_t bytes);
 // buffers as mapped in rank r's process (mine: the buffers themselves).
 bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
                size_t recvBytes, const char** rmtSend, char** rmtRecv);
-void windowsFree(ncclComm* comm);  // release every window and IPC mapping (destroy/abort)
+// release every window and IPC mapping (destroy: also asks peers to unmap this rank's registrations; abort: not)
+void windowsFree(ncclComm* comm, bool notifyPeers);
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
 ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);
 ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int variant, int64_t gridCap);

@@ -64,7 +64,9 @@ enum PipeKind { PIPE_RING_AR = 0, PIPE_RING_RS = 1, PIPE_RING_AG = 2, PIPE_CHAIN
 enum DevRedOp { DEV_SUM = 0, DEV_PROD = 1, DEV_MINMAX = 2, DEV_PREMULSUM = 3, DEV_SUMPOSTDIV = 4, DEV_NUMOPS = 5 };
 
 // Error codes written by a kernel into the host-visible error word.
-enum DevError { DERR_NONE = 0, DERR_TIMEOUT = 1, DERR_ABORT = 2 };
+// DERR_MISMATCH: a peer ran another kernel kind for the same collective (registered zero-copy vs staged; the
+// wait probe in kernels.h waitAll), reported instead of waiting for the spin timeout.
+enum DevError { DERR_NONE = 0, DERR_TIMEOUT = 1, DERR_ABORT = 2, DERR_MISMATCH = 3 };
 
 struct DevComm {
   int rank;

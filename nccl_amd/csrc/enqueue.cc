@@ -813,7 +813,8 @@ ncclResult_t enqueueCheck(CollInfo* info) {
     groupRecordError(ret);
     return ret;
   }
-  ipcDrainReleases(info->stream);  // peers' deregistered buffers, released on this thread (ipc.cc)
+  // (no ipcDrainReleases here: unmapping a peer's deregistered buffer is a device-synchronising hipFree, and a
+  // collective must return once its work is enqueued, nccl.h.in:431-442; the blocking entry points drain, ipc.cc)
   ret = argsCheck(info);
   if (ret == ncclSuccess && info->comm->asyncResult.load() != ncclSuccess) {
     WARN("%s: communicator is in error state %d", info->opName, info->comm->asyncResult.load());

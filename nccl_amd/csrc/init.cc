@@ -156,6 +156,12 @@ static void computeChannelCap(ncclComm* c) {
   bool oneDevice = true;
   for (size_t i = 1; i < c->peers.size(); i++) oneDevice = oneDevice && !strcmp(c->peers[i].busId, c->peers[0].busId);
   resolveFence(&c->tune, oneDevice);
+  // registered buffers map into every other-process peer through that peer's fd server: usable by every rank
+  // only if every such peer runs one — one comm-wide answer from the shared table (register.cc regCreate)
+  c->regIpcAll = true;
+  for (size_t i = 0; i < c->peers.size(); i++)
+    for (size_t j = 0; j < c->peers.size(); j++)
+      if (c->peers[i].pid != c->peers[j].pid && c->peers[j].fdServer[0] == 0) c->regIpcAll = false;
 }
 
 // Which HIP runtime this process bound (reference: init-time INFO lines, src/init.cc:1831-1968): in a torch
@@ -302,7 +308,7 @@ static ncclResult_t initRankCommon(ncclComm_t* newcomm, int nranks, ncclUniqueId
     return ncclInvalidArgument;
   }
   NCCLCHECK(checkConfig(config));
-  ipcDrainReleases(nullptr);
+  ipcDrainReleases();
   int dev = 0;
   HIPCHECK(hipGetDevice(&dev));
   ncclConfig_t cfgCopy;
@@ -354,7 +360,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommInitRankScalable, ncclComm_t*, int, int, int, n
 NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int* devlist) {
   logInit();
   ROCTX_RANGE("ncclCommInitAll ndev=%d", ndev);
-  ipcDrainReleases(nullptr);
+  ipcDrainReleases();
   if (comms == nullptr) {
     WARN("CommInitAll : comms argument is NULL");
     return ncclInvalidArgument;
@@ -423,10 +429,13 @@ static void pollAsync(ncclComm* comm) {
   if (comm->hostError && __atomic_load_n(comm->hostError, __ATOMIC_ACQUIRE) != DERR_NONE) {
     uint32_t e = __atomic_load_n(comm->hostError, __ATOMIC_ACQUIRE);
     int cur = ncclSuccess;
-    ncclResult_t r = e == DERR_ABORT ? ncclRemoteError : ncclSystemError;
+    ncclResult_t r = e == DERR_ABORT ? ncclRemoteError : e == DERR_MISMATCH ? ncclInvalidUsage : ncclSystemError;
     if (comm->asyncResult.compare_exchange_strong(cur, r))
       WARN("rank %d: device-side %s in a collective kernel", comm->rank,
-           e == DERR_TIMEOUT ? "spin timeout (peer never arrived)" : "abort");
+           e == DERR_TIMEOUT    ? "spin timeout (peer never arrived)"
+           : e == DERR_MISMATCH ? "kernel mismatch (a peer ran the other kernel for this collective: its buffers "
+                                  "are registered on some ranks only, e.g. a registration that failed on one rank)"
+                                : "abort");
   }
 }
 
@@ -436,16 +445,17 @@ NCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
   DeviceRestore restore;
   HIPCHECK(hipSetDevice(comm->device));
   HIPCHECK(hipDeviceSynchronize());
+  ipcDrainReleases();  // a blocking entry point: peers' deregistered buffers are unmapped here (ipc.cc)
   if (comm->bootstrap) NCCLCHECK(bootstrapBarrier(comm->bootstrap));
   comm->finalized = true;
   return ncclSuccess;
 }
 NCCL_ALIAS(ncclResult_t, ncclCommFinalize, ncclComm_t)
 
-static ncclResult_t commFree(ncclComm* comm) {
+static ncclResult_t commFree(ncclComm* comm, bool notifyPeers) {
   if (comm->initThread.joinable()) comm->initThread.join();  // a non-blocking init still running
   tunerUnload(comm);
-  windowsFree(comm);
+  windowsFree(comm, notifyPeers);
   if (comm->internalStream) (void)hipStreamDestroy(comm->internalStream);
   if (comm->evIn) (void)hipEventDestroy(comm->evIn);
   if (comm->evOut) (void)hipEventDestroy(comm->evOut);
@@ -460,7 +470,7 @@ static ncclResult_t commFree(ncclComm* comm) {
 NCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   if (comm == nullptr) return ncclSuccess;  // reference: destroying NULL is a no-op
   NCCLCHECK(commCheck(comm, "ncclCommDestroy", "comm"));
-  ipcDrainReleases(nullptr);
+  ipcDrainReleases();
   int old = 0;
   (void)hipGetDevice(&old);
   if (comm->initThread.joinable()) comm->initThread.join();
@@ -471,7 +481,7 @@ NCCL_EXPORT ncclResult_t ncclCommDestroy(ncclComm_t comm) {
   // clique in turn (the reference's single-process pattern).
   (void)hipDeviceSynchronize();
   if (!comm->finalized) (void)transportDrainCredits(comm);
-  commFree(comm);
+  commFree(comm, true);
   (void)hipSetDevice(old);
   return ncclSuccess;
 }
@@ -486,7 +496,7 @@ NCCL_EXPORT ncclResult_t ncclCommAbort(ncclComm_t comm) {
   DeviceRestore restore;
   (void)hipSetDevice(comm->device);
   (void)hipDeviceSynchronize();
-  commFree(comm);
+  commFree(comm, false);
   return ncclSuccess;
 }
 NCCL_ALIAS(ncclResult_t, ncclCommAbort, ncclComm_t)

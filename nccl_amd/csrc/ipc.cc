@@ -52,15 +52,29 @@ struct FdServer {
 };
 
 // Releasing a mapping frees its address range and tears the interop mapping down in two runtime calls (hipFree,
-// hipDestroyExternalMemory). Round 3 released peers' registered buffers on a helper thread, concurrently with
-// whatever the caller's thread did next; bench.py's N = 4 rehearsal (a deregistration, then a new communicator
-// whose slab is allocated, exported and imported right away) then failed three runs out of three at that new
-// communicator — a refused dma-buf export, a spin timeout, an illegal access in its first collective — which is
-// what a fresh allocation landing in a range still being torn down would do. So mappings are released only on a
-// thread that is inside the library — the caller's, between its own runtime calls — and every release and
-// import of this library is serialized by gMapMu. Peers' registered buffers whose owner deregistered
-// them (RELEASE requests, served without blocking: the server never waits for the device) wait in gPending until
-// the next library call on any thread drains them (ipcDrainReleases), or until their communicator's server stops.
+// hipDestroyExternalMemory); hipFree also waits for the whole device.
+//
+// Round 3's fault (gpurun_out/rehearsal_n4_diag/bench_n4.log, bench.py --gpus 4 on one GPU): a helper ("reaper")
+// thread of each fd server released peers' deregistered buffers as soon as their RELEASE requests arrived,
+// concurrently with whatever the caller's thread did next. In the bench suite the "registered" part deregistered
+// its buffers and the next part ("staged_tuning default") created a new communicator at once: its slab was
+// allocated, exported and imported by the peers while the reapers were still in hipFree / hipDestroyExternalMemory
+// of the old mappings. All four ranks then reported an illegal memory access at the first synchronize after that
+// communicator's first collective (no record names the faulting kernel or address; the other two runs of the same
+// order failed with a refused dma-buf export and a spin timeout). What the three failures share is a runtime
+// allocation / import / export racing a teardown on another thread, which the fix (dea9ffb) removed: no helper
+// thread, every import and release of this library under gMapMu.
+//
+// What the mechanism guarantees since round 4:
+//  * the fd server never touches the device for a RELEASE: it moves the mapping to gPending and answers;
+//  * gPending is drained only on the caller's thread at entry points that may block by contract — CommInitRank /
+//    InitAll, Finalize, Destroy, (Window)Register and (Window)Deregister — never inside a collective (a collective
+//    returns once its work is enqueued, reference nccl.h.in:431-442; the reference unmaps on its proxy thread for
+//    the same reason, src/transport/p2p.cc:762-780), and never concurrently with this library's allocations or
+//    imports (gMapMu);
+//  * a mapping stays valid until drained, so a kernel of this rank still reading the peer's buffer never faults:
+//    the dma-buf import keeps the peer's memory referenced even after the peer freed it.
+// The cost is memory: a peer's deregistered buffer stays mapped here until this rank's next such entry point.
 static std::mutex gMapMu;
 std::mutex& ipcMapMutex() { return gMapMu; }
 struct PendingRelease {
@@ -77,14 +91,8 @@ static void releaseLater(int device, const IpcImport& m) {
   gHavePending.store(true, std::memory_order_release);
 }
 
-void ipcDrainReleases(hipStream_t stream) {
+void ipcDrainReleases() {
   if (!gHavePending.load(std::memory_order_acquire)) return;
-  if (stream) {  // never inside a capture (hipFree synchronizes): a later call drains them
-    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-    const hipError_t e = hipStreamIsCapturing(stream, &st);
-    (void)hipGetLastError();
-    if (e != hipSuccess || st != hipStreamCaptureStatusNone) return;
-  }
   std::vector<PendingRelease> batch;
   {
     std::lock_guard<std::mutex> g(gPendMu);
@@ -286,12 +294,14 @@ ncclResult_t ipcServerStart(ncclComm* comm) {
   return ncclSuccess;
 }
 
+const char* ipcServerName(const ncclComm* comm) { return comm->fdServer ? comm->fdServer->name : ""; }
+
 void ipcServerStop(ncclComm* comm) {
   FdServer* s = comm->fdServer;
   if (!s) return;
   if (s->wakePipe[1] >= 0) (void)!write(s->wakePipe[1], "x", 1);
   if (s->thread.joinable()) s->thread.join();
-  ipcDrainReleases(nullptr);  // what RELEASE requests queued (for any communicator of this process)
+  ipcDrainReleases();  // what RELEASE requests queued (for any communicator of this process)
   for (auto& kv : s->table) close(kv.second);
   if (!s->imports.empty()) (void)hipSetDevice(comm->device);
   for (auto& kv : s->imports) ipcRelease(&kv.second);  // peers' registrations still mapped here

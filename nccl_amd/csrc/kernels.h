@@ -151,11 +151,41 @@ struct ChanState {
 };
 
 
+// Kernel-kind mismatch probe. Every rank must run the same kernel for one collective; the staged and
+// the registered zero-copy kernels exchange different flags, so ranks that disagree (a registration that failed
+// on one rank only, e.g. under graph capture) would each wait for a signal the other never sends until the spin
+// timeout. A waiting lane whose peer has meanwhile posted a flag of the OTHER kernel kind on this channel beyond
+// what this rank has consumed has proof of the disagreement: while this rank is blocked in op k on channel c,
+// that peer cannot have finished op k on c (it needs this rank's signals of op k), so its newer flag of the other
+// kind belongs to op k itself. The wait's own flag is read again after the probe (the peer's op-k signals complete
+// before its next kernel starts), so a peer that merely moved on is never taken for a mismatch. Checked on the slow
+// path only (every 256 polls): no cost while flags arrive.
+//   staged kernels: peer's SYM_ENTER[c] > this channel's symmetric epoch (counters[c][CTR_SYM][0]);
+//   symmetric kernels (ENTER wait): peer's RS_READY / AG_READY / PULL_READY[c] > what this rank consumed.
+// PROBE_STAGED: flag[0] against `epoch` (one load per lane: staged kernels run at the 128-VGPR co-residency cap);
+// PROBE_SYM: flag[k] against seen[k][peer], k < 3.
+enum ProbeKind { PROBE_NONE = 0, PROBE_STAGED = 1, PROBE_SYM = 2 };
+struct WaitProbe {
+  const uint64_t* flag[3];  // the other kind's flag words of this channel, indexed by peer
+  const uint64_t* seen[3];  // per-peer counts this rank consumed (PROBE_SYM)
+  uint64_t epoch;           // this channel's symmetric epoch (PROBE_STAGED)
+};
+template <int PROBE>
+__device__ __forceinline__ bool probeMismatch(const WaitProbe& pr, int lane) {
+  if constexpr (PROBE == PROBE_STAGED) return loadFlag(pr.flag[0] + lane) > pr.epoch;
+  bool ev = false;
+#pragma unroll
+  for (int k = 0; k < 3; k++) ev |= loadFlag(pr.flag[k] + lane) > pr.seen[k][lane];
+  return ev;
+}
+
 // Wave 0 waits until every selected flag word reaches its target (target[r] == 0: no wait on r).
 // ACQ: follow with a system-scope acquire (needed before reading data the flags publish; not for
 // credit/ack words, which guard no data). All threads must call it (it ends in a barrier).
+// PROBE / probe: the kernel-kind mismatch probe above.
+template <int PROBE = PROBE_NONE>
 __device__ bool waitAll(const DevComm& dc, ChanState& st, const uint64_t* flagBase, const uint64_t* target,
-                        bool ACQ) {
+                        bool ACQ, const WaitProbe* probe = nullptr) {
   if (threadIdx.x < 64) {
     int lane = threadIdx.x;
     bool need = lane < dc.nRanks && target[lane] != 0;
@@ -168,8 +198,16 @@ __device__ bool waitAll(const DevComm& dc, ChanState& st, const uint64_t* flagBa
       __builtin_amdgcn_s_sleep(1);
       if ((++iter & 255) == 0) {
         bool bad = false;
+        bool mismatch = false;
+        if (PROBE != PROBE_NONE && need && probeMismatch<PROBE>(*probe, lane)) {
+          __atomic_thread_fence(__ATOMIC_ACQUIRE);
+          mismatch = loadFlag(flagBase + lane) < target[lane];  // still missing after the other kind's flag
+        }
         if (__hip_atomic_load(dc.abortFlag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
           if (lane == 0) reportError(dc, DERR_ABORT);
+          bad = true;
+        } else if (__any(mismatch)) {
+          if (mismatch) reportError(dc, DERR_MISMATCH);
           bad = true;
         } else if (__hip_atomic_load(dc.errorWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
           bad = true;  // another workgroup already failed: stop waiting
@@ -542,6 +580,7 @@ struct RefGeom {
 // Per-workgroup (channel) LDS scratch for the handshake arrays.
 struct Shared {
   ChanState st;
+  WaitProbe probe;  // staged waits: a peer's SYM_ENTER beyond this channel's symmetric epoch is a mismatch
   RefGeom ref;
   const char* srcPtr[NCCL_AMD_MAX_RANKS];   // phase-B fold sources, in fold order
   char* pushPtr[NCCL_AMD_MAX_RANKS];        // phase-B remote destinations
@@ -690,7 +729,7 @@ struct Channel {
     if (COLL != COLL_AG) {
       if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
       __syncthreads();
-      if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, !noAcq)) return false;
+      if (!waitAll<PROBE_STAGED>(dc, sh.st, myFlags(FLG_RS_READY), sh.want, !noAcq, &sh.probe)) return false;
     }
     if (push) {
       if (tid < NCCL_AMD_MAX_RANKS) {
@@ -800,7 +839,7 @@ struct Channel {
     int tid = threadIdx.x;
     if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(CTR_RECV_RS, tid) + 1 : 0;
     __syncthreads();
-    if (!waitAll(dc, sh.st, myFlags(FLG_RS_READY), sh.want, !noAcq)) return false;
+    if (!waitAll<PROBE_STAGED>(dc, sh.st, myFlags(FLG_RS_READY), sh.want, !noAcq, &sh.probe)) return false;
     uint64_t lo, hi;
     sliceRange(a, cl, step, a.count, lo, hi);
     for (uint64_t x = lo; x < hi;) {
@@ -839,7 +878,7 @@ struct Channel {
     const int recvKind = agPull ? CTR_PULL_GOT : CTR_RECV_AG;
     if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(recvKind, tid) + 1 : 0;
     __syncthreads();
-    if (!waitAll(dc, sh.st, myFlags(agPull ? FLG_PULL_READY : FLG_AG_READY), sh.want, !noAcq)) return false;
+    if (!waitAll<PROBE_STAGED>(dc, sh.st, myFlags(agPull ? FLG_PULL_READY : FLG_AG_READY), sh.want, !noAcq, &sh.probe)) return false;
     for (int k = 1; k < n; k++) {
       int q = (me + n - k) % n;
       const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
@@ -871,7 +910,11 @@ __device__ __forceinline__ void loadCounters(const DevComm& dc, Shared& sh, int 
     int k = tid / NCCL_AMD_MAX_RANKS, r = tid % NCCL_AMD_MAX_RANKS;
     sh.st.ctr[k][r] = dc.counters[ctrIndex(c, k, r)];
   }
-  if (tid == 0) sh.st.abort = 0;
+  if (tid == 0) {
+    sh.st.abort = 0;
+    sh.probe.flag[0] = dc.flags[dc.rank] + flagIndex(c, FLG_SYM_ENTER, 0);
+    sh.probe.epoch = dc.counters[ctrIndex(c, CTR_SYM, 0)];
+  }
   __syncthreads();
 }
 __device__ __forceinline__ void storeCounters(const DevComm& dc, Shared& sh, int c) {
@@ -1397,6 +1440,7 @@ enum SymColl { SYM_AR = 0, SYM_AR1 = 1, SYM_RS = 2, SYM_AG = 3 };
 
 struct SymShared {
   ChanState st;
+  WaitProbe probe;  // ENTER wait: a peer's staged-kernel flags beyond what this rank consumed are a mismatch
   const char* srcPtr[NCCL_AMD_MAX_RANKS];
   uint64_t want[NCCL_AMD_MAX_RANKS];
   uint64_t* sigPtr[NCCL_AMD_MAX_RANKS];
@@ -1423,8 +1467,17 @@ __device__ __forceinline__ void symSignal(const DevComm& dc, SymShared& sh, int 
 __device__ __forceinline__ bool symWait(const DevComm& dc, SymShared& sh, int c, int kind, uint64_t e, bool ACQ) {
   const int tid = threadIdx.x, me = dc.rank;
   if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < dc.nRanks && tid != me) ? e : 0;
+  if (tid == 0 && kind == FLG_SYM_ENTER) {  // (after ENTER every rank is known to run this kernel)
+    const int fk[3] = {FLG_RS_READY, FLG_AG_READY, FLG_PULL_READY}, ck[3] = {CTR_RECV_RS, CTR_RECV_AG, CTR_PULL_GOT};
+    for (int k = 0; k < 3; k++) {
+      sh.probe.flag[k] = dc.flags[me] + flagIndex(c, fk[k], 0);
+      sh.probe.seen[k] = dc.counters + ctrIndex(c, ck[k], 0);
+    }
+  }
   __syncthreads();
-  return waitAll(dc, sh.st, dc.flags[me] + flagIndex(c, kind, 0), sh.want, ACQ);
+  const uint64_t* base = dc.flags[me] + flagIndex(c, kind, 0);
+  return kind == FLG_SYM_ENTER ? waitAll<PROBE_SYM>(dc, sh.st, base, sh.want, ACQ, &sh.probe)
+                               : waitAll(dc, sh.st, base, sh.want, ACQ);
 }
 
 template <typename T, int OP, int COLL>

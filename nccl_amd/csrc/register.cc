@@ -180,7 +180,7 @@ static uint64_t bufferIdOf(const void* p) {
 // peer's kernels stop reading it before this rank's kernel passes its DONE handshake).
 static void regRelease(ncclComm* comm, RegAlloc* ra) {
   for (int r = 0; r < comm->nRanks; r++)
-    if (ra->imported[r]) ipcRemoteRelease(comm->peers[r].stagingDesc.server, comm->rank, ra->tag);
+    if (ra->imported[r]) ipcRemoteRelease(comm->peers[r].fdServer, comm->rank, ra->tag);
   delete ra;
 }
 
@@ -201,13 +201,16 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
       ra->rmt[r] = base;
       continue;
     }
-    if (comm->peers[r].stagingDesc.server[0] == 0) {  // NCCL_AMD_IPC=legacy: no fd server to map through
-      INFO("rank %d: registered buffer %lx stays local (no fd server on rank %d)", me, (unsigned long)base, r);
+    if (!comm->regIpcAll) {  // some rank runs no fd server (NCCL_AMD_IPC=legacy): every rank stays staged
+      INFO("rank %d: registered buffer %lx stays local (a rank of this communicator has no fd server)", me,
+           (unsigned long)base);
       ra->usable = false;
       break;
     }
     if (fd < 0) {
-      hipError_t e = hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
+      hipError_t e = paramInt("NCCL_AMD_REG_FAIL_EXPORT", 0)  // tests: a registration that fails on one rank only
+                         ? hipErrorInvalidValue
+                         : hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
       if (e != hipSuccess) {
         (void)hipGetLastError();
         WARN("ncclCommRegister: allocation %lx (+%zu) cannot be exported: %s", (unsigned long)base, (size_t)size,
@@ -216,7 +219,7 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
         break;
       }
     }
-    res = ipcRemoteImport(comm->peers[r].stagingDesc.server, me, ra->tag, fd, size, &ra->rmt[r]);
+    res = ipcRemoteImport(comm->peers[r].fdServer, me, ra->tag, fd, size, &ra->rmt[r]);
     if (res == ncclSuccess) ra->imported[r] = true;
   }
   if (fd >= 0) close(fd);
@@ -311,8 +314,16 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     (void)hipThreadExchangeStreamCaptureMode(&mode);
     RegAlloc* x = nullptr;
-    if (send && !rs && regAcquire(comm, send, sendBytes, true, &x) == ncclSuccess) rs = x->usable ? x : nullptr;
-    if (!rr && regAcquire(comm, recv, recvBytes, true, &x) == ncclSuccess) rr = x->usable ? x : nullptr;
+    ncclResult_t rsRes = ncclSuccess, rrRes = ncclSuccess;
+    if (send && !rs && (rsRes = regAcquire(comm, send, sendBytes, true, &x)) == ncclSuccess) rs = x->usable ? x : nullptr;
+    if (!rr && (rrRes = regAcquire(comm, recv, recvBytes, true, &x)) == ncclSuccess) rr = x->usable ? x : nullptr;
+    // a rank whose auto-registration failed captures the staged kernel while its peers may capture the zero-copy
+    // one: the replay then fails fast on every rank with a kernel-mismatch error (kernels.h WaitProbe) instead of
+    // waiting for the spin timeout; said here so the cause is on record
+    if (rsRes != ncclSuccess || rrRes != ncclSuccess)
+      WARN("rank %d: graph registration of a captured collective's buffers failed (%d): this rank captures the staged "
+           "kernel; if its peers registered theirs, the replay stops with a kernel-mismatch error (set "
+           "NCCL_GRAPH_REGISTER=0 on every rank to avoid it)", comm->rank, (int)(rsRes != ncclSuccess ? rsRes : rrRes));
     (void)hipThreadExchangeStreamCaptureMode(&mode);
     (void)hipGetLastError();
   }
@@ -324,7 +335,7 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
   return true;
 }
 
-void windowsFree(ncclComm* comm) {
+void windowsFree(ncclComm* comm, bool notifyPeers) {
   (void)hipSetDevice(comm->device);
   for (ncclWindow_vidmem* w : comm->windows) windowRelease(comm, w);
   comm->windows.clear();
@@ -332,9 +343,14 @@ void windowsFree(ncclComm* comm) {
   comm->ipcMaps.clear();
   for (RegHandle* h : comm->regHandles) delete h;
   comm->regHandles.clear();
-  // No release requests at destroy: peers may be tearing down at the same moment, and every peer's fd server
-  // drops the mappings it holds for this communicator when it stops (ipcServerStop)
-  for (RegAlloc* ra : comm->regs) delete ra;
+  // Destroy (notifyPeers): best-effort RELEASE requests (no retry: a peer already tearing down has no server
+  // left, and its ipcServerStop drops every mapping it held for us anyway), so a peer whose communicator lives on
+  // does not keep this rank's registered allocations — graph auto-registrations included — mapped until then
+  // (the reference drops them with the registration, src/register/register.cc). Abort sends nothing.
+  for (RegAlloc* ra : comm->regs) {
+    if (notifyPeers) regRelease(comm, ra);
+    else delete ra;
+  }
   comm->regs.clear();
 }
 
@@ -346,7 +362,7 @@ using namespace ncclamd;
 
 NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle) {
   NCCLCHECK(commCheck(comm, "ncclCommRegister", "comm"));
-  ipcDrainReleases(nullptr);
+  ipcDrainReleases();
   if (handle == nullptr) {
     WARN("ncclCommRegister : handle argument is NULL");
     return ncclInvalidArgument;
@@ -379,7 +395,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommRegister, const ncclComm_t, void*, size_t, void
 
 NCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle) {
   NCCLCHECK(commCheck(comm, "ncclCommDeregister", "comm"));
-  ipcDrainReleases(nullptr);
+  ipcDrainReleases();
   if (handle == nullptr) return ncclSuccess;  // reference commDeregister: NULL reg is a no-op
   auto it = std::find(comm->regHandles.begin(), comm->regHandles.end(), (RegHandle*)handle);
   if (it == comm->regHandles.end()) {
@@ -403,7 +419,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommDeregister, const ncclComm_t, void*)
 NCCL_EXPORT ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, size_t size, ncclWindow_t* win,
                                                 int winFlags) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowRegister", "comm"));
-  ipcDrainReleases(nullptr);
+  ipcDrainReleases();
   if (win == nullptr) {
     WARN("ncclCommWindowRegister : win argument is NULL");
     return ncclInvalidArgument;
@@ -423,7 +439,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommWindowRegister, ncclComm_t, void*, size_t, nccl
 
 NCCL_EXPORT ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowDeregister", "comm"));
-  ipcDrainReleases(nullptr);
+  ipcDrainReleases();
   if (win == nullptr) return ncclSuccess;
   auto it = std::find(comm->windows.begin(), comm->windows.end(), win);
   if (it == comm->windows.end() || win->comm != comm) {

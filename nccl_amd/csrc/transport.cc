@@ -49,14 +49,19 @@ ncclResult_t transportSetup(ncclComm* comm) {
   HIPCHECK(hipSetDevice(comm->device));
   if (comm->nRanks == 1) return ncclSuccess;  // nranks==1 never touches peers (onerank.cu:49-110)
   size_t sb = stagingBytes(comm), fb = flagsBytes(comm);
-  std::lock_guard<std::mutex> mapLock(ipcMapMutex());
-  if (paramInt("NCCL_AMD_STAGING_PLAIN", 0))  // diagnostics only (scripts/ipc_hang_diag.py): cached staging
-    HIPCHECK(hipMalloc(&comm->staging, sb));
-  else
-    HIPCHECK(hipExtMallocWithFlags(&comm->staging, sb, hipDeviceMallocUncached));
-  comm->stagingAllocBytes = sb;
-  HIPCHECK(hipExtMallocWithFlags((void**)&comm->flags, fb, hipDeviceMallocUncached));
-  comm->flagsAllocBytes = fb;
+  {
+    // only the allocations themselves are serialized with imports / releases (gMapMu): the fd server thread
+    // needs the same lock to map a peer's registration, so it is never held across the device-wide sync below
+    // (a peer registering a buffer could otherwise wait behind a sync that waits on that peer)
+    std::lock_guard<std::mutex> mapLock(ipcMapMutex());
+    if (paramInt("NCCL_AMD_STAGING_PLAIN", 0))  // diagnostics only (scripts/ipc_hang_diag.py): cached staging
+      HIPCHECK(hipMalloc(&comm->staging, sb));
+    else
+      HIPCHECK(hipExtMallocWithFlags(&comm->staging, sb, hipDeviceMallocUncached));
+    comm->stagingAllocBytes = sb;
+    HIPCHECK(hipExtMallocWithFlags((void**)&comm->flags, fb, hipDeviceMallocUncached));
+    comm->flagsAllocBytes = fb;
+  }
   HIPCHECK(hipMemset(comm->flags, 0, fb));
   HIPCHECK(hipDeviceSynchronize());
   INFO("rank %d dev %d: staging %zu MiB (%d ch x %d slots x %zu KiB), flags %zu KiB", comm->rank, comm->device,
@@ -242,6 +247,7 @@ ncclResult_t exportHandles(ncclComm* comm, PeerInfo* info) {
   info->flagsPtr = (uint64_t)comm->flags;
   if (comm->nRanks == 1 || !comm->bootstrap) return ncclSuccess;
   NCCLCHECK(ipcServerStart(comm));
+  snprintf(info->fdServer, sizeof(info->fdServer), "%s", ipcServerName(comm));
   NCCLCHECK(ipcExport(comm, comm->staging, stagingBytes(comm), &info->stagingDesc));
   NCCLCHECK(ipcExport(comm, comm->flags, flagsBytes(comm), &info->flagsDesc));
   return ncclSuccess;

@@ -64,7 +64,7 @@ ncclResult_t groupDeferColl(const CollInfo&) { return ncclSuccess; }
 void groupRecordError(ncclResult_t) {}
 void tunerPick(ncclComm*, CollFunc, size_t, int, int, int*, int* nch) { *nch = 0; }
 ncclResult_t commCheck(const ncclComm*, const char*, const char*) { return ncclSuccess; }
-void ipcDrainReleases(hipStream_t) {}
+void ipcDrainReleases() {}
 }  // namespace ncclamd
 
 using namespace ncclamd;

@@ -54,7 +54,10 @@ def test_rates():
     S = 256 << 20
     v, alg, bus = bench.rates(8, S, 1.0)
     assert abs(alg - S / 1e-3 / 1e9) < 1e-6
-    assert abs(bus - alg * 2 * 7 / 8) < 1e-6 and abs(v - 8 * bus) < 1e-6
+    # at n >= 2 the value IS the metric's busBW (per rank, nccl-tests), not N x busBW
+    assert abs(bus - alg * 2 * 7 / 8) < 1e-6 and v == bus
+    v2, _, bus2 = bench.rates(2, S, 1.0)
+    assert v2 == bus2 and abs(bus2 - S / 1e-3 / 1e9) < 1e-6
     v1, _, bus1 = bench.rates(1, 64 << 20, 1.0)
     assert bus1 == 0 and abs(v1 - 2 * (64 << 20) / 1e-3 / 1e9) < 1e-6
     assert bench.hbm_bytes_per_rank("allreduce", 8, S) == int(2 * S + 4 * 7 * S / 8)

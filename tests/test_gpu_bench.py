@@ -33,6 +33,8 @@ def test_bench_two_ranks_quick(built):
     assert len(lines) == 1, out.stdout[-2000:]
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["check"] == "pass" and d["value"] > 0 and d["unit"] == "GB/s"
+    # value = the metric's busBW (per rank); the whole-job sum is reported beside it
+    assert d["value"] == d["busbw_GBps"] and abs(d["busbw_sum_GBps"] - 2 * d["busbw_GBps"]) < 0.05
     # at n >= 2 the binding roofline is the links; the HBM fraction is secondary, and the
     # kernel is named from the run (the library's kernel log), not a literal
     roof = d["roofline"]

@@ -360,3 +360,166 @@ def test_deregistration_then_new_communicator(built):
     res = _spawn(_dereg_then_new_comm_worker, 4, args=(nccl_amd.get_unique_id(),), limit_s=300)
     bad = [e for r in sorted(res) for e in res[r]]
     assert not bad, "\n".join(bad[:10])
+
+
+def _wait_file(path, limit_s=60):
+    t0 = time.time()
+    while not os.path.exists(path):
+        if time.time() - t0 > limit_s:
+            raise TimeoutError(path)
+        time.sleep(0.01)
+
+
+def _async_after_dereg_worker(rank, nranks, uid, q, tag):
+    """a collective issued right after a peer deregistered a buffer returns to the host once its
+    work is enqueued (reference nccl.h.in:431-442), even while this rank's previous kernel still waits for that
+    peer. Rank 0 issues AllReduce #1 (its kernel waits: rank 1 is deliberately late), rank 1 deregisters (its
+    RELEASE request reaches rank 0's fd server), then rank 0 issues AllReduce #2. Round 3 unmapped the peer's
+    buffer inside that call with a device-synchronising hipFree, so the call blocked until rank 1 arrived (the
+    late rank's delay); the unmapping now waits for rank 0's next blocking entry point (ipc.cc ipcDrainReleases)."""
+    try:
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "60000"
+        os.environ["NCCL_PROTO"] = "^LL"
+        import torch
+        import nccl_amd
+        from tests import gpu_cases as G
+        import oracle
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.Stream()
+        errs = []
+        reg = torch.empty(WIN_BYTES, dtype=torch.uint8, device="cuda")
+        h = comm.register_buffer(reg.data_ptr(), WIN_BYTES)
+        errs += _run([(comm, s)], [(reg, reg.data_ptr())], "allreduce", 7, 0, 200_003, 0, False, seed=11)
+        torch.cuda.synchronize()
+        count = 4 << 20  # 16 MiB fp32: the staged direct kernel
+        ins = G.make_inputs(nranks, 7, count, seed=12)
+        x = torch.from_numpy(ins[rank]).cuda()
+        y1, y2 = torch.empty_like(x), torch.empty_like(x)
+        torch.cuda.synchronize()
+        flag = lambda name: f"/tmp/nccl_amd_async_{tag}_{name}"
+        issue_s = None
+        if rank == 0:
+            comm.all_reduce_raw(x.data_ptr(), y1.data_ptr(), count, 7, 0, s.cuda_stream)  # waits for rank 1
+            open(flag("ar1"), "w").close()
+            _wait_file(flag("dereg"))
+            t0 = time.time()
+            comm.all_reduce_raw(x.data_ptr(), y2.data_ptr(), count, 7, 0, s.cuda_stream)
+            issue_s = time.time() - t0
+            open(flag("ar2"), "w").close()
+        else:
+            _wait_file(flag("ar1"))
+            comm.deregister_buffer(h)
+            h = None
+            open(flag("dereg"), "w").close()
+            time.sleep(3.0)  # deliberately late
+            comm.all_reduce_raw(x.data_ptr(), y1.data_ptr(), count, 7, 0, s.cuda_stream)
+            comm.all_reduce_raw(x.data_ptr(), y2.data_ptr(), count, 7, 0, s.cuda_stream)
+        s.synchronize()
+        if comm.async_error():
+            errs.append(f"rank {rank}: async {comm.async_error()}")
+        want = oracle.all_reduce(ins, 7, 0)
+        for name, y in (("#1", y1), ("#2", y2)):
+            if not G.same_bits(y.cpu().numpy(), want, 7):
+                errs.append(f"rank {rank}: AllReduce {name} differs")
+        if h is not None:
+            comm.deregister_buffer(h)
+        comm.destroy()
+        q.put((rank, (errs, issue_s)))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], None)))
+
+
+def test_collective_after_peer_deregistration_returns_before_its_kernel(built):
+    tag = f"{os.getpid()}_{int(time.time() * 1000)}"
+    res = _spawn(_async_after_dereg_worker, 2, args=(tag,), limit_s=300)
+    for name in ("ar1", "dereg", "ar2"):
+        try:
+            os.unlink(f"/tmp/nccl_amd_async_{tag}_{name}")
+        except OSError:
+            pass
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:10])
+    issue_s = res[0][1]
+    print(f"rank 0: AllReduce #2 issued in {issue_s * 1e3:.2f} ms while its AllReduce #1 waited for the late rank 1")
+    assert issue_s < 1.0, f"the collective blocked {issue_s:.2f} s (the late rank's delay is 3 s)"
+
+
+def _fail_export_worker(rank, nranks, uid, q):
+    """rank 1's slab export is refused (NCCL_AMD_IPC_FAIL_EXPORT=1: its peers open a hipIpc handle
+    instead), but its fd server still runs and serves registrations: every rank must still take the registered
+    zero-copy kernel (one comm-wide decision from the peer table), bit-exact."""
+    try:
+        if rank == 1:
+            os.environ["NCCL_AMD_IPC_FAIL_EXPORT"] = "1"
+        os.environ["NCCL_PROTO"] = "^LL"
+        logf = _trace_env("failexport")
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        buf = torch.empty(WIN_BYTES, dtype=torch.uint8, device="cuda")
+        h = comm.register_buffer(buf.data_ptr(), WIN_BYTES)
+        s = torch.cuda.Stream()
+        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+        errs = _run([(comm, s)], [(buf, buf.data_ptr())], "allreduce", 7, 0, 300_001, 0, False, seed=5)
+        torch.cuda.synchronize()
+        zc = _zero_copy_lines(logf, pos)
+        comm.deregister_buffer(h)
+        comm.destroy()
+        q.put((rank, (errs, len(zc))))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0)))
+
+
+def test_registration_survives_one_ranks_export_fallback(built):
+    res = _spawn(_fail_export_worker, 2)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:10])
+    assert all(zc == 1 for _, zc in res.values()), res
+
+
+def _graph_mismatch_worker(rank, nranks, uid, q):
+    """a graph auto-registration that fails on ONE rank (NCCL_AMD_REG_FAIL_EXPORT=1 on rank 1) makes
+    that rank capture the staged kernel while rank 0 captures the zero-copy one. The replay must stop on both
+    ranks with the kernel-mismatch error (ncclInvalidUsage, kernels.h WaitProbe) well before the spin timeout,
+    instead of both waiting for it."""
+    try:
+        if rank == 1:
+            os.environ["NCCL_AMD_REG_FAIL_EXPORT"] = "1"
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "60000"
+        os.environ["NCCL_AMD_DESTROY_TIMEOUT_MS"] = "500"
+        os.environ["NCCL_PROTO"] = "^LL"
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = nccl_amd.dedicated_stream(0)
+        count = 3 << 20
+        x = torch.ones(count, dtype=torch.float32, device="cuda")
+        y = torch.empty_like(x)
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s):
+            comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+        torch.cuda.synchronize()
+        t0 = time.time()
+        with torch.cuda.stream(s):
+            g.replay()
+        torch.cuda.synchronize()
+        elapsed = time.time() - t0
+        err = comm.async_error()
+        del g
+        comm.destroy()
+        q.put((rank, ([], err, elapsed)))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], -1, 0)))
+
+
+def test_graph_registration_failure_on_one_rank_is_reported(built):
+    res = _spawn(_graph_mismatch_worker, 2, limit_s=300)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:10])
+    for r, (_, err, elapsed) in res.items():
+        assert err == 5, f"rank {r}: async error {err} (want ncclInvalidUsage from the mismatch probe)"
+        assert elapsed < 20, f"rank {r}: the replay took {elapsed:.1f} s (spin timeout 60 s)"
