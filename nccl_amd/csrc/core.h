@@ -235,6 +235,7 @@ struct CommTuning {
   int refOrder;             // NCCL_AMD_REF_ORDER: AllReduce on the direct kernel in the reference's ring partition
   int refProto;             // ... of this protocol (NCCL_PROTO_LL 0, LL128 1, SIMPLE 2: the one NCCL_PROTO names)
   int64_t refChunkBytes;    // that protocol's ring chunk (NCCL_BUFFSIZE / NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE)
+  int refChannels;          // NCCL_AMD_REF_NCHANNELS: the reference run's channel count K (0: the channel cap), <= 64
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
 void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known
@@ -310,6 +311,7 @@ struct ncclComm {
   std::thread initThread;  // non-blocking ncclCommInitRankConfig (config.blocking = 0)
   uint64_t opCount = 0;
   uint32_t warnedAlgo = 0;  // NCCL_ALGO forced but unavailable for a collective: warned once per CollFunc
+  bool warnedRefClamp = false;  // the reference-order channel count was clamped to MAXCHANNELS (warned once)
   // every rank can map every other-process peer's registered buffers (each such peer runs an fd server): derived
   // from the shared peer table at init, so every rank takes the same registered / staged decision (register.cc)
   bool regIpcAll = false;

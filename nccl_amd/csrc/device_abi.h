@@ -102,10 +102,16 @@ struct CollArgs {
   int root;
   int aligned;         // send/recv base pointers are 16-byte aligned
   int protoFlags;      // NCCL_AMD_PROTO_FLAGS diagnostics (kernels.h collKernel)
-  // Ring AllReduce (PIPE_RING_AR) in the reference's partition: channel parts lo / mid (= part) / hi
-  // (ncclCollCbdPart, reference src/include/device.h:337-361), each walked in loops of n chunks of `chunk`
-  // elements (all_reduce.h:21-38). Unused by every other kernel.
+  // Ring AllReduce (PIPE_RING_AR) and the reference-order direct AllReduce (COLL_ARREF) in the reference's
+  // partition: channel parts lo / mid (= part) / hi (ncclCollCbdPart, reference src/include/device.h:337-361),
+  // each walked in loops of n chunks of `chunk` elements (all_reduce.h:21-38). Unused by every other kernel.
   uint64_t cbdLo, cbdHi;
+  // ... and refSub workgroups per reference channel part: workgroup c serves part c / refSub and, inside every
+  // chunk of that part, the sub-chunk c % refSub (an element's fold order depends only on its loop and chunk,
+  // never on which workgroup moves it), so the reference's channel count and this launch's parallelism are
+  // independent.
+  uint32_t refSub;
+  uint32_t refPad;
 };
 
 // Staged batch: up to kMaxCollBatch ops of one group with the same collective, type and op (and the same

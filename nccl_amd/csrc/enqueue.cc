@@ -149,6 +149,9 @@ void loadTuning(CommTuning* t) {
   // NCCL_AMD_REF_ORDER=1: every AllReduce folds in the reference's RING/SIMPLE order at any size, on the fast
   // direct kernel (planColl below)
   t->refOrder = (int)paramInt("NCCL_AMD_REF_ORDER", 0);
+  // the reference run's channel count for the modes that walk its partition (NCCL_AMD_REF_ORDER, NCCL_ALGO=RING):
+  // 0 = the communicator's channel cap, clamped to the reference's MAXCHANNELS (refChannelCount)
+  t->refChannels = (int)paramInt("NCCL_AMD_REF_NCHANNELS", 0);
   const int64_t buff = paramInt("NCCL_BUFFSIZE", 4 << 20);
   t->ringChunkBytes = buff / 8 * 4 / 512 * 512;
   if (t->ringChunkBytes < 512) t->ringChunkBytes = 512;
@@ -268,8 +271,8 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
 }
 
 // NCCL_ALGO=RING AllReduce: the reference's own partition, so that every element is finalised by the same ring
-// position as in the reference's RING/SIMPLE AllReduce on a communicator of K channels (here K = chanCap, i.e.
-// NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS = K there) with the same NCCL_BUFFSIZE — bit-identical results, floats
+// position as in the reference's RING/SIMPLE AllReduce on a communicator of K channels (K = refChannelCount below,
+// i.e. NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS = K there) with the same NCCL_BUFFSIZE — bit-identical results, floats
 // included. NCCL_AMD_REF_ORDER walks the same partition, or the one of RING/LL or RING/LL128
 // (`proto` 0 / 1). For one task, starting on channel 0 with no traffic planned yet:
 //  * channels: K shrunk while the bytes are below K x threads x threshold — 512 x 64 (Simple), 512 x 8n (LL),
@@ -283,6 +286,21 @@ struct RingParts {
   int nch;
   uint64_t lo, mid, hi;
 };
+// The reference never runs more than MAXCHANNELS = 64 channels (src/include/device.h:91), so a partition of
+// more parts than that is one no reference run produces: K = NCCL_AMD_REF_NCHANNELS, else the channel cap, and
+// at most 64 (warned once when a larger count is clamped).
+constexpr int kRefMaxChannels = 64;
+static int refChannelCount(ncclComm* comm) {
+  const int want = comm->tune.refChannels > 0 ? comm->tune.refChannels : comm->chanCap;
+  if (want <= kRefMaxChannels) return want < 1 ? 1 : want;
+  if (!comm->warnedRefClamp) {
+    comm->warnedRefClamp = true;
+    WARN("the reference's partition has at most %d channels (MAXCHANNELS, device.h:91): %s %d -> %d; set "
+         "NCCL_AMD_REF_NCHANNELS to the reference run's channel count", kRefMaxChannels,
+         comm->tune.refChannels > 0 ? "NCCL_AMD_REF_NCHANNELS" : "channel cap", want, kRefMaxChannels);
+  }
+  return kRefMaxChannels;
+}
 static RingParts ringParts(uint64_t count, int ts, int K, int n, int proto) {
   const uint64_t bytes = count * (uint64_t)ts;
   const uint64_t threads = proto == 1 ? 640 : 512, threshold = proto == 0 ? 8 * (uint64_t)n : proto == 1 ? 8 : 64;
@@ -315,6 +333,20 @@ static RingParts ringParts(uint64_t count, int ts, int K, int n, int proto) {
   (r.hi ? r.hi : r.lo) -= cells * eltsPerCell - count;  // the last part ends at count
   r.nch = (r.lo ? 1 : 0) + (int)nMid + (cellsHi ? 1 : 0);
   return r;
+}
+
+// Workgroups per reference channel part (CollArgs::refSub): the parts' chunks are cut into sub-chunks so that
+// the launch fills `physCap` workgroups (the channel cap, and the CU budget at n >= 3 like the default plan)
+// while no sub-chunk of a rank block drops below minChannelBytes (the default plan's per-channel granularity).
+static uint32_t refSubCount(ncclComm* comm, const RingParts& r, uint64_t chunk, int n, int ts) {
+  int physCap = comm->chanCap;
+  if (n >= 3 && comm->tune.linkChannels > 0) physCap = std::min(physCap, std::max(comm->tune.linkChannels, r.nch));
+  const uint64_t epp = 16 / ts;
+  const uint64_t maxPart = std::max(r.lo, std::max(r.mid, r.hi));
+  uint64_t ck = std::min<uint64_t>(chunk, ((maxPart + n - 1) / n + epp - 1) / epp * epp);  // largest chunk in use
+  const uint64_t minSub = std::max<uint64_t>(epp, (uint64_t)comm->tune.minChannelBytes / ts);
+  uint64_t g = std::min<uint64_t>(physCap / std::max(r.nch, 1), ck / minSub);
+  return g < 1 ? 1 : (uint32_t)g;
 }
 
 // LL eligibility and channel plan of one AllReduce, ReduceScatter, AllGather or Reduce (reference tuning: LL for
@@ -543,12 +575,13 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       const size_t span = chain ? count * ts : blockElems * ts;
       planChannels(comm, span, ts, p, (size_t)comm->tune.minChannelBytes, comm->chanCap);
       if (kind == PIPE_RING_AR) {  // the reference's channel parts and loop chunk (ringParts above)
-        const RingParts r = ringParts(count, ts, comm->chanCap, n, comm->tune.refProto);
-        p.nChannels = r.nch;
+        const RingParts r = ringParts(count, ts, refChannelCount(comm), n, comm->tune.refProto);
         p.args.cbdLo = r.lo;
         p.args.part = r.mid;
         p.args.cbdHi = r.hi;
         p.args.chunk = (uint64_t)comm->tune.refChunkBytes / ts;
+        p.args.refSub = refSubCount(comm, r, p.args.chunk, n, ts);
+        p.nChannels = r.nch * (int)p.args.refSub;
         p.args.slice = std::min<uint64_t>(p.args.chunk, comm->slotBytes / ts / epp * epp);
         p.args.nSteps = 0;  // per channel and loop (pipe.h)
       }
@@ -561,18 +594,19 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     // The reference's ring partition of the protocol NCCL_PROTO names (ringParts: channel parts, the protocol's
     // chunks, loops; Simple unless NCCL_PROTO is LL or LL128 alone) walked by the direct scatter-reduce-gather kernel: in each loop chunk q is finalised by rank q, as in the reference's ring,
     // so every element folds in its order — at the direct kernel's n-1 links instead of the ring's one (kernels.h
-    // Channel::refPart). All channels of the communicator's cap, no CU budget: the partition is the reference's.
-    const RingParts r = ringParts(count, ts, comm->chanCap, n, comm->tune.refProto);
-    p.nChannels = r.nch;
+    // Channel::refPart). K reference parts (at most 64), each served by refSub workgroups (refSubCount).
+    const RingParts r = ringParts(count, ts, refChannelCount(comm), n, comm->tune.refProto);
     p.args.cbdLo = r.lo;
     p.args.part = r.mid;
     p.args.cbdHi = r.hi;
     p.args.chunk = (uint64_t)comm->tune.refChunkBytes / ts;
+    p.args.refSub = refSubCount(comm, r, p.args.chunk, n, ts);
+    p.nChannels = r.nch * (int)p.args.refSub;
     p.args.slice = std::min<uint64_t>(p.args.chunk, comm->slotBytes / ts / epp * epp);
-    p.args.nSteps = 0;  // per channel (kernels.h Channel::refSteps)
-    TRACE("%s: direct in the reference's partition, nch %d parts %lu/%lu/%lu chunk %lu slice %lu", info.opName,
-          p.nChannels, (unsigned long)r.lo, (unsigned long)r.mid, (unsigned long)r.hi, (unsigned long)p.args.chunk,
-          (unsigned long)p.args.slice);
+    p.args.nSteps = 0;  // per channel (kernels.h Channel::refInit)
+    TRACE("%s: direct in the reference's partition, %d parts x %u workgroups, parts %lu/%lu/%lu chunk %lu slice %lu",
+          info.opName, r.nch, p.args.refSub, (unsigned long)r.lo, (unsigned long)r.mid, (unsigned long)r.hi,
+          (unsigned long)p.args.chunk, (unsigned long)p.args.slice);
     return ncclSuccess;
   }
   // Zero-copy kernels (kernels.h symKernel): buffers in NCCL_WIN_COLL_SYMMETRIC windows (reference: symmetric

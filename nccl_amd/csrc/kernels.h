@@ -572,10 +572,11 @@ __device__ __forceinline__ void sliceRange(const CollArgs& a, int c, int s, uint
 }
 
 // COLL_ARREF channel geometry (Channel::refInit): region offset, loop length, full loops, the last loop's length
-// and chunk, steps per full loop, steps in all.
+// and chunk, this workgroup's sub-chunk length in a full / the last loop, steps per full loop, steps in all, and
+// which sub-chunk of every chunk this workgroup moves.
 struct RefGeom {
-  uint64_t off, loop, rem, ckLast;
-  uint32_t full, perFull, steps;
+  uint64_t off, loop, rem, ckLast, scFull, scLast;
+  uint32_t full, perFull, steps, sub;
 };
 // Per-workgroup (channel) LDS scratch for the handshake arrays.
 struct Shared {
@@ -627,26 +628,39 @@ struct Channel {
   // channel parts. This channel walks its part (ncclCollCbdPart, device.h:337-361: cbdLo / part / cbdHi) in loops
   // of n chunks of a.chunk elements, the last loop's chunk re-cut to alignUp(divUp(rem, n), 16 / sizeof(T))
   // (all_reduce.h:34-38); chunk q of a loop is "block" q, owned and finalised by rank q, so every element folds
-  // q+1, ..., q as in the reference's ring. Step s = slice j of loop l (a.slice elements per chunk and step).
+  // q+1, ..., q as in the reference's ring. a.refSub workgroups share one reference part: workgroup cl serves part
+  // cl / refSub and moves sub-chunk cl % refSub (alignUp(divUp(chunk, refSub), 16 / sizeof(T)) elements) of every
+  // chunk of it — which workgroup moves an element never changes its fold order, so the reference's channel count
+  // and the launch's parallelism are independent. Step s = slice j of the sub-chunk of loop l.
   static constexpr bool refPart() { return COLL == COLL_ARREF; }
   // this channel's region and loop geometry, computed once per launch (refInit) into LDS (Shared::ref): the 64-bit
   // divisions stay out of the per-step code and the values out of the registers the fold needs
   __device__ void refInit() {
     constexpr uint64_t EPP = 16 / sizeof(T);
     if (threadIdx.x == 0) {
-      const int nch = (int)gridDim.x;  // never batched: the grid is the op's channels
+      const uint32_t G = a.refSub;
+      const int nParts = (int)(gridDim.x / G);  // never batched: the grid is the op's channels
+      const int k = (int)((uint32_t)cl / G);
       uint64_t off, cnt;
-      if (cl == 0) off = 0, cnt = a.cbdLo;
-      else if (cl == nch - 1) off = a.cbdLo + (uint64_t)(nch - 2) * a.part, cnt = a.cbdHi;
-      else off = a.cbdLo + (uint64_t)(cl - 1) * a.part, cnt = a.part;
+      if (k == 0) off = 0, cnt = a.cbdLo;
+      else if (k == nParts - 1) off = a.cbdLo + (uint64_t)(nParts - 2) * a.part, cnt = a.cbdHi;
+      else off = a.cbdLo + (uint64_t)(k - 1) * a.part, cnt = a.part;
       RefGeom& g = sh.ref;
       g.off = off;
+      g.sub = (uint32_t)cl - (uint32_t)k * G;
       g.loop = (uint64_t)n * a.chunk;
       g.full = (uint32_t)(cnt / g.loop);
       g.rem = cnt - (uint64_t)g.full * g.loop;
       g.ckLast = g.rem ? ((g.rem + n - 1) / n + EPP - 1) / EPP * EPP : 0;
-      g.perFull = (uint32_t)((a.chunk + a.slice - 1) / a.slice);
-      g.steps = g.full * g.perFull + (uint32_t)((g.ckLast + a.slice - 1) / a.slice);
+      g.scFull = ((a.chunk + G - 1) / G + EPP - 1) / EPP * EPP;
+      g.scLast = ((g.ckLast + G - 1) / G + EPP - 1) / EPP * EPP;
+      // this sub-chunk's length in a chunk of length ck (block 0's, the longest of a loop)
+      auto subLen = [&](uint64_t ck, uint64_t sc) -> uint64_t {
+        const uint64_t lo = min((uint64_t)g.sub * sc, ck);
+        return min(lo + sc, ck) - lo;
+      };
+      g.perFull = (uint32_t)((subLen(a.chunk, g.scFull) + a.slice - 1) / a.slice);
+      g.steps = g.full * g.perFull + (uint32_t)((subLen(g.ckLast, g.scLast) + a.slice - 1) / a.slice);
     }
     __syncthreads();
   }
@@ -662,12 +676,13 @@ struct Channel {
     const RefGeom& g = sh.ref;
     const uint32_t st = (uint32_t)step, inFull = g.full * g.perFull;
     uint32_t l, j;
-    uint64_t ck, rem;
-    if (st < inFull) l = st / g.perFull, j = st - l * g.perFull, ck = a.chunk, rem = g.loop;
-    else l = g.full, j = st - inFull, ck = g.ckLast, rem = g.rem;
+    uint64_t ck, rem, sc;
+    if (st < inFull) l = st / g.perFull, j = st - l * g.perFull, ck = a.chunk, rem = g.loop, sc = g.scFull;
+    else l = g.full, j = st - inFull, ck = g.ckLast, rem = g.rem, sc = g.scLast;
     const uint64_t bb = (uint64_t)b * ck, blen = bb >= rem ? 0 : min(ck, rem - bb);
-    lo = min((uint64_t)j * a.slice, blen);
-    hi = min(lo + a.slice, blen);
+    const uint64_t sLo = min((uint64_t)g.sub * sc, blen), sHi = min(sLo + sc, blen);  // my sub-chunk of block b
+    lo = min(sLo + (uint64_t)j * a.slice, sHi);
+    hi = min(lo + a.slice, sHi);
     off = g.off + (uint64_t)l * g.loop + bb + lo;
     len = hi - lo;
   }

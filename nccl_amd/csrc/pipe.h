@@ -211,26 +211,32 @@ __global__ void __launch_bounds__(kThreads) kCoResident pipeKernel(CollArgs a) {
     // alignUp(divUp(rem, n), 16 / sizeof(T)) (:38). Chunk q of a loop starts at rank q+1 and is finalised by
     // rank q, so every element folds exactly as in the reference's RING/SIMPLE AllReduce on the same number of
     // channels. A chunk moves through the staging slots in slices of a.slice elements; every rank walks the
-    // same loops and slices (the counts are shared), so the hops pair up.
+    // same loops and slices (the counts are shared), so the hops pair up. a.refSub workgroups share one part:
+    // workgroup c serves part c / refSub and moves sub-chunk c % refSub of every chunk (CollArgs::refSub) — the
+    // ring position that finalises an element, hence its fold order, does not depend on the workgroup.
     constexpr uint64_t EPP = 16 / ts;
-    const int nch = (int)gridDim.x;
+    const uint32_t G = a.refSub, sub = (uint32_t)c % G;
+    const int nParts = (int)(gridDim.x / G), k = (int)((uint32_t)c / G);
     uint64_t pOff, pCnt;
-    if (c == 0) pOff = 0, pCnt = a.cbdLo;
-    else if (c == nch - 1) pOff = a.cbdLo + (uint64_t)(nch - 2) * a.part, pCnt = a.cbdHi;
-    else pOff = a.cbdLo + (uint64_t)(c - 1) * a.part, pCnt = a.part;
+    if (k == 0) pOff = 0, pCnt = a.cbdLo;
+    else if (k == nParts - 1) pOff = a.cbdLo + (uint64_t)(nParts - 2) * a.part, pCnt = a.cbdHi;
+    else pOff = a.cbdLo + (uint64_t)(k - 1) * a.part, pCnt = a.part;
     const uint64_t loopCount = (uint64_t)n * a.chunk;
     for (uint64_t eo = 0; ok && eo < pCnt; eo += loopCount) {
       const uint64_t rem = pCnt - eo;
       const uint64_t ck = rem < loopCount ? ((rem + n - 1) / n + EPP - 1) / EPP * EPP : a.chunk;
+      const uint64_t sc = ((ck + G - 1) / G + EPP - 1) / EPP * EPP;  // sub-chunk length
+      const uint64_t scLo = min((uint64_t)sub * sc, ck);
       const char* inL = in + (pOff + eo) * ts;
       char* outL = outb + (pOff + eo) * ts;
-      const uint64_t nSub = (ck + a.slice - 1) / a.slice;
+      const uint64_t nSub = (min(scLo + sc, ck) - scLo + a.slice - 1) / a.slice;
       for (uint64_t s = 0; ok && s < nSub; s++) {
         uint64_t lo, hi;
-        auto sl = [&](int q) {  // slice s of chunk q (empty past the loop's end)
+        auto sl = [&](int q) {  // slice s of my sub-chunk of chunk q (empty past the loop's end)
           const uint64_t b = (uint64_t)q * ck, len = b >= rem ? 0 : min(ck, rem - b);
-          lo = min(s * a.slice, len);
-          hi = min(lo + a.slice, len);
+          const uint64_t sLo = min((uint64_t)sub * sc, len), sHi = min(sLo + sc, len);
+          lo = min(sLo + s * a.slice, sHi);
+          hi = min(lo + a.slice, sHi);
         };
         auto at = [&](int q) { return ((uint64_t)q * ck + lo) * ts; };
         int q = prev;  // step 0: send chunk ringIx - 1

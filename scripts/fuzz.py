@@ -19,7 +19,7 @@ from tests import gpu_cases as G  # noqa: E402
 KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_AG_PULL",
          "NCCL_AMD_RS_PULL", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_LL_CHANNEL_BYTES", "NCCL_AMD_LL128",
          "NCCL_AMD_LL128_CHANNEL_BYTES", "NCCL_AMD_SYM_WT", "NCCL_AMD_P2P_FENCE", "NCCL_AMD_LINK_CHANNELS",
-         "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER", "NCCL_LL_BUFFSIZE", "NCCL_LL128_BUFFSIZE")
+         "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER", "NCCL_LL_BUFFSIZE", "NCCL_LL128_BUFFSIZE", "NCCL_AMD_REF_NCHANNELS")
 
 
 def settings(rng):
@@ -56,6 +56,11 @@ def settings(rng):
         env["NCCL_AMD_LINK_CHANNELS"] = str(rng.choice([2, 8, 16]))  # the n >= 3 CU budget, tightened
     if rng.random() < 0.15:  # AllReduce on the direct kernel in the reference's ring partition
         env["NCCL_AMD_REF_ORDER"] = "1"
+    if rng.random() < 0.3 and (env.get("NCCL_AMD_REF_ORDER") or env.get("NCCL_ALGO") == "RING"):
+        # the reference run's K apart from the channel cap: its parts shared by several workgroups (refSub)
+        env["NCCL_AMD_REF_NCHANNELS"] = str(rng.choice([1, 2, 5, 16, 64, 100]))
+        if rng.random() < 0.5:
+            env["NCCL_AMD_MIN_CHANNEL_BYTES"] = str(rng.choice([512, 1024, 4096]))
     if rng.random() < 0.2:  # the reference's knob: slot size here, and the ring's chunk (many ring loops)
         env["NCCL_BUFFSIZE"] = str(rng.choice([8192, 16384, 65536]))
     if rng.random() < 0.15:  # the LL / LL128 ring chunks REF_ORDER walks when NCCL_PROTO names that protocol alone

@@ -11,8 +11,16 @@ import torch  # noqa: E402
 
 import nccl_amd  # noqa: E402
 
-MODES = {"direct": {}, "ref_order": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32"},
-         "ref_order_cap": {"NCCL_AMD_REF_ORDER": "1"}, "ring": {"NCCL_ALGO": "RING", "NCCL_MAX_CTAS": "32"}}
+# ref_order_k32 / ring_k32: the reference's K = 32 parts shared by several workgroups (refSub, the channel cap at its
+# default); *_cap32: one workgroup per part (NCCL_MAX_CTAS = 32, round 3's only form); ref_order_k64: the default K
+# (the channel cap clamped to the reference's MAXCHANNELS). MODES_SEL=a,b picks modes (a clean kernel trace).
+MODES = {"direct": {}, "ref_order_k32": {"NCCL_AMD_REF_ORDER": "1", "NCCL_AMD_REF_NCHANNELS": "32"},
+         "ref_order_k64": {"NCCL_AMD_REF_ORDER": "1"},
+         "ref_order_cap32": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32"},
+         "ring_k32": {"NCCL_ALGO": "RING", "NCCL_AMD_REF_NCHANNELS": "32"},
+         "ring_cap32": {"NCCL_ALGO": "RING", "NCCL_MAX_CTAS": "32"}}
+if os.environ.get("MODES_SEL"):
+    MODES = {k: MODES[k] for k in os.environ["MODES_SEL"].split(",")}
 
 
 def main():
@@ -28,7 +36,7 @@ def main():
             if os.environ.get("REVERSE"):
                 order.reverse()
             for mode, env in order:
-                for k in ("NCCL_AMD_REF_ORDER", "NCCL_MAX_CTAS", "NCCL_ALGO"):
+                for k in ("NCCL_AMD_REF_ORDER", "NCCL_MAX_CTAS", "NCCL_ALGO", "NCCL_AMD_REF_NCHANNELS"):
                     os.environ.pop(k, None)
                 os.environ.update(env)
                 comms = nccl_amd.Communicator.init_all([0] * n)

@@ -223,7 +223,7 @@ RING_CASES = [
 RING_PROTO_CASES = [
     ("sum", "f32", 3, 20000, 4, 65536, "ll"), ("sum", "bf16", 4, 30001, 5, 32768, "ll"),
     ("sum", "f16", 5, 60000, 6, 65536, "ll128"), ("max", "f32", 2, 25013, 3, 131072, "ll128"),
-    ("sum", "f32", 8, 3000, 256, 0, "ll"), ("sum", "bf16", 3, 200_000, 4, 0, "ll128"),
+    ("sum", "f32", 8, 3000, 64, 0, "ll"), ("sum", "bf16", 3, 200_000, 4, 0, "ll128"),
 ]
 
 

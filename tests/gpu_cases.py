@@ -51,14 +51,19 @@ def _env_int(name: str, default: int) -> int:
 
 
 def ring_channels(n: int, ranks_per_gpu: int | None = None) -> int:
-    """The channel count K a NCCL_ALGO=RING AllReduce is planned on (enqueue.cc ringParts: the communicator's
-    co-resident channel cap): NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS (default 256) capped at 2 workgroups per CU
-    divided by the ranks per GPU (init.cc computeChannelCap; every test rank shares the box's one GPU)."""
-    import torch
-    k = _env_int("NCCL_MAX_CTAS", _env_int("NCCL_MAX_NCHANNELS", 256))
-    k = max(1, min(k, 256))
-    cus = torch.cuda.get_device_properties(0).multi_processor_count
-    return max(1, min(k, 2 * cus // (ranks_per_gpu or n)))
+    """The channel count K a NCCL_ALGO=RING / NCCL_AMD_REF_ORDER AllReduce is planned on (enqueue.cc
+    refChannelCount): NCCL_AMD_REF_NCHANNELS when set, else the communicator's co-resident channel cap —
+    NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS (default 256) capped at 2 workgroups per CU divided by the ranks per GPU
+    (init.cc computeChannelCap; every test rank shares the box's one GPU) — and at most the reference's
+    MAXCHANNELS = 64 (src/include/device.h:91)."""
+    k = _env_int("NCCL_AMD_REF_NCHANNELS", 0)
+    if k <= 0:
+        import torch
+        k = _env_int("NCCL_MAX_CTAS", _env_int("NCCL_MAX_NCHANNELS", 256))
+        k = max(1, min(k, 256))
+        cus = torch.cuda.get_device_properties(0).multi_processor_count
+        k = max(1, min(k, 2 * cus // (ranks_per_gpu or n)))
+    return min(k, 64)
 
 
 def ring_runs(n: int) -> bool:

@@ -152,9 +152,11 @@ int main(int argc, char** argv) {
   const char* pipes[] = {"ring", "ring", "ring", "chain", "chain"};
   const LaunchPlan& p = gPlan;
   if (p.algo == ALGO_PIPE) {
-    printf("algo=%s kind=%d nch=%d part=%lu slice=%lu steps=%d chunk=%lu cbdlo=%lu cbdhi=%lu\n", pipes[p.pipeKind],
-           p.pipeKind, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps,
-           (unsigned long)p.args.chunk, (unsigned long)p.args.cbdLo, (unsigned long)p.args.cbdHi);
+    const unsigned sub = p.args.refSub ? p.args.refSub : 1;
+    printf("algo=%s kind=%d nch=%d part=%lu slice=%lu steps=%d chunk=%lu cbdlo=%lu cbdhi=%lu refnch=%d sub=%u\n",
+           pipes[p.pipeKind], p.pipeKind, p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice,
+           p.args.nSteps, (unsigned long)p.args.chunk, (unsigned long)p.args.cbdLo, (unsigned long)p.args.cbdHi,
+           p.nChannels / (int)sub, sub);
     return 0;
   }
   if (p.algo == ALGO_LL)
@@ -162,8 +164,9 @@ int main(int argc, char** argv) {
            p.nChannels, (unsigned long)p.ll.ops[0].part,
            (unsigned long)p.ll.ops[0].chunk);
   else
-    printf("algo=%s nch=%d part=%lu slice=%lu steps=%d chunk=%lu cbdlo=%lu cbdhi=%lu\n", names[p.algo], p.nChannels,
-           (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps, (unsigned long)p.args.chunk,
-           (unsigned long)p.args.cbdLo, (unsigned long)p.args.cbdHi);
+    printf("algo=%s nch=%d part=%lu slice=%lu steps=%d chunk=%lu cbdlo=%lu cbdhi=%lu refnch=%d sub=%u\n",
+           names[p.algo], p.nChannels, (unsigned long)p.args.part, (unsigned long)p.args.slice, p.args.nSteps,
+           (unsigned long)p.args.chunk, (unsigned long)p.args.cbdLo, (unsigned long)p.args.cbdHi,
+           p.nChannels / (int)(p.args.refSub ? p.args.refSub : 1), p.args.refSub ? p.args.refSub : 1);
   return 0;
 }

@@ -201,10 +201,13 @@ REF_GRAPH_ENVS = [
     {"NCCL_AMD_REF_ORDER": "1", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "6"},
     {"NCCL_ALGO": "RING", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "6"},
     {"NCCL_AMD_REF_ORDER": "1", "NCCL_PROTO": "LL", "NCCL_LL_BUFFSIZE": "65536", "NCCL_MAX_CTAS": "6"},
+    # reference parts shared by several workgroups (CollArgs::refSub)
+    {"NCCL_AMD_REF_ORDER": "1", "NCCL_BUFFSIZE": "16384", "NCCL_AMD_REF_NCHANNELS": "6",
+     "NCCL_AMD_MIN_CHANNEL_BYTES": "1024"},
 ]
 
 
-@pytest.mark.parametrize("env", REF_GRAPH_ENVS, ids=["reforder", "ring", "reforder-ll"])
+@pytest.mark.parametrize("env", REF_GRAPH_ENVS, ids=["reforder", "ring", "reforder-ll", "reforder-sub"])
 def test_hipgraph_reference_order_allreduce(built, env):
     """The reference-partition AllReduces (NCCL_AMD_REF_ORDER's direct kernel, the ring) captured in one hipGraph per
     rank — 3 ranks, bf16 (every hop rounds, so the fold order shows) at sizes spanning one and many channel parts
@@ -213,7 +216,8 @@ def test_hipgraph_reference_order_allreduce(built, env):
     import torch
     import nccl_amd
     from tests import gpu_cases as G
-    keys = ("NCCL_AMD_REF_ORDER", "NCCL_BUFFSIZE", "NCCL_MAX_CTAS", "NCCL_ALGO", "NCCL_PROTO", "NCCL_LL_BUFFSIZE")
+    keys = ("NCCL_AMD_REF_ORDER", "NCCL_BUFFSIZE", "NCCL_MAX_CTAS", "NCCL_ALGO", "NCCL_PROTO", "NCCL_LL_BUFFSIZE",
+            "NCCL_AMD_REF_NCHANNELS", "NCCL_AMD_MIN_CHANNEL_BYTES")
     saved = {k: os.environ.get(k) for k in keys}
     for k in keys:
         os.environ.pop(k, None)

@@ -102,6 +102,14 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             # ring itself, and the direct kernel walking the same partition (NCCL_AMD_REF_ORDER)
             (3, {"NCCL_ALGO": "RING", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "5"}),
             (3, {"NCCL_AMD_REF_ORDER": "1", "NCCL_BUFFSIZE": "16384", "NCCL_MAX_CTAS": "5"}),
+            # ... with each reference part shared by several workgroups (CollArgs::refSub; 1 KiB sub-chunks so the
+            # 8 KiB chunks split too): sub-chunk edges, ragged last loops, empty sub-chunks
+            (3, {"NCCL_ALGO": "RING", "NCCL_BUFFSIZE": "16384", "NCCL_AMD_REF_NCHANNELS": "5",
+                 "NCCL_AMD_MIN_CHANNEL_BYTES": "1024"}),
+            (3, {"NCCL_AMD_REF_ORDER": "1", "NCCL_BUFFSIZE": "16384", "NCCL_AMD_REF_NCHANNELS": "5",
+                 "NCCL_AMD_MIN_CHANNEL_BYTES": "1024"}),
+            (4, {"NCCL_AMD_REF_ORDER": "1", "NCCL_PROTO": "LL", "NCCL_LL_BUFFSIZE": "65536",
+                 "NCCL_AMD_REF_NCHANNELS": "3", "NCCL_AMD_MIN_CHANNEL_BYTES": "512"}),
             (4, {"NCCL_AMD_REF_ORDER": "1", "NCCL_AMD_SLOT_BYTES": "4096"}),
             # ... on the reference's RING/LL and RING/LL128 partitions (small protocol buffers: many parts and loops)
             (3, {"NCCL_AMD_REF_ORDER": "1", "NCCL_PROTO": "LL", "NCCL_LL_BUFFSIZE": "65536", "NCCL_MAX_CTAS": "6"}),

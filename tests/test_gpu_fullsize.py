@@ -204,12 +204,17 @@ def test_c3_reducescatter_allgather_bf16_1GiB_n8(built):
 
 
 C4_SIZES = [8, 4096 + 2, 64 << 10, (1 << 20) + 6, 16 << 20, 256 << 20]
+# The reference-partition columns run the reference's K = 32 channel parts, shared by several workgroups each
+# (NCCL_AMD_REF_NCHANNELS, the channel cap left at its default: CollArgs::refSub), and REFORDER_CAP32 with one
+# workgroup per part (NCCL_MAX_CTAS = 32).
 C4_ALGOS = {"LL": {"NCCL_PROTO": "LL"}, "ONESHOT": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
-            "DIRECT": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"}, "RING": {"NCCL_ALGO": "RING", "NCCL_MAX_CTAS": "32"},
-            "REFORDER": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32"},
+            "DIRECT": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
+            "RING": {"NCCL_ALGO": "RING", "NCCL_AMD_REF_NCHANNELS": "32"},
+            "REFORDER": {"NCCL_AMD_REF_ORDER": "1", "NCCL_AMD_REF_NCHANNELS": "32"},
+            "REFORDER_CAP32": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32"},
             # the reference's RING/LL and RING/LL128 partitions (the lower end of the curve), up to 16 MiB
-            "REFORDER_LL": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32", "NCCL_PROTO": "LL"},
-            "REFORDER_LL128": {"NCCL_AMD_REF_ORDER": "1", "NCCL_MAX_CTAS": "32", "NCCL_PROTO": "LL128"},
+            "REFORDER_LL": {"NCCL_AMD_REF_ORDER": "1", "NCCL_AMD_REF_NCHANNELS": "32", "NCCL_PROTO": "LL"},
+            "REFORDER_LL128": {"NCCL_AMD_REF_ORDER": "1", "NCCL_AMD_REF_NCHANNELS": "32", "NCCL_PROTO": "LL128"},
             "TREE": {"NCCL_ALGO": "TREE"}}
 C4_PROTO_MAX = 16 << 20
 
@@ -223,7 +228,7 @@ def _c4_worker(rank, nranks, uid, q, uids):
         s = torch.cuda.Stream()
         comms = {}
         for k, (name, env) in enumerate(C4_ALGOS.items()):  # knobs are read at init: one comm per column
-            for key in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MAX_CTAS", "NCCL_AMD_REF_ORDER"):
+            for key in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_MAX_CTAS", "NCCL_AMD_REF_ORDER", "NCCL_AMD_REF_NCHANNELS"):
                 os.environ.pop(key, None)
             os.environ.update(env)
             comms[name] = nccl_amd.Communicator.init(nranks, rank, uids[k])
@@ -251,7 +256,8 @@ def _c4_worker(rank, nranks, uid, q, uids):
                     break
                 errs += _cmp(f"C4 {name} {nbytes} B rank {rank}", recv.cpu().numpy().view(np.uint16),
                              want[name] if name in want else
-                             want["chain" if name == "TREE" else "ring" if name in ("RING", "REFORDER") else "direct"], 6)
+                             want["chain" if name == "TREE" else "ring" if name in ("RING", "REFORDER", "REFORDER_CAP32")
+                                  else "direct"], 6)
             if errs:
                 break
         for cm in comms.values():

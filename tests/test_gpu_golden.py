@@ -21,7 +21,7 @@ FIXTURES = sorted(glob.glob(os.path.join(HERE, "golden", "*.npz")))
 SETTINGS = [{}, {"NCCL_PROTO": "LL"}, {"NCCL_PROTO": "^LL", "NCCL_ALGO": "ONESHOT"},
             {"NCCL_PROTO": "^LL", "NCCL_ALGO": "DIRECT"}]
 KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_MAX_CTAS", "NCCL_BUFFSIZE", "NCCL_LL_BUFFSIZE", "NCCL_LL128_BUFFSIZE",
-         "NCCL_AMD_REF_ORDER")
+         "NCCL_AMD_REF_ORDER", "NCCL_AMD_REF_NCHANNELS", "NCCL_AMD_MIN_CHANNEL_BYTES")
 # the protocol a ring fixture's partition belongs to: its NCCL_PROTO value and buffer-size variable
 RING_PROTO = {"simple": ("Simple", "NCCL_BUFFSIZE"), "ll": ("LL", "NCCL_LL_BUFFSIZE"),
               "ll128": ("LL128", "NCCL_LL128_BUFFSIZE")}
@@ -39,12 +39,18 @@ def _fixtures(n):
 def _ring_settings(z):
     """NCCL_ALGO=RING fixtures (the reference's full-size ring partition) run on communicators of the fixture's
     channel count and protocol buffer size only, with NCCL_PROTO naming the fixture's protocol: the ring kernel
-    (NCCL_ALGO=RING) and the direct kernel on the same partition (NCCL_AMD_REF_ORDER=1)."""
+    (NCCL_ALGO=RING) and the direct kernel on the same partition (NCCL_AMD_REF_ORDER=1) — once with one workgroup
+    per reference part (NCCL_MAX_CTAS = K) and once with the parts shared by several workgroups (K given as
+    NCCL_AMD_REF_NCHANNELS, the channel cap left at its default, 1 KiB sub-chunks allowed so the fixtures' small
+    chunks split too; CollArgs::refSub)."""
     proto, var = RING_PROTO[str(z["proto"]) if "proto" in z else "simple"]
-    common = {"NCCL_MAX_CTAS": str(int(z["nchannels"]))}
-    if int(z["buffsize"]):
-        common[var] = str(int(z["buffsize"]))
-    return [dict(common, NCCL_ALGO="RING", NCCL_PROTO=proto), dict(common, NCCL_AMD_REF_ORDER="1", NCCL_PROTO=proto)]
+    k = str(int(z["nchannels"]))
+    buff = {var: str(int(z["buffsize"]))} if int(z["buffsize"]) else {}
+    out = []
+    for common in ({"NCCL_MAX_CTAS": k}, {"NCCL_AMD_REF_NCHANNELS": k, "NCCL_AMD_MIN_CHANNEL_BYTES": "1024"}):
+        common = dict(common, **buff)
+        out += [dict(common, NCCL_ALGO="RING", NCCL_PROTO=proto), dict(common, NCCL_AMD_REF_ORDER="1", NCCL_PROTO=proto)]
+    return out
 
 
 def _worker(rank, n, uids, q):

@@ -267,9 +267,9 @@ def test_reference_order_direct_allreduce(exe, built):
         if buff:
             env["NCCL_BUFFSIZE"] = buff
         p = plan(exe, n, "ar", dt, count, chancap=k, **env)
-        want = oracle.ring_nccl_plan(count, SIZES[dt], n, k, buff or 0)
+        want = oracle.ring_nccl_plan(count, SIZES[dt], n, min(k, 64), buff or 0)
         assert p["algo"] == "direct", p
-        assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (n, dt, count, k, buff, p)
+        assert (p["refnch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (n, dt, count, k, buff, p)
         assert 0 < p["slice"] <= p["chunk"]
     # NCCL_PROTO naming LL or LL128 alone: that protocol's ring partition (its cells, channel shrink and chunk, with
     # NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE), still on the direct kernel (no LL kernel in this mode)
@@ -286,16 +286,16 @@ def test_reference_order_direct_allreduce(exe, built):
                     if buff:
                         env[var] = buff
                     p = plan(exe, n, "ar", dt, count, chancap=k, **env)
-                    want = oracle.ring_nccl_plan(count, SIZES[dt], n, k, buff or 0, pid)
+                    want = oracle.ring_nccl_plan(count, SIZES[dt], n, min(k, 64), buff or 0, pid)
                     assert p["algo"] == "direct", (proto, p)
-                    assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (proto, count, n, dt, k, buff, p)
+                    assert (p["refnch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (proto, count, n, dt, k, buff, p)
                     assert 0 < p["slice"] <= p["chunk"]
     # NCCL_ALGO=RING with LL or LL128 alone: the ring kernel on that protocol's partition (no LL kernel)
     for proto, pid in (("LL", oracle.PROTO_LL), ("LL128", oracle.PROTO_LL128)):
         for count in (1, 1000, 100_003, 1 << 22):
             p = plan(exe, 3, "ar", 7, count, chancap=7, NCCL_ALGO="RING", NCCL_PROTO=proto)
             assert p["algo"] == "ring", (proto, p)
-            assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == \
+            assert (p["refnch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == \
                 oracle.ring_nccl_plan(count, 4, 3, 7, 0, pid), (proto, count, p)
     assert plan(exe, 3, "ar", 7, 1000, NCCL_ALGO="RING", NCCL_PROTO="LL,LL128")["algo"] == "ll"
     assert plan(exe, 8, "rs", 7, 8 << 20, NCCL_AMD_REF_ORDER=1)["cbdlo"] == 0
@@ -320,7 +320,36 @@ def test_ring_allreduce_takes_the_reference_partition(exe, built):
                     if buff:
                         env["NCCL_BUFFSIZE"] = buff
                     p = plan(exe, n, "ar", dt, count, chancap=k, **env)
-                    want = oracle.ring_nccl_plan(count, SIZES[dt], n, k, buff or 0)
+                    want = oracle.ring_nccl_plan(count, SIZES[dt], n, min(k, 64), buff or 0)
                     assert p["algo"] == "ring", p
-                    assert (p["nch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (count, dt, n, k, buff)
+                    assert (p["refnch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == want, (count, dt, n, k, buff)
                     assert 0 < p["slice"] <= p["chunk"] and p["slice"] % (16 // SIZES[dt]) == 0
+
+
+def test_reference_partition_is_clamped_and_decoupled(exe, built):
+    """the reference never runs more than MAXCHANNELS = 64 channels (src/include/device.h:91),
+    so NCCL_AMD_REF_ORDER / NCCL_ALGO=RING walk at most 64 reference parts (NCCL_AMD_REF_NCHANNELS names the
+    reference run's K; the channel cap otherwise), and refSub workgroups share each part, so the launch fills the
+    channel cap whatever K is: K = 32 at 256 MiB fp32, n = 2 runs 32 parts x 8 workgroups = 256."""
+    import oracle
+    S = (256 << 20) // 4
+    for env in ({"NCCL_AMD_REF_ORDER": 1}, {"NCCL_ALGO": "RING"}):
+        p = plan(exe, 2, "ar", 7, S, **env)                                     # cap 256 -> K = 64
+        assert (p["refnch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == oracle.ring_nccl_plan(S, 4, 2, 64, 0)
+        assert p["sub"] == 4 and p["nch"] == 256
+        p = plan(exe, 2, "ar", 7, S, NCCL_AMD_REF_NCHANNELS=32, **env)          # the reference run's K = 32
+        assert (p["refnch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == oracle.ring_nccl_plan(S, 4, 2, 32, 0)
+        assert p["sub"] == 8 and p["nch"] == 256
+        p = plan(exe, 2, "ar", 7, S, NCCL_AMD_REF_NCHANNELS=200, **env)         # clamped
+        assert p["refnch"] == 64
+        p = plan(exe, 2, "ar", 7, S, chancap=32, **env)                          # NCCL_MAX_CTAS=32: 32 workgroups
+        assert p["refnch"] == 32 and p["sub"] == 1 and p["nch"] == 32
+    # small messages: no sub-chunk below the default plan's 16 KiB granularity, never more than the channel cap
+    for count in (1, 1000, 100_003, 1 << 20, 3_000_001):
+        for n in (2, 3, 8):
+            p = plan(exe, n, "ar", 7, count, NCCL_AMD_REF_ORDER=1, NCCL_AMD_REF_NCHANNELS=16)
+            assert p["nch"] == p["refnch"] * p["sub"] and 1 <= p["nch"] <= 256
+            ck = min(p["chunk"], -(-(max(p["cbdlo"], p["part"], p["cbdhi"]) // 1) // n))
+            assert p["sub"] == 1 or -(-ck // p["sub"]) * 4 >= (16 << 10) - 16, (count, n, p)
+            if n >= 3:  # the CU budget of the default plan at n >= 3
+                assert p["nch"] <= max(64, p["refnch"])
