@@ -16,13 +16,13 @@ EXTRA    ?=
 COMMON   := -O3 -fPIC -std=c++17 -ffp-contract=off -fvisibility=hidden -Wall -Wno-unused-function \
             -Wno-unused-variable -Wno-unused-but-set-variable -Iinclude $(EXTRA)
 HIPFLAGS := $(COMMON) --offload-arch=$(ARCH) -fno-gpu-flush-denormals-to-zero -munsafe-fp-atomics
-HOSTSRC  := debug.cc bootstrap.cc ipc.cc transport.cc init.cc group.cc enqueue.cc register.cc tuner.cc
+HOSTSRC  := debug.cc bootstrap.cc ipc.cc transport.cc init.cc group.cc enqueue.cc register.cc tuner.cc mapcheck.cc
 HOSTOBJ  := $(HOSTSRC:%.cc=$(BUILD)/%.o)
 DEVSRC   := $(notdir $(wildcard $(SRCDIR)/*.hip))
 DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
-all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test xgmi-probe atomicity-probe \
+all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test mapcheck-test xgmi-probe atomicity-probe \
      fp8-probe
 
 lib: $(LIBDIR)/libnccl.so
@@ -161,3 +161,12 @@ tests/native/fp8_cvt_probe: tests/native/fp8_cvt_probe.hip $(SRCDIR)/numerics.h
 	$(HIPCC) -O3 --offload-arch=$(ARCH) -ffp-contract=off -fno-gpu-flush-denormals-to-zero -o $@ $<
 
 .PHONY: fp8-probe
+
+# CPU test driver of the init-time mapping check (mapcheck.cc) with the device and the imports stubbed
+mapcheck-test: tests/native/mapcheck_test
+
+tests/native/mapcheck_test: tests/native/mapcheck_test.cc $(SRCDIR)/mapcheck.cc $(SRCDIR)/debug.cc $(HDRS)
+	$(CXX) -O1 -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ tests/native/mapcheck_test.cc \
+	  $(SRCDIR)/mapcheck.cc $(SRCDIR)/debug.cc -lpthread
+
+.PHONY: mapcheck-test

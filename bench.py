@@ -672,6 +672,7 @@ def main(argv=None):
     ms_per_step = wall / args.steps * 1e3
     value, algbw, busbw = rates(n, S, ms_per_step)
     hbm_bytes = hbm_bytes_per_rank("allreduce", n, S)
+    probe_links = n > 1 and torch.cuda.device_count() >= n  # ranks on separate GPUs: links exist to measure
     # the dominant (only) kernel of a step: the first one this process launched (warm-up of the same call)
     kernels = launched_kernels(klog)
     kname = kernels[0] if kernels else None
@@ -694,7 +695,7 @@ def main(argv=None):
         meas = None
         # ranks on separate GPUs: a real xGMI measurement, taken while every rank waits at a host barrier
         # (no peer kernel spinning on its GPU or moving bytes over the links during the probe)
-        probe = torch.cuda.device_count() >= n
+        probe = probe_links
         if probe:
             barrier()
         if rank == 0 and probe:
@@ -770,6 +771,29 @@ def main(argv=None):
             cpu = {"value": None, "error": repr(e)}
     barrier()
 
+    def link_summary():
+        """N > 1, top level: GPU 0's per-link rates (the roofline's probe) and the staged
+        AllReduce with the release fence forced on / off (the suite's staged_tuning columns), each checked bitwise
+        against the default column — the cross-device evidence that decides the fence default."""
+        out = {}
+        if n > 1:
+            pr = roof.get("probe") or {}
+            out["xgmi_links"] = ({"wt_uncached_write_per_link_GBps": pr.get("wt_uncached_write_per_link_GBps"),
+                                  "read_per_link_GBps": pr.get("read_per_link_GBps"),
+                                  "wt_uncached_write_fanout_GBps": pr.get("wt_uncached_write_fanout_GBps"),
+                                  "source": "tests/native/xgmi_probe on rank 0 (GPU 0 -> each peer GPU)"}
+                                 if pr else {"skipped": "the ranks share one GPU: no link to measure"})
+            runs = {json.dumps(r["env"], sort_keys=True): r for r in extra.get("suite", {}).get("staged_tuning", {}).get("runs", [])}
+            on = runs.get(json.dumps({"NCCL_AMD_P2P_FENCE": "1"}, sort_keys=True))
+            off = runs.get(json.dumps({"NCCL_AMD_P2P_FENCE": "0"}, sort_keys=True))
+            dflt = runs.get(json.dumps("default"))
+            out["p2p_fence"] = ({"fence_on_ms": on["ms"], "fence_off_ms": off["ms"], "default_ms": dflt["ms"] if dflt else None,
+                                 "default_fence": "on" if probe_links else "off (every rank on one GPU)",
+                                 "check": "pass" if on["check"].startswith("pass") and off["check"].startswith("pass")
+                                 else "FAIL", "source": "suite.staged_tuning"}
+                                if on and off else {"skipped": "suite not run"})
+        return out
+
     def headline():
         return {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": n, "steps": args.steps,
@@ -783,7 +807,7 @@ def main(argv=None):
                                             "1450-1492, the nccl-tests figure); busbw_sum_GBps = N x busBW")},
             "algbw_GBps": round(algbw, 2), "busbw_GBps": round(busbw, 2),
             **({"busbw_sum_GBps": round(n * busbw, 2)} if n > 1 else {}),
-            "roofline": roof, "cpu_baseline": cpu, "check": "pass" if ok else "FAIL", **extra,
+            "roofline": roof, "cpu_baseline": cpu, "check": "pass" if ok else "FAIL", **link_summary(), **extra,
         }
 
     if n > 1 and not args.no_suite:

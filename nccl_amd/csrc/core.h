@@ -280,6 +280,7 @@ struct ncclComm {
   uint32_t* hostAbort = nullptr;         // pinned, mapped: host→device abort flag
   uint32_t* hostError = nullptr;         // pinned, mapped: device→host error word
   size_t stagingAllocBytes = 0, flagsAllocBytes = 0, countersAllocBytes = 0;  // as allocated (ncclCommMemStats)
+  size_t probeOffset = 0;  // mapping-check area in the flag allocation (mapcheck.cc), same on every rank
   size_t slotBytes = 0;
   int nSlots = 0;
   int maxChannels = 0;
@@ -327,6 +328,28 @@ ncclResult_t transportFree(ncclComm* comm);
 ncclResult_t transportDrainCredits(ncclComm* comm);  // wait for acks peers still owe (destroy)
 ncclResult_t commAllocDevState(ncclComm* comm);  // counters, DevComm upload, abort/error words
 size_t commDeviceBytes(const ncclComm* comm);     // device memory held (ncclCommMemStats)
+
+// ---------------------------------------------------------------- mapping check (mapcheck.cc)
+// At init, every rank writes a pattern into every peer's staging slab and flag block THROUGH its mapping of them and
+// reads back the peers' own patterns the same way; a mapping that does not carry the bytes fails the init with
+// ncclSystemError naming the device pair, the allocation, the direction and the import path.
+constexpr size_t kMapProbeBytes = 2 * NCCL_AMD_MAX_RANKS * 16;
+uint64_t mapCheckWord(uint64_t nonce, int kind, int src, int dst, int half);  // expected word (kind: 0 staging, 1 flags)
+struct MapCheckObs {
+  // got[kind][peer][half]: written by `peer` into MY allocation (dir 0), read by me from peer's (dir 1)
+  uint64_t wrote[2][NCCL_AMD_MAX_RANKS][2];
+  uint64_t read[2][NCCL_AMD_MAX_RANKS][2];
+};
+struct MapCheckPeer {  // how this rank reaches peer r (for the message)
+  int device;
+  char busId[32];
+  const char* path;    // how this rank maps r's memory: same-GPU pointer, peer pointer, dma-buf import, hipIpc handle
+  const char* pathIn;  // how r maps this rank's memory (as far as this rank knows: what it exported)
+};
+// The failures of one rank's observations, one line each ("" = every mapping carried the patterns).
+std::string mapCheckVerify(int me, int nRanks, uint64_t nonce, const MapCheckObs& obs, const MapCheckPeer* peers);
+ncclResult_t mapCheck(const std::vector<ncclComm*>& comms);  // the check for these local comms (init.cc)
+ncclResult_t launchMapCheck(const DevComm* dc, const MapCheckArgs& a, uint64_t* out, hipStream_t stream);  // kernels.hip
 
 // ---------------------------------------------------------------- enqueue (reference src/enqueue.cc)
 enum CollFunc { FUNC_ALLREDUCE = 0, FUNC_REDUCESCATTER = 1, FUNC_ALLGATHER = 2, FUNC_REDUCE = 3 };

@@ -179,6 +179,14 @@ struct SymArgs {
   int relFence;        // publish with a system release fence even after write-through stores (across devices)
 };
 
+// Mapping check at communicator init (mapcheck.cc, kernels.hip mapCheckKernel): the words this rank stores into
+// peer p's staging slab (w[p][0]) and flag block (w[p][1]) through its mappings of them.
+struct MapCheckArgs {
+  uint64_t w[NCCL_AMD_MAX_RANKS][2][2];
+  uint64_t probeOff;  // the check area inside every rank's flag allocation (same offset everywhere)
+  int skip;           // tests (NCCL_AMD_MAPCHECK_FAULT): no stores, as a mapping that drops them
+};
+
 __host__ __device__ inline uint64_t stagingOffset(const DevComm& dc, int c, int kind, int slot, int from) {
   return ((((uint64_t)c * STG_KINDS + kind) * dc.nSlots + slot) * dc.nRanks + from) * dc.slotBytes;
 }

@@ -222,6 +222,8 @@ static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id
   TRACE("rank %d: peers mapped", rank);
   if ((res = commAllocDevState(comm)) != ncclSuccess) goto fail;
   TRACE("rank %d: device state ready", rank);
+  // every peer mapping carries bytes both ways before the first collective (mapcheck.cc; all ranks fail together)
+  if ((res = mapCheck({comm})) != ncclSuccess) goto fail;
   if ((res = tunerLoad(comm)) != ncclSuccess) goto fail;
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
   unexportHandles(comm);  // every peer has mapped our slab and flags
@@ -405,6 +407,7 @@ NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
     if (res == ncclSuccess) res = commAllocDevState(cs[i]);
     if (res == ncclSuccess) res = tunerLoad(cs[i]);
   }
+  if (res == ncclSuccess) res = mapCheck(cs);  // every peer pointer carries bytes both ways (mapcheck.cc)
   (void)hipSetDevice(oldDev);
   if (res != ncclSuccess) {
     for (auto* c : cs)

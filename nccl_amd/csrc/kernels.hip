@@ -147,6 +147,42 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
   return ncclSuccess;
 }
 
+// ------------------------------------------------------------------------------------ mapping check (mapcheck.cc)
+
+// One wave: lane p (a peer) stores the pattern (me -> p) into p's staging slot [0][RS][0][me] and flag probe row 0
+// [me] through this rank's mapping of p — 16-byte system-scope write-through stores, the collective kernels' own
+// remote-store flavour — and loads p's self patterns (staging slot [0][AG][0][p], probe row 1) through the same
+// mappings, with the flag loads' system scope, into out[p][0..3]. skip (tests): no remote stores, as a mapping that
+// drops them would.
+__global__ void __launch_bounds__(64) mapCheckKernel(const DevComm* dcp, MapCheckArgs a, uint64_t* out) {
+  const DevComm& dc = *dcp;
+  const int p = threadIdx.x, me = dc.rank;
+  if (p < dc.nRanks && p != me) {
+    const uint64_t slotW = stagingOffset(dc, 0, STG_RS, 0, me), slotR = stagingOffset(dc, 0, STG_AG, 0, p);
+    char* fl = (char*)dc.flags[p] + a.probeOff;
+    if (!a.skip) {
+      u32x4 v0, v1;
+      __builtin_memcpy(&v0, a.w[p][0], 16);
+      __builtin_memcpy(&v1, a.w[p][1], 16);
+      storeRemote(dc.staging[p] + slotW, v0);
+      storeRemote(fl + (size_t)me * 16, v1);
+    }
+    const uint64_t* rs = (const uint64_t*)(dc.staging[p] + slotR);
+    const uint64_t* rf = (const uint64_t*)(fl + NCCL_AMD_MAX_RANKS * 16);
+    out[p * 4 + 0] = loadFlag(rs);
+    out[p * 4 + 1] = loadFlag(rs + 1);
+    out[p * 4 + 2] = loadFlag(rf);
+    out[p * 4 + 3] = loadFlag(rf + 1);
+  }
+  drainStores();
+}
+
+ncclResult_t launchMapCheck(const DevComm* dc, const MapCheckArgs& a, uint64_t* out, hipStream_t stream) {
+  NCCL_AMD_LAUNCH(mapCheckKernel, dim3(1), dim3(64), 0, stream, dc, a, out);
+  HIPCHECK(hipGetLastError());
+  return ncclSuccess;
+}
+
 ncclResult_t launchPlan(const LaunchPlan& p) {
   if (p.algo == ALGO_COPY)
     return launchCopy(p.args.recvbuff, p.args.sendbuff, p.bytes, p.stream, p.copyVariant, p.copyGrid);

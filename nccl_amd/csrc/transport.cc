@@ -27,9 +27,11 @@ static size_t flagWordBytes(const ncclComm* c) {
 static size_t llOffset(const ncclComm* c) { return (flagWordBytes(c) + 4095) / 4096 * 4096; }
 // LL area, then the LL64 area of the same geometry (device_abi.h)
 static size_t ll64Offset(const ncclComm* c) { return llOffset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes; }
-static size_t flagsBytes(const ncclComm* c) {
-  return ll64Offset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes;
+// then the mapping-check area (mapcheck.cc): 2 rows x NCCL_AMD_MAX_RANKS x 16 bytes, used once at init
+static size_t probeOffset(const ncclComm* c) {
+  return (ll64Offset(c) + (size_t)c->llChannels * 2 * c->nRanks * c->llBytes + 255) / 256 * 256;
 }
+static size_t flagsBytes(const ncclComm* c) { return probeOffset(c) + kMapProbeBytes; }
 
 // Device memory this communicator holds on its GPU (ncclCommMemStats): staging slab, flag/LL lines,
 // step counters and the device copy of DevComm. All of it lives as long as the communicator.
@@ -61,6 +63,7 @@ ncclResult_t transportSetup(ncclComm* comm) {
     comm->stagingAllocBytes = sb;
     HIPCHECK(hipExtMallocWithFlags((void**)&comm->flags, fb, hipDeviceMallocUncached));
     comm->flagsAllocBytes = fb;
+    comm->probeOffset = probeOffset(comm);  // (llChannels may be lowered later; the layout stays as allocated)
   }
   HIPCHECK(hipMemset(comm->flags, 0, fb));
   HIPCHECK(hipDeviceSynchronize());

@@ -6,6 +6,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include <string>
 #include <vector>
 
 #define CK(x)                                                                                   \
@@ -81,16 +82,18 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-  auto run = [&](bool write, int npeers, bool wt = false) -> double {
+  // first: the first peer (GPU 1 + first) of the npeers consecutive ones
+  auto run = [&](bool write, int npeers, bool wt = false, int first = 0) -> double {
     Targets t = {};
     t.n = npeers;
     for (int k = 0; k < npeers; k++) {
       char* mine = (char*)local2 + (size_t)k * bytes;
+      const int peer = 1 + first + k;
       if (write) {
         t.src[k] = (const u32x4*)mine;
-        t.dst[k] = (u32x4*)(wt ? ubuf[1 + k] : buf[1 + k]);
+        t.dst[k] = (u32x4*)(wt ? ubuf[peer] : buf[peer]);
       } else {
-        t.src[k] = (const u32x4*)buf[1 + k];
+        t.src[k] = (const u32x4*)buf[peer];
         t.dst[k] = (u32x4*)mine;
       }
     }
@@ -120,10 +123,22 @@ int main(int argc, char** argv) {
   double r1 = run(false, 1), ra = run(false, all);
   // the collective's own store flavour: write-through system-scope stores into uncached peer memory
   double u1 = run(true, 1, true), ua = run(true, all, true);
+  // every link of GPU 0 on its own (GPU 0 -> GPU d): the collective's store flavour and plain reads; a slow or
+  // missing link shows here before it shows as a slow collective
+  std::string wl = "[", rl = "[";
+  char num[32];
+  for (int k = 0; k < all; k++) {
+    snprintf(num, sizeof(num), "%s%.1f", k ? ", " : "", run(true, 1, true, k));
+    wl += num;
+    snprintf(num, sizeof(num), "%s%.1f", k ? ", " : "", run(false, 1, false, k));
+    rl += num;
+  }
+  wl += "]";
+  rl += "]";
   printf("{\"method\": \"CU copy kernel on GPU 0, 16-byte nontemporal vectors, %zu MiB per peer, %d iters%s\", "
          "\"peers\": %d, \"write_1link_GBps\": %.1f, \"read_1link_GBps\": %.1f, \"write_fanout_GBps\": %.1f, "
          "\"read_fanin_GBps\": %.1f, \"wt_uncached_write_1link_GBps\": %.1f, \"wt_uncached_write_fanout_GBps\": %.1f, "
-         "\"wrong_bytes\": %zu}\n", mib, iters, loop ? ", LOOPBACK on one GPU" : "",
-         all, w1, r1, wa, ra, u1, ua, wrong);
+         "\"wt_uncached_write_per_link_GBps\": %s, \"read_per_link_GBps\": %s, \"wrong_bytes\": %zu}\n",
+         mib, iters, loop ? ", LOOPBACK on one GPU" : "", all, w1, r1, wa, ra, u1, ua, wl.c_str(), rl.c_str(), wrong);
   return wrong ? 1 : 0;
 }

@@ -50,6 +50,9 @@ def test_bench_two_ranks_quick(built):
     assert s["registered"]["check"].startswith("pass")
     assert all(r["check"].startswith("pass") for r in s["staged_tuning"]["runs"]), s["staged_tuning"]
     assert s["group_aggregation"]["aggregated_us_per_group"] > 0
+    # the link probe and the fence on / off column at the top level of the N > 1 line
+    assert "xgmi_links" in d and d["p2p_fence"]["check"] == "pass", (d.get("xgmi_links"), d.get("p2p_fence"))
+    assert d["p2p_fence"]["fence_on_ms"] > 0 and d["p2p_fence"]["fence_off_ms"] > 0
 
 
 def test_bench_one_gpu_line(built):

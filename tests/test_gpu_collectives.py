@@ -661,3 +661,67 @@ def test_forced_ring_and_tree(built, algo, nranks, monkeypatch):
         if errs:
             break
     assert not errs, "\n".join(errs[:20])
+
+
+def _mapcheck_worker(rank, nranks, uid, q, fault_rank):
+    try:
+        logf = f"/tmp/nccl_amd_mapcheck_{os.getpid()}.log"
+        os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_FILE=logf, NCCL_AMD_SPIN_TIMEOUT_MS="20000")
+        if rank == fault_rank:
+            os.environ["NCCL_AMD_MAPCHECK_FAULT"] = "1"
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        try:
+            comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        except nccl_amd.NcclError as e:
+            text = open(logf).read() if os.path.exists(logf) else ""
+            q.put((rank, ("error", e.code, str(e) + "\n" + text)))
+            return
+        from tests import gpu_cases as G
+        errs = G.run_case([(comm, torch.cuda.Stream())], "allreduce", 7, 0, 100_001, 0, seed=3)
+        comm.destroy()
+        text = open(logf).read() if os.path.exists(logf) else ""
+        q.put((rank, ("ok", "peer mappings verified" in text, errs)))
+    except Exception as e:
+        q.put((rank, ("exception", repr(e), [])))
+
+
+@pytest.mark.parametrize("fault_rank", [-1, 2])
+def test_mapping_check_at_init(built, fault_rank):
+    """every communicator init stores a pattern through each peer mapping (staging and flags, the
+    kernels' own write-through store) and loads the peers' patterns back before the first collective. Same-device
+    here (every rank on the box's one GPU over dma-buf imports); with NCCL_AMD_MAPCHECK_FAULT=1 on rank 2 (its stores
+    dropped, as a broken mapping would) every rank's init fails together with ncclSystemError within seconds, the
+    ranks that saw it naming rank 2 and the failing allocation (the failure branches: tests/test_mapcheck.py)."""
+    import queue
+    import time
+    _torch()
+    import nccl_amd
+    uid = nccl_amd.get_unique_id()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_mapcheck_worker, args=(r, 3, uid, q, fault_rank)) for r in range(3)]
+    t0 = time.time()
+    for p in ps:
+        p.start()
+    res = {}
+    while len(res) < 3 and time.time() - t0 < 240:
+        try:
+            r, out = q.get(timeout=30)
+            res[r] = out
+        except queue.Empty:
+            if not any(p.is_alive() for p in ps):
+                break
+    for p in ps:
+        if p.is_alive():
+            p.kill()
+        p.join(timeout=60)
+    assert len(res) == 3, res
+    if fault_rank < 0:
+        assert all(o[0] == "ok" and o[1] and not o[2] for o in res.values()), res
+    else:
+        assert all(o[0] == "error" and o[1] == 2 for o in res.values()), res
+        for r in (0, 1):
+            assert f"rank 2 (device 0" in res[r][2] and "did not arrive" in res[r][2], res[r]
+        assert time.time() - t0 < 120

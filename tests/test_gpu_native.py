@@ -43,6 +43,9 @@ def test_xgmi_probe_loopback(built):
     assert out.returncode == 0, out.stdout + out.stderr
     rep = json.loads(out.stdout.strip().splitlines()[-1])
     assert rep["wrong_bytes"] == 0 and rep["write_fanout_GBps"] > 0
+    # one rate per link of GPU 0 (the bench line's xgmi_links at N > 1)
+    assert len(rep["wt_uncached_write_per_link_GBps"]) == rep["peers"] == len(rep["read_per_link_GBps"])
+    assert all(x > 0 for x in rep["wt_uncached_write_per_link_GBps"] + rep["read_per_link_GBps"])
 
 
 def test_store_atomicity_probe_one_gpu(built):

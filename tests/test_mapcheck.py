@@ -1,0 +1,68 @@
+"""CPU tests of the init-time mapping check (nccl_amd/csrc/mapcheck.cc) with the device and the
+imports stubbed (tests/native/mapcheck_test: ranks in host memory, the check kernel emulated, faults injected where
+a real mapping could go wrong). A clean set of mappings passes; a mapping that points at other memory, stores that
+never arrive, or a hipIpc-fallback mapping that fails make the init return ncclSystemError (2) with one WARN line
+per failing (pair, allocation, direction) naming both devices' bus ids and the import path."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "tests", "native", "mapcheck_test")
+
+
+@pytest.fixture(scope="module")
+def exe():
+    src = os.path.join(ROOT, "tests", "native", "mapcheck_test.cc")
+    if not os.path.exists(EXE) or os.path.getmtime(EXE) < os.path.getmtime(src):
+        subprocess.check_call(["make", "mapcheck-test"], cwd=ROOT, stdout=subprocess.DEVNULL)
+    return EXE
+
+
+def run(exe, n, *faults):
+    env = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_")}
+    env["NCCL_DEBUG"] = "WARN"
+    out = subprocess.run([exe, str(n), *faults], env=env, capture_output=True, text=True, timeout=30)
+    assert out.returncode == 0, out.stdout + out.stderr
+    res = int(re.search(r"result=(\d+)", out.stdout).group(1))
+    warns = [l.split("NCCL WARN ", 1)[1] for l in out.stderr.splitlines() if "NCCL WARN mapping check" in l]
+    return res, warns
+
+
+@pytest.mark.parametrize("n", [2, 3, 8, 16])
+def test_clean_mappings_pass(exe, n):
+    assert run(exe, n) == (0, [])
+    assert run(exe, n, "samepid") == (0, [])
+
+
+def test_wrong_staging_mapping_names_both_directions(exe):
+    res, warns = run(exe, 3, "wrongmap:1:2:0")
+    assert res == 2 and len(warns) == 2, warns
+    load = [w for w in warns if "<-" in w]
+    store = [w for w in warns if "->" in w]
+    assert load and "rank 1 (device 1, 0000:11:00.0) <- rank 2 (device 2, 0000:12:00.0)" in load[0]
+    assert "staging slab" in load[0] and "dma-buf import" in load[0] and "5a5a5a5a5a5a5a5a" in load[0]
+    assert store and "rank 1 (device 1, 0000:11:00.0) -> rank 2 (device 2, 0000:12:00.0)" in store[0]
+    assert "did not arrive" in store[0]
+
+
+def test_flag_block_mapping_and_hipipc_path(exe):
+    res, warns = run(exe, 4, "legacy:0:1", "wrongmap:0:1:1")
+    assert res == 2
+    assert any("<- rank 1" in w and "flag block" in w and "hipIpc handle" in w for w in warns), warns
+    assert not any("staging slab" in w for w in warns), warns
+
+
+def test_dropped_stores_fail_every_peer(exe):
+    res, warns = run(exe, 4, "skip:3")
+    assert res == 2
+    pairs = {(m.group(1), m.group(2)) for w in warns for m in [re.search(r"rank (\d+) \(device.*?-> rank (\d+)", w)] if m}
+    assert pairs == {("3", "0"), ("3", "1"), ("3", "2")}, warns
+    assert len(warns) == 6  # staging + flags for each of the 3 peers
+
+
+def test_single_process_peer_pointer_path(exe):
+    res, warns = run(exe, 2, "samepid", "wrongmap:0:1:0")
+    assert res == 2 and all("hipDeviceEnablePeerAccess" in w for w in warns), warns
