@@ -288,18 +288,19 @@ struct RingParts {
 };
 // The reference never runs more than MAXCHANNELS = 64 channels (src/include/device.h:91), so a partition of
 // more parts than that is one no reference run produces: K = NCCL_AMD_REF_NCHANNELS, else the channel cap, and
-// at most 64 (warned once when a larger count is clamped).
+// at most 64 (warned once when a larger count is clamped). Every part needs a workgroup of its own, so K never
+// exceeds the channel cap either (several ranks per GPU, NCCL_MAX_CTAS): the staging holds that many channels.
 constexpr int kRefMaxChannels = 64;
 static int refChannelCount(ncclComm* comm) {
   const int want = comm->tune.refChannels > 0 ? comm->tune.refChannels : comm->chanCap;
-  if (want <= kRefMaxChannels) return want < 1 ? 1 : want;
-  if (!comm->warnedRefClamp) {
+  const int k = std::max(1, std::min(want, std::min(kRefMaxChannels, comm->chanCap)));
+  if (k != want && !comm->warnedRefClamp && want >= 1) {
     comm->warnedRefClamp = true;
-    WARN("the reference's partition has at most %d channels (MAXCHANNELS, device.h:91): %s %d -> %d; set "
-         "NCCL_AMD_REF_NCHANNELS to the reference run's channel count", kRefMaxChannels,
-         comm->tune.refChannels > 0 ? "NCCL_AMD_REF_NCHANNELS" : "channel cap", want, kRefMaxChannels);
+    WARN("the reference's partition is cut into %d channel parts, not %d (%s): at most %d (MAXCHANNELS, device.h:91) "
+         "and at most the channel cap %d; set NCCL_AMD_REF_NCHANNELS to the reference run's channel count", k, want,
+         comm->tune.refChannels > 0 ? "NCCL_AMD_REF_NCHANNELS" : "the channel cap", kRefMaxChannels, comm->chanCap);
   }
-  return kRefMaxChannels;
+  return k;
 }
 static RingParts ringParts(uint64_t count, int ts, int K, int n, int proto) {
   const uint64_t bytes = count * (uint64_t)ts;
@@ -715,6 +716,19 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   return ncclSuccess;
 }
 
+// Host-side guard before any channel kernel launches: its grid never exceeds the channels the staging slab, flag
+// block and counters were allocated for, nor the co-resident cap (a kernel indexing past them would fault the GPU).
+static ncclResult_t checkGrid(const ncclComm* comm, int kind, const LaunchPlan& p, const SymPlan& sp) {
+  int grid = 0, cap = comm->chanCap;
+  if (kind == PLAN_SYM) grid = sp.nChannels;
+  else if (p.algo == ALGO_LL) grid = p.nChannels, cap = std::min(cap, comm->llChannels);
+  else if (p.algo == ALGO_DIRECT || p.algo == ALGO_ONESHOT || p.algo == ALGO_PIPE) grid = p.nChannels;
+  else return ncclSuccess;  // one-rank kernels: no channels
+  if (grid >= 1 && grid <= cap && grid <= comm->maxChannels) return ncclSuccess;
+  WARN("internal: a plan of %d channels (cap %d, %d allocated) was refused before launch", grid, cap, comm->maxChannels);
+  return ncclInternalError;
+}
+
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   ncclComm* comm = info.comm;
   HIPCHECK(hipSetDevice(comm->device));
@@ -723,6 +737,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   int kind;
   NCCLCHECK(planColl(info, p, sp, &kind));
   if (kind == PLAN_NONE) return ncclSuccess;
+  NCCLCHECK(checkGrid(comm, kind, p, sp));
   // a comm sharing its GPU with other ranks of this process runs on its own hardware queue, between a fork
   // and a join (see ncclComm::internalStream)
   const bool shared =
@@ -777,6 +792,7 @@ ncclResult_t launchBatch(std::vector<PlannedColl>& run) {
   const bool shared =
       comm->sharedDevInProcess && !(run[0].kind == PLAN_KERNEL && (p.algo == ALGO_COPY || p.algo == ALGO_ONERANK));
   if (shared) p.stream = run[0].sp.stream = comm->internalStream;
+  for (const PlannedColl& x : run) NCCLCHECK(checkGrid(comm, x.kind, x.p, x.sp));
   if (run.size() == 1) return run[0].kind == PLAN_SYM ? launchSymPlan(run[0].sp) : launchPlan(p);
   if (p.algo == ALGO_LL) {
     int off = p.ll.ops[0].nch % comm->llChannels, used = p.ll.ops[0].nch;

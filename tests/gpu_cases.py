@@ -55,15 +55,14 @@ def ring_channels(n: int, ranks_per_gpu: int | None = None) -> int:
     refChannelCount): NCCL_AMD_REF_NCHANNELS when set, else the communicator's co-resident channel cap —
     NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS (default 256) capped at 2 workgroups per CU divided by the ranks per GPU
     (init.cc computeChannelCap; every test rank shares the box's one GPU) — and at most the reference's
-    MAXCHANNELS = 64 (src/include/device.h:91)."""
-    k = _env_int("NCCL_AMD_REF_NCHANNELS", 0)
-    if k <= 0:
-        import torch
-        k = _env_int("NCCL_MAX_CTAS", _env_int("NCCL_MAX_NCHANNELS", 256))
-        k = max(1, min(k, 256))
-        cus = torch.cuda.get_device_properties(0).multi_processor_count
-        k = max(1, min(k, 2 * cus // (ranks_per_gpu or n)))
-    return min(k, 64)
+    MAXCHANNELS = 64 (src/include/device.h:91) and the channel cap."""
+    import torch
+    cap = _env_int("NCCL_MAX_CTAS", _env_int("NCCL_MAX_NCHANNELS", 256))
+    cap = max(1, min(cap, 256))
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    cap = max(1, min(cap, 2 * cus // (ranks_per_gpu or n)))
+    k = _env_int("NCCL_AMD_REF_NCHANNELS", 0) or cap
+    return max(1, min(k, 64, cap))  # every part needs a workgroup: never more parts than the channel cap
 
 
 def ring_runs(n: int) -> bool:

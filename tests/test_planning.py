@@ -125,10 +125,18 @@ def test_plan_invariants(exe, n, func, dtype, count):
 
 
 def test_channel_cap(exe):
-    # several ranks per GPU: every channel of a launch must be co-resident, so plans respect chanCap
-    for cap in (1, 7, 64):
+    # several ranks per GPU: every channel of a launch must be co-resident, so plans respect chanCap — every
+    # algorithm, the reference-partition ones with any NCCL_AMD_REF_NCHANNELS included (the launch guard,
+    # enqueue.cc checkGrid, refuses a plan past the cap rather than index past the staging)
+    for cap in (1, 3, 7, 64):
         assert plan(exe, 4, "ar", 7, 64 << 20, chancap=cap)["nch"] <= cap
         assert plan(exe, 4, "ar", 7, 1000, chancap=cap, NCCL_PROTO="LL")["nch"] <= cap
+        for env in ({"NCCL_ALGO": "RING"}, {"NCCL_AMD_REF_ORDER": 1}, {"NCCL_ALGO": "TREE"}):
+            for k in (1, 5, 64, 100):
+                for count in (1000, 100_003, 1 << 22):
+                    p = plan(exe, 3, "ar", 7, count, chancap=cap, NCCL_AMD_REF_NCHANNELS=k,
+                             NCCL_AMD_MIN_CHANNEL_BYTES=1024, **env)
+                    assert 1 <= p["nch"] <= cap, (cap, env, k, count, p)
 
 
 def test_ll_channels_never_empty(exe):
@@ -344,6 +352,9 @@ def test_reference_partition_is_clamped_and_decoupled(exe, built):
         assert p["refnch"] == 64
         p = plan(exe, 2, "ar", 7, S, chancap=32, **env)                          # NCCL_MAX_CTAS=32: 32 workgroups
         assert p["refnch"] == 32 and p["sub"] == 1 and p["nch"] == 32
+        p = plan(exe, 3, "ar", 7, S, chancap=3, NCCL_AMD_REF_NCHANNELS=5, **env)  # a part per workgroup at least:
+        assert p["refnch"] == 3 and p["nch"] == 3                                 # K clamped to the channel cap
+        assert (p["refnch"], p["cbdlo"], p["part"], p["cbdhi"], p["chunk"]) == oracle.ring_nccl_plan(S, 4, 3, 3, 0)
     # small messages: no sub-chunk below the default plan's 16 KiB granularity, never more than the channel cap
     for count in (1, 1000, 100_003, 1 << 20, 3_000_001):
         for n in (2, 3, 8):
