@@ -149,290 +149,312 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     def _tm(fn, stream_, iters: int, warmup: int = 3) -> float:  # collectives: ranks aligned first (_time_ms)
         return _time_ms(fn, stream_, iters, warmup, align=dist.barrier)
 
-    trace("rs_ag_bf16")
-    # --- configs[2]: ZeRO bucket, bf16, 1 GiB ---
-    bucket = (64 if quick else 1024) * MIB
-    cnt = bucket // 2
+    # BENCH_SUITE_PARTS=a,b (diagnostics): only these parts, in the suite's fixed order
+    only = [x for x in os.environ.get("BENCH_SUITE_PARTS", "").split(",") if x]
+    want = lambda part: not only or part in only
     g = torch.Generator(device="cuda")
-    g.manual_seed(77)
-    base = torch.randint(-4, 5, (cnt,), device="cuda", generator=g, dtype=torch.int32).to(torch.bfloat16)
-    send = base * (rank + 1)
-    shard = torch.empty(cnt // n, dtype=torch.bfloat16, device="cuda")
-    full = torch.empty(cnt, dtype=torch.bfloat16, device="cuda")
-    rs = lambda: comm.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp)
-    ag = lambda: comm.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp)
-    ms_rs = tmax(_tm(rs, stream, 10))
-    ms_ag = tmax(_tm(ag, stream, 10))
-    rs()
-    ag()
-    torch.cuda.synchronize()
-    ok = bool(torch.equal(full, base * (n * (n + 1) // 2)))
-    bw = lambda ms: round(bucket / (ms * 1e-3) / 1e9 * (n - 1) / n, 2)
-    out["rs_ag_bf16"] = {"config": f"ncclReduceScatter + ncclAllGather bf16, {bucket // MIB} MiB bucket, n={n}",
-                         "rs_ms": round(ms_rs, 4), "rs_busbw_GBps": bw(ms_rs), "ag_ms": round(ms_ag, 4),
-                         "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(ok) else "FAIL"}
-    # the same with the pull variants of both phases (xGMI reads instead of writes), its own communicator
-    pulls = ("NCCL_AMD_RS_PULL", "NCCL_AMD_AG_PULL")
-    saved_p = {k: os.environ.get(k) for k in pulls}
-    os.environ.update({k: "1" for k in pulls})
-    cp = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
-    for k, v in saved_p.items():
-        os.environ.pop(k, None)
-        if v is not None:
-            os.environ[k] = v
-    ms_rs = tmax(_tm(lambda: cp.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp), stream, 10))
-    ms_ag = tmax(_tm(lambda: cp.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp), stream, 10))
-    full.zero_()
-    cp.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp)
-    cp.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp)
-    torch.cuda.synchronize()
-    okp = bool(torch.equal(full, base * (n * (n + 1) // 2)))
-    cp.destroy()
-    out["rs_ag_bf16"]["pull"] = {"rs_ms": round(ms_rs, 4), "rs_busbw_GBps": bw(ms_rs), "ag_ms": round(ms_ag, 4),
-                                 "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(okp) else "FAIL",
-                                 "env": "NCCL_AMD_RS_PULL=1 NCCL_AMD_AG_PULL=1"}
-    del send, shard, full, base
 
-    trace("ar_fp16_sweep")
-    # --- configs[3]: fp16 AllReduce sweep: LL vs one-shot vs direct. Protocol/algorithm knobs are read at
-    #     communicator init (like the reference's NCCL_PARAMs), so each column gets its own communicator ---
-    top = (16 if quick else 256) * MIB
-    buf = torch.empty(top // 2, dtype=torch.float16, device="cuda").uniform_(-1, 1)
-    res = torch.empty_like(buf)
-    cols = {"ll": {"NCCL_PROTO": "LL"}, "ll128": {"NCCL_PROTO": "LL128"},
-            "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
-            "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
-            "ring": {"NCCL_ALGO": "RING"}, "tree": {"NCCL_ALGO": "TREE"}, "default": {},
-            # the reference's RING/SIMPLE partition walked by the direct kernel: its cost vs default
-            "reforder": {"NCCL_AMD_REF_ORDER": "1"}}
-    limits = {"ll": 512 * 1024, "ll128": 896 * 1024, "oneshot": 64 * MIB}
-    rows = {}
-    saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION", "NCCL_AMD_REF_ORDER")}
-    for name, env in cols.items():  # ll128: the LL64-line protocol (64-byte lines)
-        for k in saved:
-            os.environ.pop(k, None)
-        os.environ.update(env)
-        cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
-        size = 8
-        while size <= top:
-            if size <= limits.get(name, top):
-                c = size // 2
-                it = 50 if size <= 4 * MIB else 10
-                ms = tmax(_tm(lambda: cm.all_reduce_raw(buf.data_ptr(), res.data_ptr(), c, 6, 0, sp), stream, it))
-                row = rows.setdefault(size, {"bytes": size})
-                row[name + "_us"] = round(ms * 1e3, 2)
-                row[name + "_busbw_GBps"] = round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)
-            size *= 2
+    if want("rs_ag_bf16"):
+        trace("rs_ag_bf16")
+        # --- configs[2]: ZeRO bucket, bf16, 1 GiB ---
+        bucket = (64 if quick else 1024) * MIB
+        cnt = bucket // 2
+        g.manual_seed(77)
+        base = torch.randint(-4, 5, (cnt,), device="cuda", generator=g, dtype=torch.int32).to(torch.bfloat16)
+        send = base * (rank + 1)
+        shard = torch.empty(cnt // n, dtype=torch.bfloat16, device="cuda")
+        full = torch.empty(cnt, dtype=torch.bfloat16, device="cuda")
+        rs = lambda: comm.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp)
+        ag = lambda: comm.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp)
+        ms_rs = tmax(_tm(rs, stream, 10))
+        ms_ag = tmax(_tm(ag, stream, 10))
+        rs()
+        ag()
         torch.cuda.synchronize()
-        cm.destroy()
-    out["ar_fp16_sweep"] = [rows[k] for k in sorted(rows)]
-
-    trace("group_aggregation")
-    # --- group aggregation: 32 small AllReduce ops in one ncclGroupStart/End,
-    #     one LL launch vs one launch per op ---
-    agg = {}
-    for name, env in (("aggregated", {}), ("one_launch_per_op", {"NCCL_AMD_NO_AGGREGATION": "1"})):
-        for k in saved:
+        ok = bool(torch.equal(full, base * (n * (n + 1) // 2)))
+        bw = lambda ms: round(bucket / (ms * 1e-3) / 1e9 * (n - 1) / n, 2)
+        out["rs_ag_bf16"] = {"config": f"ncclReduceScatter + ncclAllGather bf16, {bucket // MIB} MiB bucket, n={n}",
+                             "rs_ms": round(ms_rs, 4), "rs_busbw_GBps": bw(ms_rs), "ag_ms": round(ms_ag, 4),
+                             "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(ok) else "FAIL"}
+        # the same with the pull variants of both phases (xGMI reads instead of writes), its own communicator
+        pulls = ("NCCL_AMD_RS_PULL", "NCCL_AMD_AG_PULL")
+        saved_p = {k: os.environ.get(k) for k in pulls}
+        os.environ.update({k: "1" for k in pulls})
+        cp = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+        for k, v in saved_p.items():
             os.environ.pop(k, None)
-        os.environ.update(env)
-        cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
-
-        def grouped():
-            with nccl_amd.group():
-                for k in range(32):
-                    cm.all_reduce_raw(buf.data_ptr() + k * 8192, res.data_ptr() + k * 8192, 2048, 6, 0, sp)
-        ms = tmax(_tm(grouped, stream, 20))
-        agg[name + "_us_per_group"] = round(ms * 1e3, 2)
+            if v is not None:
+                os.environ[k] = v
+        ms_rs = tmax(_tm(lambda: cp.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp), stream, 10))
+        ms_ag = tmax(_tm(lambda: cp.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp), stream, 10))
+        full.zero_()
+        cp.reduce_scatter_raw(send.data_ptr(), shard.data_ptr(), cnt // n, 9, 0, sp)
+        cp.all_gather_raw(shard.data_ptr(), full.data_ptr(), cnt // n, 9, sp)
         torch.cuda.synchronize()
-        cm.destroy()
-    agg["config"] = "32 x ncclAllReduce fp16 4 KiB in one group"
-    out["group_aggregation"] = agg
-    for k, v in saved.items():
-        os.environ.pop(k, None)
-        if v is not None:
-            os.environ[k] = v
-    del buf, res
+        okp = bool(torch.equal(full, base * (n * (n + 1) // 2)))
+        cp.destroy()
+        out["rs_ag_bf16"]["pull"] = {"rs_ms": round(ms_rs, 4), "rs_busbw_GBps": bw(ms_rs), "ag_ms": round(ms_ag, 4),
+                                     "ag_busbw_GBps": bw(ms_ag), "check": "pass" if agree(okp) else "FAIL",
+                                     "env": "NCCL_AMD_RS_PULL=1 NCCL_AMD_AG_PULL=1"}
+        del send, shard, full, base
 
-    trace("reduce_int32")
-    # --- configs[4]: Reduce int32 min / max, 128 MiB, root 0 ---
-    S = (16 if quick else 128) * MIB
-    c = S // 4
-    g.manual_seed(99)
-    base = torch.randint(-2**31 + 64, 2**31 - 64, (c,), device="cuda", generator=g, dtype=torch.int64).to(torch.int32)
-    send = base + rank
-    recv = torch.empty_like(send) if rank == 0 else None
-    red = {}
-    okr = True
-    for name, op, want in (("min", 3, 0), ("max", 2, n - 1)):
-        fn = lambda: comm.reduce_raw(send.data_ptr(), recv.data_ptr() if recv is not None else None, c, 2, op, 0, sp)
-        ms = tmax(_tm(fn, stream, 10))
+    if want("ar_fp16_sweep"):
+        trace("ar_fp16_sweep")
+        # --- configs[3]: fp16 AllReduce sweep: LL vs one-shot vs direct. Protocol/algorithm knobs are read at
+        #     communicator init (like the reference's NCCL_PARAMs), so each column gets its own communicator ---
+        top = (16 if quick else 256) * MIB
+        buf = torch.empty(top // 2, dtype=torch.float16, device="cuda").uniform_(-1, 1)
+        res = torch.empty_like(buf)
+        cols = {"ll": {"NCCL_PROTO": "LL"}, "ll128": {"NCCL_PROTO": "LL128"},
+                "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
+                "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
+                "ring": {"NCCL_ALGO": "RING"}, "tree": {"NCCL_ALGO": "TREE"}, "default": {},
+                # the reference's RING/SIMPLE partition walked by the direct kernel: its cost vs default
+                "reforder": {"NCCL_AMD_REF_ORDER": "1"}}
+        if os.environ.get("BENCH_SWEEP_COLS"):  # diagnostics: a subset of the columns
+            cols = {k: cols[k] for k in os.environ["BENCH_SWEEP_COLS"].split(",")}
+        limits = {"ll": 512 * 1024, "ll128": 896 * 1024, "oneshot": 64 * MIB}
+        rows = {}
+        saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION", "NCCL_AMD_REF_ORDER")}
+        for name, env in cols.items():  # ll128: the LL64-line protocol (64-byte lines)
+            for k in saved:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+            size = 8
+            while size <= top:
+                if size <= limits.get(name, top):
+                    c = size // 2
+                    it = 50 if size <= 4 * MIB else 10
+                    ms = tmax(_tm(lambda: cm.all_reduce_raw(buf.data_ptr(), res.data_ptr(), c, 6, 0, sp), stream, it))
+                    row = rows.setdefault(size, {"bytes": size})
+                    row[name + "_us"] = round(ms * 1e3, 2)
+                    row[name + "_busbw_GBps"] = round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)
+                size *= 2
+            torch.cuda.synchronize()
+            cm.destroy()
+        out["ar_fp16_sweep"] = [rows[k] for k in sorted(rows)]
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+        del buf, res
+
+    if want("group_aggregation"):
+        trace("group_aggregation")
+        # --- group aggregation: 32 small AllReduce ops in one ncclGroupStart/End,
+        #     one LL launch vs one launch per op ---
+        agg = {}
+        buf = torch.empty(32 * 4096, dtype=torch.float16, device="cuda").uniform_(-1, 1)
+        res = torch.empty_like(buf)
+        saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION", "NCCL_AMD_REF_ORDER")}
+        for name, env in (("aggregated", {}), ("one_launch_per_op", {"NCCL_AMD_NO_AGGREGATION": "1"})):
+            for k in saved:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+
+            def grouped():
+                with nccl_amd.group():
+                    for k in range(32):
+                        cm.all_reduce_raw(buf.data_ptr() + k * 8192, res.data_ptr() + k * 8192, 2048, 6, 0, sp)
+            ms = tmax(_tm(grouped, stream, 20))
+            agg[name + "_us_per_group"] = round(ms * 1e3, 2)
+            torch.cuda.synchronize()
+            cm.destroy()
+        agg["config"] = "32 x ncclAllReduce fp16 4 KiB in one group"
+        out["group_aggregation"] = agg
+        for k, v in saved.items():
+            os.environ.pop(k, None)
+            if v is not None:
+                os.environ[k] = v
+        del buf, res
+
+    if want("reduce_int32"):
+        trace("reduce_int32")
+        # --- configs[4]: Reduce int32 min / max, 128 MiB, root 0 ---
+        S = (16 if quick else 128) * MIB
+        c = S // 4
+        g.manual_seed(99)
+        base = torch.randint(-2**31 + 64, 2**31 - 64, (c,), device="cuda", generator=g, dtype=torch.int64).to(torch.int32)
+        send = base + rank
+        recv = torch.empty_like(send) if rank == 0 else None
+        red = {}
+        okr = True
+        for name, op, want in (("min", 3, 0), ("max", 2, n - 1)):
+            fn = lambda: comm.reduce_raw(send.data_ptr(), recv.data_ptr() if recv is not None else None, c, 2, op, 0, sp)
+            ms = tmax(_tm(fn, stream, 10))
+            fn()
+            torch.cuda.synchronize()
+            if rank == 0:
+                okr = okr and bool(torch.equal(recv, base + want))
+            red[name + "_ms"] = round(ms, 4)
+            red[name + "_busbw_GBps"] = round(S / (ms * 1e-3) / 1e9, 2)
+        red["config"] = f"ncclReduce min/max int32, {S // MIB} MiB, root 0, n={n}"
+        red["check"] = "pass (bit-exact)" if agree(okr) else "FAIL"
+        out["reduce_int32"] = red
+        del send, recv, base
+
+    if want("symmetric_window"):
+        trace("symmetric_window")
+        # --- symmetric windows (zero-copy pull kernels): the headline AllReduce and the
+        #     fp16 latency curve with send/recv inside an NCCL_WIN_COLL_SYMMETRIC window ---
+        S = (16 if quick else 256) * MIB
+        c = S // 4
+        win_t = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
+        win = comm.register_window(win_t.data_ptr(), 2 * S)
+        sendw = win_t[:S].view(torch.float32)
+        recvw = win_t[S:].view(torch.float32)
+        g.manual_seed(4321)
+        base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
+        sendw.copy_(base * (rank + 1))
+        fn = lambda: comm.all_reduce_raw(sendw.data_ptr(), recvw.data_ptr(), c, 7, 0, sp)
+        ms = tmax(_tm(fn, stream, 20, warmup=5))
+        recvw.zero_()
         fn()
         torch.cuda.synchronize()
-        if rank == 0:
-            okr = okr and bool(torch.equal(recv, base + want))
-        red[name + "_ms"] = round(ms, 4)
-        red[name + "_busbw_GBps"] = round(S / (ms * 1e-3) / 1e9, 2)
-    red["config"] = f"ncclReduce min/max int32, {S // MIB} MiB, root 0, n={n}"
-    red["check"] = "pass (bit-exact)" if agree(okr) else "FAIL"
-    out["reduce_int32"] = red
-    del send, recv, base
+        oks = bool(torch.equal(recvw, base * (n * (n + 1) / 2)))
+        sym = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, buffers in symmetric windows, n={n}",
+               "ms": round(ms, 4), "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+               "value_equiv_GBps": round(n * S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+               "check": "pass (dyadic, exact)" if agree(oks) else "FAIL"}
+        lat = []
+        hbuf = win_t[:S].view(torch.float16)
+        hres = win_t[S:].view(torch.float16)
+        size = 8
+        while size <= (16 if quick else 64) * MIB:
+            cc = size // 2
+            it = 50 if size <= 4 * MIB else 10
+            ms = tmax(_tm(lambda: comm.all_reduce_raw(hbuf.data_ptr(), hres.data_ptr(), cc, 6, 0, sp), stream, it))
+            lat.append({"bytes": size, "us": round(ms * 1e3, 2),
+                        "busbw_GBps": round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)})
+            size *= 4
+        sym["ar_fp16_sweep"] = lat
+        out["symmetric_window"] = sym
+        torch.cuda.synchronize()
+        comm.deregister_window(win)
+        del win_t, sendw, recvw, base, hbuf, hres
 
-    trace("symmetric_window")
-    # --- symmetric windows (zero-copy pull kernels): the headline AllReduce and the
-    #     fp16 latency curve with send/recv inside an NCCL_WIN_COLL_SYMMETRIC window ---
-    S = (16 if quick else 256) * MIB
-    c = S // 4
-    win_t = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
-    win = comm.register_window(win_t.data_ptr(), 2 * S)
-    sendw = win_t[:S].view(torch.float32)
-    recvw = win_t[S:].view(torch.float32)
-    g.manual_seed(4321)
-    base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
-    sendw.copy_(base * (rank + 1))
-    fn = lambda: comm.all_reduce_raw(sendw.data_ptr(), recvw.data_ptr(), c, 7, 0, sp)
-    ms = tmax(_tm(fn, stream, 20, warmup=5))
-    recvw.zero_()
-    fn()
-    torch.cuda.synchronize()
-    oks = bool(torch.equal(recvw, base * (n * (n + 1) / 2)))
-    sym = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, buffers in symmetric windows, n={n}",
-           "ms": round(ms, 4), "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
-           "value_equiv_GBps": round(n * S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
-           "check": "pass (dyadic, exact)" if agree(oks) else "FAIL"}
-    lat = []
-    hbuf = win_t[:S].view(torch.float16)
-    hres = win_t[S:].view(torch.float16)
-    size = 8
-    while size <= (16 if quick else 64) * MIB:
-        cc = size // 2
-        it = 50 if size <= 4 * MIB else 10
-        ms = tmax(_tm(lambda: comm.all_reduce_raw(hbuf.data_ptr(), hres.data_ptr(), cc, 6, 0, sp), stream, it))
-        lat.append({"bytes": size, "us": round(ms * 1e3, 2),
-                    "busbw_GBps": round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)})
-        size *= 4
-    sym["ar_fp16_sweep"] = lat
-    out["symmetric_window"] = sym
-    torch.cuda.synchronize()
-    comm.deregister_window(win)
-    del win_t, sendw, recvw, base, hbuf, hres
-
-    trace("staged_tuning")
-    # --- staged-path tuning matrix at the headline size (data for the next tuning round: knobs are read
-    #     at communicator init, so each setting gets its own communicator). Every column's result must equal the
-    #     default column's bit for bit (same fold order), which checks the fence-free release over the links ---
-    S = (16 if quick else 256) * MIB
-    c = S // 4
-    xs = torch.empty(c, dtype=torch.float32, device="cuda").uniform_(-1, 1)
-    ys = torch.empty_like(xs)
-    tuning = []
-    knobs = ("NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_AG_PULL",
-             "NCCL_AMD_RS_PULL", "NCCL_AMD_P2P_FENCE")
-    saved = {k: os.environ.get(k) for k in knobs}
-    # (the staging slab is capped at 1 GiB per rank, so slot sizes scale with channels x slots x n:
-    #  default 128 KiB slots at n = 8, 256 KiB with 128 channels)
-    ref = None
-    for env in ({}, {"NCCL_AMD_P2P_FENCE": "0"}, {"NCCL_AMD_P2P_FENCE": "1"}, {"NCCL_MAX_CTAS": "256"},
-                {"NCCL_AMD_SLOT_BYTES": "32768"}, {"NCCL_AMD_SLOT_BYTES": "65536"},
-                {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_AMD_NSLOTS": "4"}, {"NCCL_MAX_CTAS": "128"},
-                {"NCCL_MAX_CTAS": "64"}, {"NCCL_MAX_CTAS": "32"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}, {"NCCL_AMD_AG_PULL": "1"},
-                {"NCCL_AMD_RS_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}):
-        for k in knobs:
+    if want("staged_tuning"):
+        trace("staged_tuning")
+        # --- staged-path tuning matrix at the headline size (data for the next tuning round: knobs are read
+        #     at communicator init, so each setting gets its own communicator). Every column's result must equal the
+        #     default column's bit for bit (same fold order), which checks the fence-free release over the links ---
+        S = (16 if quick else 256) * MIB
+        c = S // 4
+        xs = torch.empty(c, dtype=torch.float32, device="cuda").uniform_(-1, 1)
+        ys = torch.empty_like(xs)
+        tuning = []
+        knobs = ("NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_AG_PULL",
+                 "NCCL_AMD_RS_PULL", "NCCL_AMD_P2P_FENCE")
+        saved = {k: os.environ.get(k) for k in knobs}
+        # (the staging slab is capped at 1 GiB per rank, so slot sizes scale with channels x slots x n:
+        #  default 128 KiB slots at n = 8, 256 KiB with 128 channels)
+        ref = None
+        for env in ({}, {"NCCL_AMD_P2P_FENCE": "0"}, {"NCCL_AMD_P2P_FENCE": "1"}, {"NCCL_MAX_CTAS": "256"},
+                    {"NCCL_AMD_SLOT_BYTES": "32768"}, {"NCCL_AMD_SLOT_BYTES": "65536"},
+                    {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_AMD_NSLOTS": "4"}, {"NCCL_MAX_CTAS": "128"},
+                    {"NCCL_MAX_CTAS": "64"}, {"NCCL_MAX_CTAS": "32"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}, {"NCCL_AMD_AG_PULL": "1"},
+                    {"NCCL_AMD_RS_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}):
+            for k in knobs:
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+            trace(f"staged_tuning {env or 'default'}")
+            ms = tmax(_tm(lambda: cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, sp), stream, 10))
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = ys.clone()
+                same = True
+            else:
+                same = bool(torch.equal(ys, ref))
+            tuning.append({"env": env or "default", "ms": round(ms, 4),
+                           "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+                           "check": "pass (= default, bitwise)" if agree(same) else "FAIL"})
+            cm.destroy()
+        for k, v in saved.items():
             os.environ.pop(k, None)
-        os.environ.update(env)
-        cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
-        trace(f"staged_tuning {env or 'default'}")
-        ms = tmax(_tm(lambda: cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, sp), stream, 10))
-        torch.cuda.synchronize()
-        if ref is None:
-            ref = ys.clone()
-            same = True
-        else:
-            same = bool(torch.equal(ys, ref))
-        tuning.append({"env": env or "default", "ms": round(ms, 4),
-                       "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
-                       "check": "pass (= default, bitwise)" if agree(same) else "FAIL"})
-        cm.destroy()
-    for k, v in saved.items():
-        os.environ.pop(k, None)
-        if v is not None:
-            os.environ[k] = v
-    out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}", "runs": tuning}
-    del xs, ys, ref
+            if v is not None:
+                os.environ[k] = v
+        out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}", "runs": tuning}
+        del xs, ys, ref
 
-    trace("xgmi_probe")
-    # --- xGMI probes (rank 0, peer copies via hipMemcpyPeerAsync) ---
-    ndev = torch.cuda.device_count()
-    if rank == 0 and ndev > 1:
-        probe = {}
-        nbytes = 256 * MIB
-        src = torch.empty(nbytes // 4, device="cuda:0")
-        dsts = [torch.empty(nbytes // 4, device=f"cuda:{d}") for d in range(1, ndev)]
-        ms = _time_ms(lambda: dsts[0].copy_(src), stream, 5)
-        probe["one_link_0to1_GBps"] = round(nbytes / (ms * 1e-3) / 1e9, 1)
-        streams = [torch.cuda.Stream(device=0) for _ in dsts]
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(3):
-            for s, d in zip(streams, dsts):
-                with torch.cuda.stream(s):
-                    d.copy_(src)
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / 3
-        probe["fanout_0toall_GBps"] = round(len(dsts) * nbytes / dt / 1e9, 1)
-        probe["method"] = "torch copy_ (hipMemcpyPeerAsync); fan-out = concurrent copies on separate streams"
-        # the CU-driven probe (tests/native/xgmi_probe): 16-byte vector loads/stores from GPU 0's CUs, the
-        # access pattern of the collective kernels, one link and all links, write and read
-        exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "xgmi_probe")
-        if os.path.exists(exe):
-            try:
-                import subprocess
-                r = subprocess.run([exe, "256", "10"], capture_output=True, text=True, timeout=120)
-                probe["cu_kernel"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
-                    {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
-            except Exception as e:
-                probe["cu_kernel"] = {"error": repr(e)}
-        # single-copy atomicity over the link: GPU 1 writes LL-style lines into GPU 0's
-        # uncached memory while GPU 0 polls them; torn 8/16/64/128-byte lines are counted (LL needs torn8 == 0,
-        # an LL128-class protocol would need torn64 == torn128 == 0)
-        exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "store_atomicity_probe")
-        if os.path.exists(exe):
-            try:
-                import subprocess
-                r = subprocess.run([exe, "1", "0", "20000", "64", "3000"], capture_output=True, text=True,
-                                   timeout=60)
-                probe["store_atomicity"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 \
-                    else {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
-            except Exception as e:
-                probe["store_atomicity"] = {"error": repr(e)}
-        out["xgmi_probe"] = probe
-        del src, dsts
-    if dist is not None:
-        dist.barrier()  # the other ranks wait here, not spinning in a collective, while rank 0 probes the links
+    if want("xgmi_probe"):
+        trace("xgmi_probe")
+        # --- xGMI probes (rank 0, peer copies via hipMemcpyPeerAsync) ---
+        ndev = torch.cuda.device_count()
+        if rank == 0 and ndev > 1:
+            probe = {}
+            nbytes = 256 * MIB
+            src = torch.empty(nbytes // 4, device="cuda:0")
+            dsts = [torch.empty(nbytes // 4, device=f"cuda:{d}") for d in range(1, ndev)]
+            ms = _time_ms(lambda: dsts[0].copy_(src), stream, 5)
+            probe["one_link_0to1_GBps"] = round(nbytes / (ms * 1e-3) / 1e9, 1)
+            streams = [torch.cuda.Stream(device=0) for _ in dsts]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(3):
+                for s, d in zip(streams, dsts):
+                    with torch.cuda.stream(s):
+                        d.copy_(src)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 3
+            probe["fanout_0toall_GBps"] = round(len(dsts) * nbytes / dt / 1e9, 1)
+            probe["method"] = "torch copy_ (hipMemcpyPeerAsync); fan-out = concurrent copies on separate streams"
+            # the CU-driven probe (tests/native/xgmi_probe): 16-byte vector loads/stores from GPU 0's CUs, the
+            # access pattern of the collective kernels, one link and all links, write and read
+            exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "xgmi_probe")
+            if os.path.exists(exe):
+                try:
+                    import subprocess
+                    r = subprocess.run([exe, "256", "10"], capture_output=True, text=True, timeout=120)
+                    probe["cu_kernel"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 else \
+                        {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
+                except Exception as e:
+                    probe["cu_kernel"] = {"error": repr(e)}
+            # single-copy atomicity over the link: GPU 1 writes LL-style lines into GPU 0's
+            # uncached memory while GPU 0 polls them; torn 8/16/64/128-byte lines are counted (LL needs torn8 == 0,
+            # an LL128-class protocol would need torn64 == torn128 == 0)
+            exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "native", "store_atomicity_probe")
+            if os.path.exists(exe):
+                try:
+                    import subprocess
+                    r = subprocess.run([exe, "1", "0", "20000", "64", "3000"], capture_output=True, text=True,
+                                       timeout=60)
+                    probe["store_atomicity"] = json.loads(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 \
+                        else {"error": f"rc {r.returncode}: {r.stderr.strip()[-200:]}"}
+                except Exception as e:
+                    probe["store_atomicity"] = {"error": repr(e)}
+            out["xgmi_probe"] = probe
+            del src, dsts
+        if dist is not None:
+            dist.barrier()  # the other ranks wait here, not spinning in a collective, while rank 0 probes the links
 
-    trace("registered")
-    # --- buffers registered with ncclCommRegister (zero-copy kernel in registered mode): the
-    #     headline AllReduce on plain torch allocations, no window. Last: the newest path, and its deregistration
-    #     makes every peer release a mapping ---
-    S = (16 if quick else 256) * MIB
-    c = S // 4
-    g.manual_seed(4322)
-    base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
-    sendr = base * (rank + 1)
-    recvr = torch.empty_like(sendr)
-    hs = [comm.register_buffer(sendr.data_ptr(), S), comm.register_buffer(recvr.data_ptr(), S)]
-    fn = lambda: comm.all_reduce_raw(sendr.data_ptr(), recvr.data_ptr(), c, 7, 0, sp)
-    ms = tmax(_tm(fn, stream, 20, warmup=5))
-    recvr.zero_()
-    fn()
-    torch.cuda.synchronize()
-    okr = bool(torch.equal(recvr, base * (n * (n + 1) / 2)))
-    out["registered"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, ncclCommRegister'd buffers, n={n}",
-                         "ms": round(ms, 4), "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
-                         "check": "pass (dyadic, exact)" if agree(okr) else "FAIL"}
-    torch.cuda.synchronize()
-    for h in hs:
-        comm.deregister_buffer(h)
-    del sendr, recvr, base
+    if want("registered"):
+        trace("registered")
+        # --- buffers registered with ncclCommRegister (zero-copy kernel in registered mode): the
+        #     headline AllReduce on plain torch allocations, no window. Last: the newest path, and its deregistration
+        #     makes every peer release a mapping ---
+        S = (16 if quick else 256) * MIB
+        c = S // 4
+        g.manual_seed(4322)
+        base = torch.randint(-1024, 1025, (c,), device="cuda", generator=g, dtype=torch.int32).float() / 256
+        sendr = base * (rank + 1)
+        recvr = torch.empty_like(sendr)
+        hs = [comm.register_buffer(sendr.data_ptr(), S), comm.register_buffer(recvr.data_ptr(), S)]
+        fn = lambda: comm.all_reduce_raw(sendr.data_ptr(), recvr.data_ptr(), c, 7, 0, sp)
+        ms = tmax(_tm(fn, stream, 20, warmup=5))
+        recvr.zero_()
+        fn()
+        torch.cuda.synchronize()
+        okr = bool(torch.equal(recvr, base * (n * (n + 1) / 2)))
+        out["registered"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, ncclCommRegister'd buffers, n={n}",
+                             "ms": round(ms, 4), "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+                             "check": "pass (dyadic, exact)" if agree(okr) else "FAIL"}
+        torch.cuda.synchronize()
+        for h in hs:
+            comm.deregister_buffer(h)
+        del sendr, recvr, base
 
     return out
 
@@ -461,6 +483,9 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
     # of chunk k-1 overlap, so both PCIe directions stay busy at once (the reference's proxy pipelines its
     # network-staged transfers the same way, src/proxy.cc:954-1012). 4 chunks: 6.6 ms vs 7.6 ms at 16 (per-copy
     # cost) and 9.5 ms serial on the MI355X box (scripts/host_pipe_probe.py, profiles/r03_host_staged_pipeline.json)
+    if os.environ.get("BENCH_HOST_STAGED_PIPE") == "0":  # diagnostics: the one-stream measurement only
+        return {"bytes_per_rank": S, "ms_per_step": round(ms, 4), "algbw_GBps_incl_pcie": round(S / (ms * 1e-3) / 1e9, 2),
+                "device_resident_ms": round(ms_dev, 4)}
     nchunk = 4
     cc = count // nchunk
     s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
@@ -759,10 +784,14 @@ def main(argv=None):
         except Exception as e:  # secondary measurement
             extra["host_staged"] = {"error": repr(e)}
 
-    # At N > 1 it runs after the suite: on the one-GPU rehearsal every small collective the suite timed after it
-    # took 27.6 us instead of 4.2 (LL, 8 B - 32 KiB; profiles/r03_host_staged_order_n2_onegpu.txt), an effect the
-    # same calls in a standalone probe do not show (scripts/tr_issue_probe.py) — kept out of the suite's numbers.
-    if not args.no_extra and n == 1:
+    # Part order (the same at every N): the headline loop and its check, the link probe, the N = 1 extras and CPU
+    # baseline, the suite (N > 1), then the host-staged bucket. Every collective-rate part runs on the launch stream alone; the
+    # host-staged part is the only one that uses two more streams (its pipelined variant), i.e. two more hardware
+    # queues per rank, which stay mapped for the rest of the process — so it runs after every part whose rate it
+    # would change. Measured on the one-GPU rehearsal: once a rank process holds three or more hardware queues, every
+    # later small collective takes ~27.6 us instead of ~4 us (profiles/r04_queue_order_n2_onegpu.txt).
+    # BENCH_HOST_STAGED=first (diagnostics) runs it before the suite instead.
+    if not args.no_extra and n > 1 and os.environ.get("BENCH_HOST_STAGED") == "first":
         run_host_staged()
 
     cpu = None  # the contract's CPU baseline is an N=1 figure (rank 0 only)
@@ -851,7 +880,7 @@ def main(argv=None):
         barrier()
         done.set()
         suite["seconds"] = round(time.perf_counter() - t_suite, 1)
-    if not args.no_extra and n > 1:
+    if not args.no_extra and (n == 1 or os.environ.get("BENCH_HOST_STAGED") != "first"):
         run_host_staged()
 
     if rank == 0:
