@@ -144,6 +144,7 @@ void ipcUnexport(ncclComm* comm, const IpcDesc& d);
 ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d);  // serve an fd (owned) under a new key
 ncclResult_t ipcFetchFd(const IpcDesc& d, int* fd);  // an exporter's fd for d, over its fd server (bounded)
 ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out);
+ncclResult_t ipcImportHandle(const IpcDesc& d, IpcImport* out);  // the hipIpc handle only (d.hasHandle or d.legacy)
 void ipcRelease(IpcImport* m);
 // Registered buffers (register.cc): ask the fd server `server` (a peer's) to map the dma-buf `fd` (sent along,
 // the caller keeps its copy) on its device on behalf of `rank`, remembered under `tag`; *addr = where it
@@ -349,6 +350,9 @@ struct MapCheckPeer {  // how this rank reaches peer r (for the message)
 // The failures of one rank's observations, one line each ("" = every mapping carried the patterns).
 std::string mapCheckVerify(int me, int nRanks, uint64_t nonce, const MapCheckObs& obs, const MapCheckPeer* peers);
 ncclResult_t mapCheck(const std::vector<ncclComm*>& comms);  // the check for these local comms (init.cc)
+// Re-import peer r's staging slab and flag block through the hipIpc handles of their exports (the dma-buf import's
+// fallback) and refresh the device's view of them; ncclSystemError when peer r has no such handle (transport.cc).
+ncclResult_t transportRemapPeer(ncclComm* comm, int r);
 ncclResult_t launchMapCheck(const DevComm* dc, const MapCheckArgs& a, uint64_t* out, hipStream_t stream);  // kernels.hip
 
 // ---------------------------------------------------------------- enqueue (reference src/enqueue.cc)

@@ -578,6 +578,16 @@ ncclResult_t ipcImport(const IpcDesc& d, IpcImport* out) {
   return importLegacy(d, out);
 }
 
+ncclResult_t ipcImportHandle(const IpcDesc& d, IpcImport* out) {
+  memset(out, 0, sizeof(*out));
+  out->fd = -1;
+  if (!d.legacy && !d.hasHandle) {
+    WARN("ipc: export %llu of %s carries no hipIpc handle to fall back to", (unsigned long long)d.key, d.server);
+    return ncclSystemError;
+  }
+  return importLegacy(d, out);
+}
+
 void ipcRelease(IpcImport* m) {
   if (!m->ptr) return;
   std::lock_guard<std::mutex> g(gMapMu);

@@ -18,7 +18,10 @@
 //      with the expected words (mapCheckWord: a function of a nonce every rank derives from the shared peer table);
 //   4. the ranks exchange their outcome, so every rank fails the init together (ncclSystemError), each naming the
 //      device pairs, allocations, directions and import paths it saw fail.
-// NCCL_AMD_MAPCHECK=0 skips it; NCCL_AMD_MAPCHECK_FAULT=1 (tests) makes this rank skip its remote stores.
+// A failed first round gets one more try: the ranks whose mappings failed re-import those peers through the hipIpc
+// handle that rides along the dma-buf export (ipc.cc; transportRemapPeer) and every rank checks again; only a failure
+// that survives it fails the init. NCCL_AMD_MAPCHECK=0 skips the check, NCCL_AMD_MAPCHECK_FALLBACK=0 the second
+// round; NCCL_AMD_MAPCHECK_FAULT=1 (tests) makes this rank skip its remote stores, =2 in the first round only.
 #include <string.h>
 
 #include "core.h"
@@ -129,7 +132,7 @@ static ncclResult_t mapPrepare(ncclComm* c, uint64_t nonce) {
 }
 
 // step 2: the remote stores and loads (one wave), results into a device buffer
-static ncclResult_t mapRun(ncclComm* c, uint64_t nonce, uint64_t** outDev) {
+static ncclResult_t mapRun(ncclComm* c, uint64_t nonce, int attempt, uint64_t** outDev) {
   HIPCHECK(hipSetDevice(c->device));
   HIPCHECK(hipMalloc((void**)outDev, (size_t)NCCL_AMD_MAX_RANKS * 4 * sizeof(uint64_t)));
   HIPCHECK(hipMemset(*outDev, 0, (size_t)NCCL_AMD_MAX_RANKS * 4 * sizeof(uint64_t)));
@@ -139,7 +142,9 @@ static ncclResult_t mapRun(ncclComm* c, uint64_t nonce, uint64_t** outDev) {
     for (int k = 0; k < 2; k++)
       for (int h = 0; h < 2; h++) a.w[p][k][h] = mapCheckWord(nonce, k, c->rank, p, h);
   a.probeOff = c->probeOffset;
-  a.skip = (int)paramInt("NCCL_AMD_MAPCHECK_FAULT", 0);
+  // tests: 1 = this rank's stores never arrive; 2 = only in the first round (the remap below then fixes it)
+  const int64_t fault = paramInt("NCCL_AMD_MAPCHECK_FAULT", 0);
+  a.skip = fault == 1 || (fault == 2 && attempt == 0);
   NCCLCHECK(launchMapCheck(c->devComm, a, *outDev, nullptr));
   return ncclSuccess;
 }
@@ -168,19 +173,19 @@ static ncclResult_t localBarrier(ncclComm* c) {
   return ncclSuccess;  // ncclCommInitAll: one thread drives every rank, the steps run rank by rank
 }
 
-ncclResult_t mapCheck(const std::vector<ncclComm*>& comms) {
-  if (comms.empty() || comms[0]->nRanks == 1 || !paramInt("NCCL_AMD_MAPCHECK", 1)) return ncclSuccess;
-  int oldDev = 0;
-  (void)hipGetDevice(&oldDev);
+// One round of the check for the local comms. fail[r] (every rank of the communicator, filled for the local ones):
+// bit p of .load = rank r's loads from p failed, bit p of .store = p's stores into rank r failed.
+struct MapFail {
+  uint32_t load, store;
+};
+static ncclResult_t mapRound(const std::vector<ncclComm*>& comms, uint64_t nonce, int attempt, std::vector<MapFail>& fail,
+                             std::string& report) {
   ncclResult_t res = ncclSuccess;
-  const uint64_t nonce = mapNonce(comms[0]);
   std::vector<uint64_t*> outs(comms.size(), nullptr);
-  std::vector<char> ok(comms[0]->nRanks, 1);
-  std::string report;
   for (ncclComm* c : comms)
     if (res == ncclSuccess) res = mapPrepare(c, nonce);
   if (res == ncclSuccess) res = localBarrier(comms[0]);
-  for (size_t i = 0; i < comms.size() && res == ncclSuccess; i++) res = mapRun(comms[i], nonce, &outs[i]);
+  for (size_t i = 0; i < comms.size() && res == ncclSuccess; i++) res = mapRun(comms[i], nonce, attempt, &outs[i]);
   for (size_t i = 0; i < comms.size() && res == ncclSuccess; i++) {
     (void)hipSetDevice(comms[i]->device);
     if (hipDeviceSynchronize() != hipSuccess) res = ncclUnhandledCudaError;
@@ -198,10 +203,17 @@ ncclResult_t mapCheck(const std::vector<ncclComm*>& comms) {
       peers[r].path = r == c->rank ? "local" : pathTo(c, r);
       peers[r].pathIn = r == c->rank ? "local" : pathFrom(c, r);
     }
-    std::string bad = mapCheckVerify(c->rank, c->nRanks, nonce, obs, peers.data());
-    if (!bad.empty()) {
-      ok[c->rank] = 0;
-      report += bad;
+    report += mapCheckVerify(c->rank, c->nRanks, nonce, obs, peers.data());
+    MapFail& f = fail[c->rank];
+    f.load = f.store = 0;
+    for (int p = 0; p < c->nRanks; p++) {
+      if (p == c->rank) continue;
+      for (int k = 0; k < 2; k++) {
+        if (obs.read[k][p][0] != mapCheckWord(nonce, 2 + k, p, p, 0) || obs.read[k][p][1] != mapCheckWord(nonce, 2 + k, p, p, 1))
+          f.load |= 1u << p;
+        if (obs.wrote[k][p][0] != mapCheckWord(nonce, k, p, c->rank, 0) || obs.wrote[k][p][1] != mapCheckWord(nonce, k, p, c->rank, 1))
+          f.store |= 1u << p;
+      }
     }
   }
   for (size_t i = 0; i < comms.size(); i++)
@@ -209,14 +221,47 @@ ncclResult_t mapCheck(const std::vector<ncclComm*>& comms) {
       (void)hipSetDevice(comms[i]->device);
       (void)hipFree(outs[i]);
     }
+  if (res != ncclSuccess) return res;
+  // every rank learns every rank's row (a rank whose own view is clean still learns that it must remap or fail)
+  if (comms[0]->bootstrap) NCCLCHECK(bootstrapAllGather(comms[0]->bootstrap, fail.data(), sizeof(MapFail)));
+  return ncclSuccess;
+}
+
+ncclResult_t mapCheck(const std::vector<ncclComm*>& comms) {
+  if (comms.empty() || comms[0]->nRanks == 1 || !paramInt("NCCL_AMD_MAPCHECK", 1)) return ncclSuccess;
+  int oldDev = 0;
+  (void)hipGetDevice(&oldDev);
+  const int n = comms[0]->nRanks;
+  const uint64_t nonce = mapNonce(comms[0]);
+  std::vector<MapFail> fail(n, MapFail{0, 0});
+  std::string report;
+  ncclResult_t res = mapRound(comms, nonce, 0, fail, report);
+  auto anyFail = [&]() {
+    for (const MapFail& f : fail)
+      if (f.load | f.store) return true;
+    return false;
+  };
+  if (res == ncclSuccess && anyFail() && paramInt("NCCL_AMD_MAPCHECK_FALLBACK", 1)) {
+    // Second chance for cross-process mappings: a rank re-imports every peer p whose loads through its mapping
+    // failed, or into which its stores did not arrive (p's row), through the hipIpc handle that rides along the
+    // dma-buf export where the runtime can open one (ipc.cc) — then every rank runs the check again. Every rank
+    // sees the same table, so all take the second round together.
+    for (const std::string& line : {report})
+      if (!line.empty()) INFO("mapping check, first round:\n%s", line.c_str());
+    report.clear();
+    for (ncclComm* c : comms) {
+      const int me = c->rank;
+      for (int p = 0; p < n && res == ncclSuccess; p++) {
+        if (p == me || !(((fail[me].load >> p) & 1) || ((fail[p].store >> me) & 1))) continue;
+        res = transportRemapPeer(c, p);
+      }
+    }
+    if (res == ncclSuccess) res = mapRound(comms, nonce ^ 0x5eedull, 1, fail, report);
+  }
   (void)hipSetDevice(oldDev);
   if (res != ncclSuccess) return res;
-  // every rank learns every rank's outcome and fails together (a rank whose own view is clean still reports)
   ncclComm* c0 = comms[0];
-  if (c0->bootstrap) NCCLCHECK(bootstrapAllGather(c0->bootstrap, ok.data(), 1));
-  int nbad = 0;
-  for (char x : ok) nbad += x ? 0 : 1;
-  if (nbad == 0) {
+  if (!anyFail()) {
     INFO("rank %d: peer mappings verified (store and load through every mapping, staging and flags)", c0->rank);
     return ncclSuccess;
   }
@@ -228,6 +273,8 @@ ncclResult_t mapCheck(const std::vector<ncclComm*>& comms) {
       pos = e + 1;
     }
   } else {
+    int nbad = 0;
+    for (const MapFail& f : fail) nbad += (f.load | f.store) ? 1 : 0;
     WARN("mapping check: rank %d's mappings carried the patterns, but %d rank(s) saw a mapping fail (their logs name "
          "the device pairs)", c0->rank, nbad);
   }

@@ -122,6 +122,35 @@ ncclResult_t transportConnect(ncclComm* comm) {
   return ncclSuccess;
 }
 
+// The mapping check's second chance (mapcheck.cc): map peer r's slab and flags through the hipIpc handles of their
+// exports instead of the dma-buf imports, and give the device the new pointers.
+ncclResult_t transportRemapPeer(ncclComm* comm, int r) {
+  const PeerInfo& p = comm->peers[r];
+  if (p.pid == comm->peers[comm->rank].pid) {
+    WARN("rank %d: no other way to map rank %d (same process: a peer pointer)", comm->rank, r);
+    return ncclSuccess;  // the second round reports it
+  }
+  HIPCHECK(hipSetDevice(comm->device));
+  IpcImport st, fl;
+  if (ipcImportHandle(p.stagingDesc, &st) != ncclSuccess || ipcImportHandle(p.flagsDesc, &fl) != ncclSuccess) {
+    ipcRelease(&st);
+    WARN("rank %d: rank %d's slab cannot be mapped through a hipIpc handle; keeping the dma-buf mapping", comm->rank, r);
+    return ncclSuccess;  // the second round reports it
+  }
+  ipcRelease(&comm->peerStagingMap[r]);
+  ipcRelease(&comm->peerFlagsMap[r]);
+  comm->peerStagingMap[r] = st;
+  comm->peerFlagsMap[r] = fl;
+  comm->peerStaging[r] = st.ptr;
+  comm->peerFlags[r] = (uint64_t*)fl.ptr;
+  comm->hostDevComm.staging[r] = (char*)st.ptr;
+  comm->hostDevComm.flags[r] = (uint64_t*)fl.ptr;
+  HIPCHECK(hipMemcpy(comm->devComm, &comm->hostDevComm, sizeof(DevComm), hipMemcpyHostToDevice));
+  WARN("rank %d: rank %d (device %d, %s) remapped through hipIpc handles after the dma-buf mapping failed the check",
+       comm->rank, r, p.device, p.busId);
+  return ncclSuccess;
+}
+
 // Before freeing: every slice this rank sent must have been acknowledged (RS_ACK == sendRS and
 // AG_ACK == sendAG per channel and peer). Acks are written by peers' kernels after they consumed our
 // data, possibly after our own kernels finished; waiting for them (bounded) keeps those stores out of

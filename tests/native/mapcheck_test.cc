@@ -9,6 +9,7 @@
 //     legacy:R:P      rank R maps rank P's memory through a hipIpc handle (the dma-buf import's fallback)
 //     skip:R          rank R's stores never arrive (NCCL_AMD_MAPCHECK_FAULT on that rank)
 //     samepid         every rank in one process (peer pointers) instead of one process per rank
+//     fixable:R:P     rank R's remap of rank P (the second round, transportRemapPeer) repairs its mapping
 // prints "result=<ncclResult_t>"; the check's WARN lines go to stderr.
 #include <stdio.h>
 #include <stdlib.h>
@@ -66,6 +67,21 @@ ncclResult_t launchMapCheck(const DevComm* dcp, const MapCheckArgs& a, uint64_t*
   }
   return ncclSuccess;
 }
+// the second round's remap (transport.cc transportRemapPeer): "fixable" faults are repaired by it
+static std::vector<std::vector<int>> gFixable;
+static std::vector<DevComm>* gDcs = nullptr;
+static std::vector<ncclComm*>* gComms = nullptr;
+int gRemaps = 0;
+ncclResult_t transportRemapPeer(ncclComm* comm, int r) {
+  gRemaps++;
+  if (gFixable[comm->rank][r]) {
+    (*gDcs)[comm->rank].staging[r] = (char*)(*gComms)[r]->staging;
+    (*gDcs)[comm->rank].flags[r] = (*gComms)[r]->flags;
+    comm->peerStagingMap[r].legacy = 1;
+  }
+  printf("remap %d<-%d\n", comm->rank, r);
+  return ncclSuccess;
+}
 }  // namespace ncclamd
 
 using namespace ncclamd;
@@ -73,6 +89,7 @@ using namespace ncclamd;
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 2;
   gSkip.assign(n, 0);
+  gFixable.assign(n, std::vector<int>(n, 0));
   bool samePid = false;
   const size_t slot = 4096, probe = 8192;
   std::vector<ncclComm*> cs(n);
@@ -133,8 +150,12 @@ int main(int argc, char** argv) {
       cs[R]->peerStagingMap[P].legacy = 1;
     } else if (sscanf(argv[i], "skip:%d", &R) == 1) {
       gSkip[R] = 1;
+    } else if (sscanf(argv[i], "fixable:%d:%d", &R, &P) == 2) {
+      gFixable[R][P] = 1;
     }
   }
+  gDcs = &dcs;
+  gComms = &cs;
   logInit();
   ncclResult_t res = mapCheck(cs);
   printf("result=%d\n", (int)res);

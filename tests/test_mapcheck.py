@@ -66,3 +66,17 @@ def test_dropped_stores_fail_every_peer(exe):
 def test_single_process_peer_pointer_path(exe):
     res, warns = run(exe, 2, "samepid", "wrongmap:0:1:0")
     assert res == 2 and all("hipDeviceEnablePeerAccess" in w for w in warns), warns
+
+
+def test_second_round_remaps_and_passes(exe):
+    """A mapping that fails the first round is re-imported through the export's hipIpc handle (transportRemapPeer,
+    stubbed: it repairs the mapping) by the rank that owns it — found from its own loads or from the peer's report of
+    its stores — and the second round passes; a mapping the remap cannot repair still fails the init."""
+    env = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_")}
+    out = subprocess.run([exe, "3", "wrongmap:1:2:0", "fixable:1:2"], env=env, capture_output=True, text=True, timeout=30)
+    assert "remap 1<-2" in out.stdout and "result=0" in out.stdout, out.stdout
+    out = subprocess.run([exe, "4", "skip:3"], env=env, capture_output=True, text=True, timeout=30)
+    assert all(f"remap 3<-{p}" in out.stdout for p in (0, 1, 2)) and "result=2" in out.stdout, out.stdout
+    env["NCCL_AMD_MAPCHECK_FALLBACK"] = "0"
+    out = subprocess.run([exe, "3", "wrongmap:1:2:0", "fixable:1:2"], env=env, capture_output=True, text=True, timeout=30)
+    assert "remap" not in out.stdout and "result=2" in out.stdout, out.stdout
