@@ -151,10 +151,10 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
 
     # BENCH_SUITE_PARTS=a,b (diagnostics): only these parts, in the suite's fixed order
     only = [x for x in os.environ.get("BENCH_SUITE_PARTS", "").split(",") if x]
-    want = lambda part: not only or part in only
+    selected = lambda part: not only or part in only
     g = torch.Generator(device="cuda")
 
-    if want("rs_ag_bf16"):
+    if selected("rs_ag_bf16"):
         trace("rs_ag_bf16")
         # --- configs[2]: ZeRO bucket, bf16, 1 GiB ---
         bucket = (64 if quick else 1024) * MIB
@@ -198,7 +198,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                                      "env": "NCCL_AMD_RS_PULL=1 NCCL_AMD_AG_PULL=1"}
         del send, shard, full, base
 
-    if want("ar_fp16_sweep"):
+    if selected("ar_fp16_sweep"):
         trace("ar_fp16_sweep")
         # --- configs[3]: fp16 AllReduce sweep: LL vs one-shot vs direct. Protocol/algorithm knobs are read at
         #     communicator init (like the reference's NCCL_PARAMs), so each column gets its own communicator ---
@@ -240,7 +240,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                 os.environ[k] = v
         del buf, res
 
-    if want("group_aggregation"):
+    if selected("group_aggregation"):
         trace("group_aggregation")
         # --- group aggregation: 32 small AllReduce ops in one ncclGroupStart/End,
         #     one LL launch vs one launch per op ---
@@ -270,7 +270,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                 os.environ[k] = v
         del buf, res
 
-    if want("reduce_int32"):
+    if selected("reduce_int32"):
         trace("reduce_int32")
         # --- configs[4]: Reduce int32 min / max, 128 MiB, root 0 ---
         S = (16 if quick else 128) * MIB
@@ -295,7 +295,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         out["reduce_int32"] = red
         del send, recv, base
 
-    if want("symmetric_window"):
+    if selected("symmetric_window"):
         trace("symmetric_window")
         # --- symmetric windows (zero-copy pull kernels): the headline AllReduce and the
         #     fp16 latency curve with send/recv inside an NCCL_WIN_COLL_SYMMETRIC window ---
@@ -335,7 +335,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         comm.deregister_window(win)
         del win_t, sendw, recvw, base, hbuf, hres
 
-    if want("staged_tuning"):
+    if selected("staged_tuning"):
         trace("staged_tuning")
         # --- staged-path tuning matrix at the headline size (data for the next tuning round: knobs are read
         #     at communicator init, so each setting gets its own communicator). Every column's result must equal the
@@ -379,7 +379,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}", "runs": tuning}
         del xs, ys, ref
 
-    if want("xgmi_probe"):
+    if selected("xgmi_probe"):
         trace("xgmi_probe")
         # --- xGMI probes (rank 0, peer copies via hipMemcpyPeerAsync) ---
         ndev = torch.cuda.device_count()
@@ -430,7 +430,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         if dist is not None:
             dist.barrier()  # the other ranks wait here, not spinning in a collective, while rank 0 probes the links
 
-    if want("registered"):
+    if selected("registered"):
         trace("registered")
         # --- buffers registered with ncclCommRegister (zero-copy kernel in registered mode): the
         #     headline AllReduce on plain torch allocations, no window. Last: the newest path, and its deregistration
