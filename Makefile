@@ -151,7 +151,7 @@ tests/native/store_atomicity_probe: tests/native/store_atomicity_probe.hip
 .PHONY: atomicity-probe
 
 # fp8 conversion probe: gfx950's fp8 convert instructions vs numerics.h's software conversions, every code and
-# every half value (GPU test tests/test_gpu_numerics.py; decides the hardware fp8 path, DESIGN.md §8)
+# every half value (GPU test tests/test_gpu_numerics.py; decides the hardware fp8 path, DESIGN.md §8.3)
 fp8-probe: tests/native/fp8_cvt_probe tests/native/fp8_f16_probe
 
 tests/native/fp8_f16_probe: tests/native/fp8_f16_probe.hip $(SRCDIR)/numerics.h

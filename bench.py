@@ -209,7 +209,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                 "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
                 "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
                 "ring": {"NCCL_ALGO": "RING"}, "tree": {"NCCL_ALGO": "TREE"}, "default": {},
-                # the reference's RING/SIMPLE partition walked by the direct kernel (DESIGN.md §2.1): its cost vs default
+                # the reference's RING/SIMPLE partition walked by the direct kernel (DESIGN.md §2.2): its cost vs default
                 "reforder": {"NCCL_AMD_REF_ORDER": "1"}}
         if os.environ.get("BENCH_SWEEP_COLS"):  # diagnostics: a subset of the columns
             cols = {k: cols[k] for k in os.environ["BENCH_SWEEP_COLS"].split(",")}
@@ -297,7 +297,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
 
     if selected("symmetric_window"):
         trace("symmetric_window")
-        # --- symmetric windows (zero-copy pull kernels, DESIGN.md §10): the headline AllReduce and the
+        # --- symmetric windows (zero-copy pull kernels, DESIGN.md §10.3): the headline AllReduce and the
         #     fp16 latency curve with send/recv inside an NCCL_WIN_COLL_SYMMETRIC window ---
         S = (16 if quick else 256) * MIB
         c = S // 4
@@ -789,7 +789,7 @@ def main(argv=None):
     # host-staged part is the only one that uses two more streams (its pipelined variant), i.e. two more hardware
     # queues per rank, which stay mapped for the rest of the process — so it runs after every part whose rate it
     # would change. Measured on the one-GPU rehearsal: once a rank process holds three or more hardware queues, every
-    # later small collective takes ~27.6 us instead of ~4 us (DESIGN.md §7, profiles/r04_queue_order_n2_onegpu.txt).
+    # later small collective takes ~27.6 us instead of ~4 us (DESIGN.md §7.2, profiles/r04_queue_order_n2_onegpu.txt).
     # BENCH_HOST_STAGED=first (diagnostics) runs it before the suite instead.
     if not args.no_extra and n > 1 and os.environ.get("BENCH_HOST_STAGED") == "first":
         run_host_staged()

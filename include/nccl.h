@@ -177,7 +177,7 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId,
 ncclResult_t pncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId commId, int rank);
 
 /* nccl.h.in:263 — several ids (same number and order on every rank); this single-node star rendezvouses at
- * commIds[0] and tells the other ids' roots to exit (DESIGN.md §10.7). */
+ * commIds[0] and tells the other ids' roots to exit (DESIGN.md §10.5). */
 ncclResult_t ncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
                                       ncclUniqueId* commIds, ncclConfig_t* config);
 ncclResult_t pncclCommInitRankScalable(ncclComm_t* newcomm, int nranks, int myrank, int nId,
@@ -222,7 +222,7 @@ ncclResult_t ncclCommMemStats(ncclComm_t comm, ncclCommMemStat_t stat, uint64_t*
 ncclResult_t pncclCommMemStats(ncclComm_t comm, ncclCommMemStat_t stat, uint64_t* value);
 
 /* ---- Buffer registration (nccl.h.in:301-307, 350-360) ---- */
-/* nccl.h.in:302 — local (non-collective) registration hint; see DESIGN.md §10. */
+/* nccl.h.in:302 — local (non-collective) registration hint; see DESIGN.md §10.3. */
 ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
 ncclResult_t pncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle);
 /* nccl.h.in:306 */

@@ -273,7 +273,7 @@ static void planChannels(ncclComm* comm, size_t blockBytes, int eltSize, LaunchP
 // NCCL_ALGO=RING AllReduce: the reference's own partition, so that every element is finalised by the same ring
 // position as in the reference's RING/SIMPLE AllReduce on a communicator of K channels (K = refChannelCount below,
 // i.e. NCCL_MIN_NCHANNELS = NCCL_MAX_NCHANNELS = K there) with the same NCCL_BUFFSIZE — bit-identical results, floats
-// included (DESIGN.md §2.1). NCCL_AMD_REF_ORDER walks the same partition, or the one of RING/LL or RING/LL128
+// included (DESIGN.md §2.2). NCCL_AMD_REF_ORDER walks the same partition, or the one of RING/LL or RING/LL128
 // (`proto` 0 / 1). For one task, starting on channel 0 with no traffic planned yet:
 //  * channels: K shrunk while the bytes are below K x threads x threshold — 512 x 64 (Simple), 512 x 8n (LL),
 //    640 x 8 (LL128) (topoGetAlgoInfo, enqueue.cc:2091-2097; tuning.cc:244-257, 589-593);

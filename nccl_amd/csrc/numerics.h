@@ -423,7 +423,7 @@ __device__ inline uint32_t fp8Encode4(const float* f) {
 // ---- 1-byte integer Sum / MinMax on four bytes per dword (SWAR) ----
 // Bit-identical to Red<uint8_t, OP>::red on each byte (tests/test_numerics.py checks every byte pair). The fold
 // uses it for uint8 / int8 so a 16-byte pack stays four registers instead of sixteen unpacked bytes, which
-// lets it keep four packs per thread in flight within the 128-VGPR co-residency budget (DESIGN.md §8).
+// lets it keep four packs per thread in flight within the 128-VGPR co-residency budget (DESIGN.md §8.2).
 template <int OP> struct Swar8 { static constexpr bool ok = false; };
 template <> struct Swar8<0> {  // DEV_SUM: byte-wise add mod 256 (carries masked out of each byte)
   static constexpr bool ok = true;

@@ -116,7 +116,7 @@ int main(int argc, char** argv) {
     HIPCK(hipSetDevice(devs[r]));
     HIPCK(hipMalloc(&send[r], maxB));
     HIPCK(hipMalloc(&recv[r], maxB));
-    // own hardware queue per rank (ranks sharing a device must run concurrently, see DESIGN.md §8)
+    // own hardware queue per rank (ranks sharing a device must run concurrently, see DESIGN.md §8.1)
     int ncu = 0;
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, devs[r]));
     std::vector<uint32_t> mask((ncu + 31) / 32, 0u);

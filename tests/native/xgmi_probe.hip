@@ -1,4 +1,4 @@
-// xgmi_probe.hip — CU-driven peer-to-peer bandwidth over xGMI (the roofline denominators of DESIGN §7):
+// xgmi_probe.hip — CU-driven peer-to-peer bandwidth over xGMI (the roofline denominators of DESIGN §5, §7):
 // GPU 0 writes to (or reads from) 1 peer and all peers at once with 16-byte vector accesses, the way the
 // collective kernels move data, instead of the SDMA engines behind hipMemcpyPeer. Prints one JSON line.
 //   xgmi_probe [MiB per peer (default 256)] [iterations (default 10)]
