@@ -21,7 +21,8 @@
 // A failed first round gets one more try: the ranks whose mappings failed re-import those peers through the hipIpc
 // handle that rides along the dma-buf export (ipc.cc; transportRemapPeer) and every rank checks again; only a failure
 // that survives it fails the init. NCCL_AMD_MAPCHECK=0 skips the check, NCCL_AMD_MAPCHECK_FALLBACK=0 the second
-// round; NCCL_AMD_MAPCHECK_FAULT=1 (tests) makes this rank skip its remote stores, =2 in the first round only.
+// round; NCCL_AMD_MAPCHECK_FAULT=1 (tests) makes this rank skip its remote stores, =2 in the first round only, =3
+// fails this rank's part of the check before its kernel (the peers must fail with ncclRemoteError at once).
 #include <string.h>
 
 #include "core.h"
@@ -174,23 +175,27 @@ static ncclResult_t localBarrier(ncclComm* c) {
 }
 
 // One round of the check for the local comms. fail[r] (every rank of the communicator, filled for the local ones):
-// bit p of .load = rank r's loads from p failed, bit p of .store = p's stores into rank r failed.
+// bit p of .load = rank r's loads from p failed, bit p of .store = p's stores into rank r failed; .err = a step of
+// the check itself failed on rank r (a HIP call, a remap). A rank whose step fails still joins both barriers and the
+// closing all-gather, so its peers learn it at once instead of waiting in a barrier for the bootstrap timeout.
 struct MapFail {
   uint32_t load, store;
+  int32_t err;
+  uint32_t pad;
 };
-static ncclResult_t mapRound(const std::vector<ncclComm*>& comms, uint64_t nonce, int attempt, std::vector<MapFail>& fail,
-                             std::string& report) {
-  ncclResult_t res = ncclSuccess;
+static ncclResult_t mapRound(const std::vector<ncclComm*>& comms, uint64_t nonce, int attempt, ncclResult_t localErr,
+                             std::vector<MapFail>& fail, std::string& report) {
+  ncclResult_t res = localErr;
   std::vector<uint64_t*> outs(comms.size(), nullptr);
   for (ncclComm* c : comms)
     if (res == ncclSuccess) res = mapPrepare(c, nonce);
-  if (res == ncclSuccess) res = localBarrier(comms[0]);
+  NCCLCHECK(localBarrier(comms[0]));
   for (size_t i = 0; i < comms.size() && res == ncclSuccess; i++) res = mapRun(comms[i], nonce, attempt, &outs[i]);
   for (size_t i = 0; i < comms.size() && res == ncclSuccess; i++) {
     (void)hipSetDevice(comms[i]->device);
     if (hipDeviceSynchronize() != hipSuccess) res = ncclUnhandledCudaError;
   }
-  if (res == ncclSuccess) res = localBarrier(comms[0]);
+  NCCLCHECK(localBarrier(comms[0]));
   for (size_t i = 0; i < comms.size() && res == ncclSuccess; i++) {
     ncclComm* c = comms[i];
     MapCheckObs obs;
@@ -221,9 +226,16 @@ static ncclResult_t mapRound(const std::vector<ncclComm*>& comms, uint64_t nonce
       (void)hipSetDevice(comms[i]->device);
       (void)hipFree(outs[i]);
     }
-  if (res != ncclSuccess) return res;
+  for (ncclComm* c : comms) fail[c->rank].err = (int32_t)res;
   // every rank learns every rank's row (a rank whose own view is clean still learns that it must remap or fail)
   if (comms[0]->bootstrap) NCCLCHECK(bootstrapAllGather(comms[0]->bootstrap, fail.data(), sizeof(MapFail)));
+  if (res != ncclSuccess) return res;
+  for (size_t r = 0; r < fail.size(); r++)
+    if (fail[r].err != ncclSuccess) {
+      WARN("mapping check: rank %zu could not run its part of the check (error %d); failing the init here too", r,
+           (int)fail[r].err);
+      return ncclRemoteError;
+    }
   return ncclSuccess;
 }
 
@@ -233,9 +245,11 @@ ncclResult_t mapCheck(const std::vector<ncclComm*>& comms) {
   (void)hipGetDevice(&oldDev);
   const int n = comms[0]->nRanks;
   const uint64_t nonce = mapNonce(comms[0]);
-  std::vector<MapFail> fail(n, MapFail{0, 0});
+  std::vector<MapFail> fail(n, MapFail{0, 0, 0, 0});
   std::string report;
-  ncclResult_t res = mapRound(comms, nonce, 0, fail, report);
+  // tests: 3 = this rank's check fails before its kernel (as a HIP error would)
+  const ncclResult_t injected = paramInt("NCCL_AMD_MAPCHECK_FAULT", 0) == 3 ? ncclUnhandledCudaError : ncclSuccess;
+  ncclResult_t res = mapRound(comms, nonce, 0, injected, fail, report);
   auto anyFail = [&]() {
     for (const MapFail& f : fail)
       if (f.load | f.store) return true;
@@ -245,18 +259,18 @@ ncclResult_t mapCheck(const std::vector<ncclComm*>& comms) {
     // Second chance for cross-process mappings: a rank re-imports every peer p whose loads through its mapping
     // failed, or into which its stores did not arrive (p's row), through the hipIpc handle that rides along the
     // dma-buf export where the runtime can open one (ipc.cc) — then every rank runs the check again. Every rank
-    // sees the same table, so all take the second round together.
-    for (const std::string& line : {report})
-      if (!line.empty()) INFO("mapping check, first round:\n%s", line.c_str());
+    // sees the same table, so all take the second round together (a rank whose remap fails joins it with the error).
+    if (!report.empty()) INFO("mapping check, first round:\n%s", report.c_str());
     report.clear();
+    ncclResult_t remap = ncclSuccess;
     for (ncclComm* c : comms) {
       const int me = c->rank;
-      for (int p = 0; p < n && res == ncclSuccess; p++) {
+      for (int p = 0; p < n && remap == ncclSuccess; p++) {
         if (p == me || !(((fail[me].load >> p) & 1) || ((fail[p].store >> me) & 1))) continue;
-        res = transportRemapPeer(c, p);
+        remap = transportRemapPeer(c, p);
       }
     }
-    if (res == ncclSuccess) res = mapRound(comms, nonce ^ 0x5eedull, 1, fail, report);
+    res = mapRound(comms, nonce ^ 0x5eedull, 1, remap, fail, report);
   }
   (void)hipSetDevice(oldDev);
   if (res != ncclSuccess) return res;

@@ -10,16 +10,23 @@
 //     skip:R          rank R's stores never arrive (NCCL_AMD_MAPCHECK_FAULT on that rank)
 //     samepid         every rank in one process (peer pointers) instead of one process per rank
 //     fixable:R:P     rank R's remap of rank P (the second round, transportRemapPeer) repairs its mapping
-// prints "result=<ncclResult_t>"; the check's WARN lines go to stderr.
+//     threads         one thread per rank, each calling mapCheck for its own comm (ncclCommInitRank), with the
+//                     bootstrap's barrier and all-gather emulated across the threads
+//     runfail:R       rank R's check kernel cannot be launched (a HIP error on that rank only)
+// prints "result=<ncclResult_t>" (rank 0's) and "results=<r0>,<r1>,..."; the check's WARN lines go to stderr.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include "../../nccl_amd/csrc/core.h"
 
 static std::vector<int> gSkip;
+static std::vector<int> gRunFail;
 
 extern "C" {
 hipError_t hipSetDevice(int) { return hipSuccess; }
@@ -49,12 +56,48 @@ hipError_t hipFree(void* p) {
 }
 
 namespace ncclamd {
-ncclResult_t bootstrapBarrier(Bootstrap*) { return ncclSuccess; }
-ncclResult_t bootstrapAllGather(Bootstrap*, void*, size_t) { return ncclSuccess; }
+// "threads" mode: the bootstrap of rank r is the pointer value r + 1; barrier and all-gather across the threads
+static int gN = 0;
+static std::mutex gMu;
+static std::condition_variable gCv;
+static int gArrived = 0, gGen = 0;
+static std::vector<char> gGather;
+static int rankOf(Bootstrap* b) { return (int)(intptr_t)b - 1; }
+static void barrier() {
+  std::unique_lock<std::mutex> lk(gMu);
+  const int gen = gGen;
+  if (++gArrived == gN) {
+    gArrived = 0;
+    gGen++;
+    gCv.notify_all();
+  } else {
+    gCv.wait(lk, [&] { return gGen != gen; });
+  }
+}
+ncclResult_t bootstrapBarrier(Bootstrap*) {
+  barrier();
+  return ncclSuccess;
+}
+ncclResult_t bootstrapAllGather(Bootstrap* b, void* data, size_t bytes) {
+  const int r = rankOf(b);
+  {
+    std::lock_guard<std::mutex> lk(gMu);
+    if (gGather.size() < bytes * gN) gGather.resize(bytes * gN);
+    memcpy(gGather.data() + r * bytes, (char*)data + r * bytes, bytes);
+  }
+  barrier();
+  {
+    std::lock_guard<std::mutex> lk(gMu);
+    memcpy(data, gGather.data(), bytes * gN);
+  }
+  barrier();
+  return ncclSuccess;
+}
 // the check kernel, on the host (kernels.hip mapCheckKernel)
 ncclResult_t launchMapCheck(const DevComm* dcp, const MapCheckArgs& a, uint64_t* out, hipStream_t) {
   const DevComm& dc = *dcp;
   const int me = dc.rank;
+  if (gRunFail[me]) return ncclUnhandledCudaError;
   for (int p = 0; p < dc.nRanks; p++) {
     if (p == me) continue;
     char* fl = (char*)dc.flags[p] + a.probeOff;
@@ -89,6 +132,9 @@ using namespace ncclamd;
 int main(int argc, char** argv) {
   const int n = argc > 1 ? atoi(argv[1]) : 2;
   gSkip.assign(n, 0);
+  gRunFail.assign(n, 0);
+  gN = n;
+  bool threads = false;
   gFixable.assign(n, std::vector<int>(n, 0));
   bool samePid = false;
   const size_t slot = 4096, probe = 8192;
@@ -108,8 +154,10 @@ int main(int argc, char** argv) {
     memset(c->staging, 0xEE, (size_t)STG_KINDS * 2 * n * slot);  // fresh memory is not zeroed
     cs[r] = c;
   }
-  for (int i = 2; i < argc; i++)
+  for (int i = 2; i < argc; i++) {
     if (!strcmp(argv[i], "samepid")) samePid = true;
+    if (!strcmp(argv[i], "threads")) threads = true;
+  }
   for (int r = 0; r < n; r++) {
     PeerInfo& p = peers[r];
     memset(&p, 0, sizeof(p));
@@ -152,12 +200,26 @@ int main(int argc, char** argv) {
       gSkip[R] = 1;
     } else if (sscanf(argv[i], "fixable:%d:%d", &R, &P) == 2) {
       gFixable[R][P] = 1;
+    } else if (sscanf(argv[i], "runfail:%d", &R) == 1) {
+      gRunFail[R] = 1;
     }
   }
   gDcs = &dcs;
   gComms = &cs;
   logInit();
-  ncclResult_t res = mapCheck(cs);
-  printf("result=%d\n", (int)res);
+  std::vector<ncclResult_t> res(n, ncclSuccess);
+  if (threads) {
+    std::vector<std::thread> ts;
+    for (int r = 0; r < n; r++) {
+      cs[r]->bootstrap = (Bootstrap*)(intptr_t)(r + 1);
+      ts.emplace_back([&, r] { res[r] = mapCheck(std::vector<ncclComm*>{cs[r]}); });
+    }
+    for (std::thread& t : ts) t.join();
+  } else {
+    res.assign(n, mapCheck(cs));
+  }
+  printf("result=%d\nresults=", (int)res[0]);
+  for (int r = 0; r < n; r++) printf("%s%d", r ? "," : "", (int)res[r]);
+  printf("\n");
   return 0;
 }

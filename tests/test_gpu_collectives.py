@@ -663,14 +663,14 @@ def test_forced_ring_and_tree(built, algo, nranks, monkeypatch):
     assert not errs, "\n".join(errs[:20])
 
 
-def _mapcheck_worker(rank, nranks, uid, q, fault_rank):
+def _mapcheck_worker(rank, nranks, uid, q, fault_rank, fault):
     try:
         logf = f"/tmp/nccl_amd_mapcheck_{os.getpid()}.log"
         os.environ.update(NCCL_DEBUG="INFO", NCCL_DEBUG_FILE=logf, NCCL_AMD_SPIN_TIMEOUT_MS="20000")
-        if rank == abs(fault_rank):
-            # 1: this rank's stores never arrive (the init fails); 2 (fault_rank < 0 here): only in the first round,
-            # so the second round's remap through hipIpc handles repairs it
-            os.environ["NCCL_AMD_MAPCHECK_FAULT"] = "1" if fault_rank > 0 else "2"
+        if rank == fault_rank:
+            # 1: this rank's stores never arrive (the init fails); 2: only in the first round, so the second round's
+            # remap through hipIpc handles repairs it; 3: this rank's part of the check fails before its kernel
+            os.environ["NCCL_AMD_MAPCHECK_FAULT"] = str(fault)
         import torch
         import nccl_amd
         torch.cuda.set_device(0)
@@ -689,15 +689,17 @@ def _mapcheck_worker(rank, nranks, uid, q, fault_rank):
         q.put((rank, ("exception", repr(e), [])))
 
 
-@pytest.mark.parametrize("fault_rank", [None, 2, -2], ids=["clean", "broken", "repaired"])
-def test_mapping_check_at_init(built, fault_rank):
+@pytest.mark.parametrize("fault", [0, 1, 2, 3], ids=["clean", "broken", "repaired", "stepfail"])
+def test_mapping_check_at_init(built, fault):
     """every communicator init stores a pattern through each peer mapping (staging and flags, the
     kernels' own write-through store) and loads the peers' patterns back before the first collective. Same-device
     here (every rank on the box's one GPU over dma-buf imports). broken: NCCL_AMD_MAPCHECK_FAULT=1 on rank 2 (its
     stores dropped in both rounds, as a broken mapping would) — every rank's init fails together with ncclSystemError
     within seconds, the ranks that saw it naming rank 2 and the failing allocation. repaired: dropped in the first
     round only — rank 2 re-imports its peers through the exports' hipIpc handles, the second round passes and the
-    AllReduce is bit-exact on those mappings (the failure branches: tests/test_mapcheck.py)."""
+    AllReduce is bit-exact on those mappings. stepfail: rank 2's part of the check fails before its kernel — it returns
+    that error and its peers ncclRemoteError at once, not after the bootstrap timeout (the failure branches:
+    tests/test_mapcheck.py)."""
     import queue
     import time
     _torch()
@@ -705,7 +707,7 @@ def test_mapping_check_at_init(built, fault_rank):
     uid = nccl_amd.get_unique_id()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_mapcheck_worker, args=(r, 3, uid, q, fault_rank if fault_rank else 99)) for r in range(3)]
+    ps = [ctx.Process(target=_mapcheck_worker, args=(r, 3, uid, q, 2 if fault else 99, fault)) for r in range(3)]
     t0 = time.time()
     for p in ps:
         p.start()
@@ -722,11 +724,17 @@ def test_mapping_check_at_init(built, fault_rank):
             p.kill()
         p.join(timeout=60)
     assert len(res) == 3, res
-    if fault_rank is None or fault_rank < 0:
+    if fault in (0, 2):
         assert all(o[0] == "ok" and o[1] and not o[2] for o in res.values()), res
-        assert res[2][3] == (fault_rank is not None) and not res[0][3] and not res[1][3], res
-    else:
+        assert res[2][3] == (fault == 2) and not res[0][3] and not res[1][3], res
+    elif fault == 1:
         assert all(o[0] == "error" and o[1] == 2 for o in res.values()), res
         for r in (0, 1):
             assert f"rank 2 (device 0" in res[r][2] and "did not arrive" in res[r][2], res[r]
+        assert time.time() - t0 < 120
+    else:
+        assert all(o[0] == "error" for o in res.values()), res
+        assert res[2][1] == 1 and res[0][1] == 6 and res[1][1] == 6, res
+        for r in (0, 1):
+            assert "rank 2 could not run its part of the check" in res[r][2], res[r]
         assert time.time() - t0 < 120

@@ -80,3 +80,30 @@ def test_second_round_remaps_and_passes(exe):
     env["NCCL_AMD_MAPCHECK_FALLBACK"] = "0"
     out = subprocess.run([exe, "3", "wrongmap:1:2:0", "fixable:1:2"], env=env, capture_output=True, text=True, timeout=30)
     assert "remap" not in out.stdout and "result=2" in out.stdout, out.stdout
+
+
+def run_all(exe, n, *args):
+    env = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_")}
+    env["NCCL_DEBUG"] = "WARN"
+    out = subprocess.run([exe, str(n), *args], env=env, capture_output=True, text=True, timeout=30)
+    assert out.returncode == 0, out.stdout + out.stderr
+    return [int(x) for x in re.search(r"results=([\d,]+)", out.stdout).group(1).split(",")], out.stderr
+
+
+def test_one_thread_per_rank_with_the_bootstrap_exchange(exe):
+    """ncclCommInitRank's form: each rank checks its own comm, the barriers and the failure-row all-gather go over the
+    (emulated) bootstrap; every rank reaches the same verdict."""
+    assert run_all(exe, 4, "threads")[0] == [0, 0, 0, 0]
+    res, err = run_all(exe, 4, "threads", "skip:3")
+    assert res == [2, 2, 2, 2], err
+    res, err = run_all(exe, 3, "threads", "wrongmap:1:2:0", "fixable:1:2")
+    assert res == [0, 0, 0], err
+
+
+def test_a_rank_whose_check_cannot_run_fails_every_rank_at_once(exe):
+    """A rank whose part of the check fails (here its kernel launch) still joins the barriers and the all-gather: it
+    returns its own error and every peer ncclRemoteError (6) naming it, instead of the peers waiting in a barrier for the
+    bootstrap timeout."""
+    res, err = run_all(exe, 4, "threads", "runfail:2")
+    assert res == [6, 6, 1, 6], err
+    assert "rank 2 could not run its part of the check" in err
