@@ -20,11 +20,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* base) {
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, -1, 0x00020000);
 }
 
-// LPOL < 0: global nontemporal load (the library's); else buffer load with cache policy LPOL.
-template <int LPOL>
+// LPOL < 0: global nontemporal load (the library's); else buffer load with cache policy LPOL. XCD: workgroup b
+// (dispatched to XCD b % 8) copies tile (b % 8) * (grid / 8) + b / 8, so each XCD streams one contiguous eighth
+// instead of every eighth tile (grid a multiple of 8).
+template <int LPOL, bool XCD = false>
 __global__ void __launch_bounds__(256) tileCopy(u32x4* __restrict__ d, const u32x4* __restrict__ s, uint64_t npk) {
   constexpr int U = 2;
-  const uint64_t t0 = (uint64_t)blockIdx.x * 256 * U;
+  const uint64_t tile = XCD ? (uint64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8 : blockIdx.x;
+  const uint64_t t0 = tile * 256 * U;
   const uint64_t base = t0 + threadIdx.x;
   u32x4 v[U];
   __amdgpu_buffer_rsrc_t rs;
@@ -44,17 +47,17 @@ __global__ void __launch_bounds__(256) tileCopy(u32x4* __restrict__ d, const u32
 static u32x4* gS[8];
 static u32x4* gD[8];
 
-template <int LPOL>
+template <int LPOL, bool XCD = false>
 static void run(const char* name, uint64_t npk, size_t bytes, int rot) {
   const int grid = (int)(npk / 512);
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  for (int i = 0; i < 8; i++) hipLaunchKernelGGL((tileCopy<LPOL>), dim3(grid), dim3(256), 0, 0, gD[i % rot], gS[i % rot], npk);
+  for (int i = 0; i < 8; i++) hipLaunchKernelGGL((tileCopy<LPOL, XCD>), dim3(grid), dim3(256), 0, 0, gD[i % rot], gS[i % rot], npk);
   const int iters = 40;
   CK(hipEventRecord(a));
   for (int i = 0; i < iters; i++)
-    hipLaunchKernelGGL((tileCopy<LPOL>), dim3(grid), dim3(256), 0, 0, gD[i % rot], gS[i % rot], npk);
+    hipLaunchKernelGGL((tileCopy<LPOL, XCD>), dim3(grid), dim3(256), 0, 0, gD[i % rot], gS[i % rot], npk);
   CK(hipEventRecord(b));
   CK(hipEventSynchronize(b));
   float ms = 0;
@@ -129,6 +132,7 @@ int main() {
     run<18>("buffer load sc1 nt", npk, bytes, rot);
     run<17>("buffer load sc0 sc1", npk, bytes, rot);
     run<19>("buffer load sc0 sc1 nt", npk, bytes, rot);
+    run<-1, true>("global nt load, XCD-contiguous tiles", npk, bytes, rot);
     run<-1>("global nt load (library)", npk, bytes, rot);
   }
   gap(S, D, npk);
