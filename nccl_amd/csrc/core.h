@@ -232,6 +232,7 @@ struct CommTuning {
   int64_t oneShotChannelBytes;  // NCCL_AMD_ONESHOT_CHANNEL_BYTES
   int copyVariant;          // NCCL_AMD_COPY_VARIANT (nRanks == 1 copy kernel, diagnostics)
   int64_t copyGrid;         // NCCL_AMD_COPY_GRID (cap on its workgroups; default: one per 16 KiB tile)
+  int copyXcdShift;         // NCCL_AMD_COPY_XCD_SHIFT (6): each XCD copies runs of 2^shift consecutive tiles
   int64_t ringChunkBytes;   // NCCL_ALGO=RING AllReduce chunk: NCCL_BUFFSIZE / NCCL_STEPS * ALLREDUCE_CHUNKSTEPS
   int refOrder;             // NCCL_AMD_REF_ORDER: AllReduce on the direct kernel in the reference's ring partition
   int refProto;             // ... of this protocol (NCCL_PROTO_LL 0, LL128 1, SIMPLE 2: the one NCCL_PROTO names)
@@ -389,6 +390,7 @@ struct LaunchPlan {  // one kernel launch (reference: struct ncclKernelPlan, src
   CollBatchArgs batch;  // ALGO_DIRECT / ALGO_ONESHOT group batch when batch.nOps > 1 (collBatchKernel)
   int copyVariant;  // ALGO_COPY
   int64_t copyGrid;
+  int copyXcdShift;
   int pipeKind;     // ALGO_PIPE: PipeKind (pipe.h)
 };
 
@@ -447,7 +449,8 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
 void windowsFree(ncclComm* comm, bool notifyPeers);
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
 ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);
-ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int variant, int64_t gridCap);
+ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int variant, int64_t gridCap,
+                        int xcdShift);
 ncclResult_t warmKernels();  // load all kernel code objects on the current device (kernels.hip)
 int typeSize(ncclDataType_t t);
 

@@ -144,6 +144,7 @@ void loadTuning(CommTuning* t) {
   t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
   t->copyVariant = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
   t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);
+  t->copyXcdShift = (int)paramInt("NCCL_AMD_COPY_XCD_SHIFT", 6);
   // the reference's RING/SIMPLE chunk: stepSize (NCCL_BUFFSIZE / NCCL_STEPS) x ALLREDUCE_CHUNKSTEPS (NCCL_STEPS / 2),
   // in 512-byte grains (enqueue.cc:2222-2225, 2321; collectives.h:19-20; default NCCL_BUFFSIZE 4 MiB, init.cc:813)
   // NCCL_AMD_REF_ORDER=1: every AllReduce folds in the reference's RING/SIMPLE order at any size, on the fast
@@ -468,6 +469,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     p.bytes = bytes;
     p.copyVariant = comm->tune.copyVariant;
     p.copyGrid = comm->tune.copyGrid;
+    p.copyXcdShift = comm->tune.copyXcdShift;
     return ncclSuccess;
   }
 

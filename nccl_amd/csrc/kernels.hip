@@ -75,12 +75,22 @@ void kernelLogNote(const void* fn, unsigned grid, unsigned block) {
 // replacement): 16 B per lane, U packs in flight per lane, grid-stride over 256*U*16-byte tiles.
 // NTL selects nontemporal loads; SPOL the store: -2 plain, -1 global nontemporal, >= 0 a buffer store with
 // that cache policy (sc0 = 1, nt = 2, sc1 = 16; offsets from the tile's own base, so 32 bits suffice)
-// (measured variants).
-template <int U, bool NTL, int SPOL>
+// (measured variants). XCD: the dispatcher hands workgroup b to XCD b % 8, so with the identity
+// mapping every XCD streams every eighth tile; instead the tiles are permuted so that each XCD streams runs of
+// 2^kshift consecutive tiles (the grid's last G % (8 << kshift) workgroups keep their own tile). Default 2^6 tiles
+// (512 KiB per XCD, 4 MiB per round): bench N=1 frac 0.911-0.916 warm, 0.798-0.807 cold vs 0.899-0.906 / 0.792-0.800
+// for the identity mapping; runs of 2^3-2^5 and 2^10-2^12 tiles were no better (profiles/r04_copy_xcd_shift_ab.txt).
+template <int U, bool NTL, int SPOL, bool XCD = false>
 __global__ void __launch_bounds__(256) copyKernel(u32x4* __restrict__ dst, const u32x4* __restrict__ src,
-                                                  uint64_t npk) {
+                                                  uint64_t npk, uint32_t kshift) {
   uint64_t stride = (uint64_t)gridDim.x * 256 * U;
-  for (uint64_t t0 = (uint64_t)blockIdx.x * 256 * U; t0 < npk; t0 += stride) {
+  uint64_t tile = blockIdx.x;
+  if constexpr (XCD) {
+    // rounds of 8 * 2^kshift tiles: XCD x takes the x-th run of 2^kshift consecutive tiles of each round
+    const uint32_t grp = 8u << kshift, j = blockIdx.x >> 3, x = blockIdx.x & 7;
+    if (blockIdx.x < gridDim.x / grp * grp) tile = (uint64_t)(j >> kshift) * grp + (x << kshift) + (j & ((1u << kshift) - 1));
+  }
+  for (uint64_t t0 = tile * 256 * U; t0 < npk; t0 += stride) {
     const uint64_t base = t0 + threadIdx.x;
     u32x4 v[U];
 #pragma unroll
@@ -103,33 +113,39 @@ __global__ void copyBytesKernel(char* dst, const char* src, uint64_t n) {
     dst[i] = src[i];
 }
 
-ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int var, int64_t gridCap) {
+ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int var, int64_t gridCap,
+                        int xcdShift) {
   if (bytes == 0 || dst == src) return ncclSuccess;
   if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0) {
     uint64_t npk = bytes >> 4;
     if (npk) {
       // variant (NCCL_AMD_COPY_VARIANT): 0 (default) nt loads + system-scope write-through buffer stores
-      // (sc0|sc1), 2 packs per thread (8 KiB tiles); 1 plain/plain U4, 2 plain/global-nt U4, 3 nt/global-nt U8,
-      // 9 nt/global-nt U4 (the round-1/2 default); nt loads with U4 buffer stores under cache policy 4 sc0|sc1,
-      // 5 sc1, 6 sc1|nt, 7 nt, 8 none (scripts/copy_policy_probe.hip, copy_shape_probe.hip)
+      // (sc0|sc1), 2 packs per thread (8 KiB tiles), tiles mapped XCD-contiguous; 10 the same with the identity
+      // tile mapping (the round-3 default); 1 plain/plain U4, 2 plain/global-nt U4, 3 nt/global-nt U8, 9 nt/global-nt
+      // U4 (the round-1/2 default); nt loads with U4 buffer stores under cache policy 4 sc0|sc1, 5 sc1, 6 sc1|nt,
+      // 7 nt, 8 none (scripts/copy_policy_probe.hip, copy_shape_probe.hip, load_policy_probe.hip)
       int U = var == 3 ? 8 : (var == 0 || var > 9) ? 2 : 4;
       uint64_t tiles = (npk + 256 * U - 1) / (256 * U);
       // one 16 KiB tile per workgroup by default: measured best on 256 MiB with buffers rotated past the
       // 256 MiB Infinity Cache (6.48 TB/s vs 6.26 for a 2048-block grid-stride; scripts/copy_variants.hip)
       int grid = (int)std::min<uint64_t>(tiles, (uint64_t)(gridCap > 0 ? gridCap : 1));
+      // the XCD runs: 2^xcdShift tiles (NCCL_AMD_COPY_XCD_SHIFT), capped at an eighth of the grid
+      uint32_t xshift = (uint32_t)std::max(0, xcdShift);
+      while (xshift > 0 && ((uint64_t)8 << xshift) > (uint64_t)grid) xshift--;
       u32x4* d = (u32x4*)dst;
       const u32x4* s = (const u32x4*)src;
       switch (var) {
-        case 1: NCCL_AMD_LAUNCH((copyKernel<4, false, -2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 2: NCCL_AMD_LAUNCH((copyKernel<4, false, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 3: NCCL_AMD_LAUNCH((copyKernel<8, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 5: NCCL_AMD_LAUNCH((copyKernel<4, true, 16>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 6: NCCL_AMD_LAUNCH((copyKernel<4, true, 18>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 7: NCCL_AMD_LAUNCH((copyKernel<4, true, 2>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 8: NCCL_AMD_LAUNCH((copyKernel<4, true, 0>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 9: NCCL_AMD_LAUNCH((copyKernel<4, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        case 4: NCCL_AMD_LAUNCH((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
-        default: NCCL_AMD_LAUNCH((copyKernel<2, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk); break;
+        case 1: NCCL_AMD_LAUNCH((copyKernel<4, false, -2>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 2: NCCL_AMD_LAUNCH((copyKernel<4, false, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 3: NCCL_AMD_LAUNCH((copyKernel<8, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 5: NCCL_AMD_LAUNCH((copyKernel<4, true, 16>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 6: NCCL_AMD_LAUNCH((copyKernel<4, true, 18>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 7: NCCL_AMD_LAUNCH((copyKernel<4, true, 2>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 8: NCCL_AMD_LAUNCH((copyKernel<4, true, 0>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 9: NCCL_AMD_LAUNCH((copyKernel<4, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 4: NCCL_AMD_LAUNCH((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 10: NCCL_AMD_LAUNCH((copyKernel<2, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        default: NCCL_AMD_LAUNCH((copyKernel<2, true, 17, true>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
       }
       HIPCHECK(hipGetLastError());
     }
@@ -185,7 +201,7 @@ ncclResult_t launchMapCheck(const DevComm* dc, const MapCheckArgs& a, uint64_t* 
 
 ncclResult_t launchPlan(const LaunchPlan& p) {
   if (p.algo == ALGO_COPY)
-    return launchCopy(p.args.recvbuff, p.args.sendbuff, p.bytes, p.stream, p.copyVariant, p.copyGrid);
+    return launchCopy(p.args.recvbuff, p.args.sendbuff, p.bytes, p.stream, p.copyVariant, p.copyGrid, p.copyXcdShift);
   if (p.func == FUNC_ALLGATHER) return launchKernGather(p);
   switch (p.datatype) {
     case ncclInt8: case ncclUint8: return launchKernU8(p);

@@ -37,6 +37,30 @@ def test_one_rank_all_cases(built):
     assert not errs, "\n".join(errs[:20])
 
 
+@pytest.mark.parametrize("variant,grid", [("0", None), ("10", None), ("0", "13"), ("0", "3")])
+def test_one_rank_copy_tile_mappings(built, monkeypatch, variant, grid):
+    """The n = 1 copy (onerank.cu:49-110's cudaMemcpyAsync, here copyKernel) under the XCD-contiguous tile mapping
+    (default) and the identity mapping (variant 10): byte-identical output at grids that are / are not multiples of 8,
+    below 8 tiles, partial last tiles and byte tails, and with a capped grid (NCCL_AMD_COPY_GRID) striding over the
+    permuted tiles."""
+    torch = _torch()
+    import nccl_amd
+    torch.cuda.set_device(0)
+    monkeypatch.setenv("NCCL_AMD_COPY_VARIANT", variant)
+    if grid:
+        monkeypatch.setenv("NCCL_AMD_COPY_GRID", grid)
+    comm = nccl_amd.Communicator.init_all([0])[0]
+    g = torch.Generator(device="cuda").manual_seed(7)
+    tile = 8192
+    for nbytes in (tile * 40, tile * 43, tile * 43 + 48, tile * 43 + 48 + 7, tile * 7, tile * 8 * 33 + 16, 5):
+        src = torch.randint(0, 256, (nbytes,), dtype=torch.uint8, device="cuda", generator=g)
+        dst = torch.zeros_like(src)
+        comm.allreduce(src, dst, nccl_amd.SUM)
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst), (variant, grid, nbytes)
+    comm.destroy()
+
+
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_single_process_multirank(built, nranks):
     torch = _torch()
