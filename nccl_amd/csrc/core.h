@@ -447,6 +447,8 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
                size_t recvBytes, const char** rmtSend, char** rmtRecv);
 // release every window and IPC mapping (destroy: also asks peers to unmap this rank's registrations; abort: not)
 void windowsFree(ncclComm* comm, bool notifyPeers);
+// graph-held registration references whose graphs are gone (register.cc): dropped at this comm's blocking calls
+void regDrainGraphReleases(ncclComm* comm);
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
 ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);
 ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int variant, int64_t gridCap,

@@ -20,6 +20,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <mutex>
 
 #include "core.h"
 
@@ -293,6 +294,82 @@ static RegAlloc* regFind(ncclComm* comm, const void* p, size_t bytes, bool captu
   return nullptr;
 }
 
+// Graph-held references (NCCL_GRAPH_REGISTER). Every captured use of a registration holds one reference, owned by a
+// hipUserObject retained by the capturing graph: the runtime destroys the object when the graph and every executable
+// instantiated from it are gone (scripts/user_object_probe.hip: on torch's HIP runtime and on /opt/rocm's, the
+// executable keeps it after hipGraphDestroy — PyTorch destroys the hipGraph_t right after instantiating it). The
+// destructor makes no HIP call; it queues (comm, tag), and the next blocking call on that communicator drops the
+// reference (regDrainGraphReleases) — the last one sends the peers RELEASE, as ncclCommDeregister does (the reference
+// ties graph registrations to the graph the same way, src/register/register.cc graph cleanup). Tags are unique in the
+// process, so a token that outlives its communicator matches nothing.
+struct GraphRelease {
+  ncclComm* comm;
+  uint64_t tag;
+};
+static std::mutex gGraphRelMu;
+static std::vector<GraphRelease> gGraphRel;
+
+static void graphReleaseFn(void* p) {
+  GraphRelease* g = (GraphRelease*)p;
+  {
+    std::lock_guard<std::mutex> lk(gGraphRelMu);
+    gGraphRel.push_back(*g);
+  }
+  delete g;
+}
+
+// Take a graph reference on `ra` (unless regAcquire just took it: `counted`) for the graph being captured on `stream`.
+// Without a user object (a runtime that refuses one) the reference stays until the communicator is destroyed.
+static void graphHold(ncclComm* comm, RegAlloc* ra, hipStream_t stream, bool counted) {
+  if (!counted) ra->graphRefs++;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nDeps = 0;
+  if (hipStreamGetCaptureInfo_v2(stream, &st, &id, &g, &deps, &nDeps) != hipSuccess || st != hipStreamCaptureStatusActive ||
+      g == nullptr) {
+    (void)hipGetLastError();
+    return;
+  }
+  GraphRelease* tok = new GraphRelease{comm, ra->tag};
+  hipUserObject_t obj = nullptr;
+  if (hipUserObjectCreate(&obj, tok, graphReleaseFn, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
+    (void)hipGetLastError();
+    delete tok;
+    return;
+  }
+  if (hipGraphRetainUserObject(g, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipUserObjectRelease(obj, 1);  // its destructor queues the release of the reference taken above
+  }
+}
+
+void regDrainGraphReleases(ncclComm* comm) {
+  std::vector<uint64_t> tags;
+  {
+    std::lock_guard<std::mutex> lk(gGraphRelMu);
+    for (size_t i = 0; i < gGraphRel.size();)
+      if (gGraphRel[i].comm == comm) {
+        tags.push_back(gGraphRel[i].tag);
+        gGraphRel[i] = gGraphRel.back();
+        gGraphRel.pop_back();
+      } else {
+        i++;
+      }
+  }
+  for (uint64_t tag : tags)
+    for (RegAlloc* ra : comm->regs)
+      if (ra->tag == tag && ra->graphRefs > 0) {
+        const bool last = ra->graphRefs == 1 && ra->localRefs == 0;
+        if (last)
+          INFO("rank %d: automatic registration of allocation %lx released (its graphs are gone)", comm->rank,
+               (unsigned long)ra->base);
+        regPut(comm, ra, true);
+        break;
+      }
+}
+
 bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
                size_t recvBytes, const char** rmtSend, char** rmtRecv) {
   if (comm->nRanks == 1) return false;
@@ -307,16 +384,27 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
   RegAlloc* rr = regFind(comm, recv, recvBytes, capturing);
   if (capturing) {
     // NCCL_GRAPH_REGISTER (reference enqueue.cc:283, coll_reg.cc:383-387): a captured collective registers its
-    // buffers itself; the registrations live until the communicator is destroyed (or their range is freed and
-    // re-allocated, regFind)
+    // buffers itself and holds them for the graph's lifetime (graphHold; a registration whose range is freed and
+    // re-allocated is dropped earlier, regFind)
     // (relaxed capture mode around the export: the capture of this thread stays valid whatever the runtime
     // deems unsafe among the calls below)
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     (void)hipThreadExchangeStreamCaptureMode(&mode);
+    regDrainGraphReleases(comm);
     RegAlloc* x = nullptr;
     ncclResult_t rsRes = ncclSuccess, rrRes = ncclSuccess;
-    if (send && !rs && (rsRes = regAcquire(comm, send, sendBytes, true, &x)) == ncclSuccess) rs = x->usable ? x : nullptr;
-    if (!rr && (rrRes = regAcquire(comm, recv, recvBytes, true, &x)) == ncclSuccess) rr = x->usable ? x : nullptr;
+    if (send && rs) {
+      graphHold(comm, rs, stream, false);
+    } else if (send && (rsRes = regAcquire(comm, send, sendBytes, true, &x)) == ncclSuccess) {
+      graphHold(comm, x, stream, true);
+      rs = x->usable ? x : nullptr;
+    }
+    if (rr) {
+      graphHold(comm, rr, stream, false);
+    } else if ((rrRes = regAcquire(comm, recv, recvBytes, true, &x)) == ncclSuccess) {
+      graphHold(comm, x, stream, true);
+      rr = x->usable ? x : nullptr;
+    }
     // a rank whose auto-registration failed captures the staged kernel while its peers may capture the zero-copy
     // one: the replay then fails fast on every rank with a kernel-mismatch error (kernels.h WaitProbe) instead of
     // waiting for the spin timeout; said here so the cause is on record
@@ -337,6 +425,11 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
 
 void windowsFree(ncclComm* comm, bool notifyPeers) {
   (void)hipSetDevice(comm->device);
+  {  // graph releases still queued for this communicator: every registration goes below anyway
+    std::lock_guard<std::mutex> lk(gGraphRelMu);
+    gGraphRel.erase(std::remove_if(gGraphRel.begin(), gGraphRel.end(), [&](const GraphRelease& g) { return g.comm == comm; }),
+                    gGraphRel.end());
+  }
   for (ncclWindow_vidmem* w : comm->windows) windowRelease(comm, w);
   comm->windows.clear();
   for (IpcMapping& m : comm->ipcMaps) ipcRelease(&m.map);
@@ -363,6 +456,7 @@ using namespace ncclamd;
 NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle) {
   NCCLCHECK(commCheck(comm, "ncclCommRegister", "comm"));
   ipcDrainReleases();
+  regDrainGraphReleases(comm);
   if (handle == nullptr) {
     WARN("ncclCommRegister : handle argument is NULL");
     return ncclInvalidArgument;
@@ -396,6 +490,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommRegister, const ncclComm_t, void*, size_t, void
 NCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle) {
   NCCLCHECK(commCheck(comm, "ncclCommDeregister", "comm"));
   ipcDrainReleases();
+  regDrainGraphReleases(comm);
   if (handle == nullptr) return ncclSuccess;  // reference commDeregister: NULL reg is a no-op
   auto it = std::find(comm->regHandles.begin(), comm->regHandles.end(), (RegHandle*)handle);
   if (it == comm->regHandles.end()) {
@@ -420,6 +515,7 @@ NCCL_EXPORT ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, siz
                                                 int winFlags) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowRegister", "comm"));
   ipcDrainReleases();
+  regDrainGraphReleases(comm);
   if (win == nullptr) {
     WARN("ncclCommWindowRegister : win argument is NULL");
     return ncclInvalidArgument;
@@ -440,6 +536,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommWindowRegister, ncclComm_t, void*, size_t, nccl
 NCCL_EXPORT ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowDeregister", "comm"));
   ipcDrainReleases();
+  regDrainGraphReleases(comm);
   if (win == nullptr) return ncclSuccess;
   auto it = std::find(comm->windows.begin(), comm->windows.end(), win);
   if (it == comm->windows.end() || win->comm != comm) {

@@ -207,6 +207,88 @@ def test_graph_register_multi_process(built):
         assert eager == 0, f"rank {r}: an eager call used an automatic registration"
 
 
+def _graph_lifetime_worker(rank, nranks, uid, q):
+    """Automatic registrations live as long as the graphs that captured them: after the executable graph is destroyed
+    (PyTorch already destroyed the hipGraph_t at instantiation), this rank's next blocking call releases them and
+    tells the peers (RELEASE), whose own next blocking call unmaps them; a new capture registers the buffers again and
+    replays bit-exact."""
+    try:
+        logf = _trace_env(f"graphlife{nranks}")
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = nccl_amd.dedicated_stream(0)
+        count = 3 << 20
+        x = torch.empty(count, dtype=torch.float32, device="cuda")
+        y = torch.empty(count, dtype=torch.float32, device="cuda")
+        dummy = torch.empty(4096, dtype=torch.uint8, device="cuda")
+
+        def capture_and_check(seed):
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g, stream=s):
+                comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+            ins = G.make_inputs(nranks, 7, count, seed=seed)
+            x.copy_(torch.from_numpy(ins[rank]))
+            torch.cuda.synchronize()
+            with torch.cuda.stream(s):
+                g.replay()
+            torch.cuda.synchronize()
+            ok = not comm.async_error() and G.same_bits(y.cpu().numpy(), oracle.all_reduce(ins, 7, 0), 7)
+            return g, ok
+
+        def blocking_call():  # any blocking entry point drains; a registration round trip is one
+            h = comm.register_buffer(dummy.data_ptr(), dummy.numel())
+            comm.deregister_buffer(h)
+
+        errs = []
+        pos0 = os.path.getsize(logf) if os.path.exists(logf) else 0
+        g, ok = capture_and_check(700)
+        if not ok:
+            errs.append(f"rank {rank}: first capture differs")
+        held = open(logf).read()[pos0:].count("automatic registration of allocation")
+        g.reset()
+        torch.cuda.synchronize()
+        time.sleep(0.3)
+        pos = os.path.getsize(logf)
+        blocking_call()  # releases this rank's automatic registrations, RELEASE to the peers
+        torch.cuda.synchronize()
+        time.sleep(0.3)
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), 1024, 7, 0, s.cuda_stream)  # every rank past its release
+        torch.cuda.synchronize()
+        blocking_call()  # unmaps what the peers released
+        text = open(logf).read()[pos:]
+        released = text.count("automatic registration of allocation")
+        peer_unmaps = sum(int(n) for n in re.findall(r"ipc: released (\d+) peer mapping", text))
+        pos = os.path.getsize(logf)
+        g2, ok = capture_and_check(701)
+        if not ok:
+            errs.append(f"rank {rank}: capture after the release differs")
+        zc = _zero_copy_lines(logf, pos)
+        del g2
+        comm.destroy()
+        q.put((rank, (errs, held, released, peer_unmaps, len(zc))))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0, 0, 0)))
+
+
+def test_graph_registrations_released_with_their_graph(built):
+    """graph auto-registrations were kept until communicator destroy. Now a hipUserObject retained by the
+    capturing graph drops the reference when the last executable of it is destroyed (register.cc graphHold)."""
+    res = _spawn(_graph_lifetime_worker, 2)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:20])
+    for r, (_, held, released, peer_unmaps, zc) in res.items():
+        assert held == 0, f"rank {r}: a registration was released while its graph lived"
+        assert released == 2, f"rank {r}: {released} automatic registrations released (want x and y)"
+        # the peer's x and y plus at least its first dummy registration (the dummies alone give at most 2)
+        assert peer_unmaps >= 3, f"rank {r}: unmapped {peer_unmaps} of the peer's released buffers (want >= 3)"
+        assert zc == 1, f"rank {r}: the re-capture planned {zc} zero-copy AllReduces (want 1)"
+
+
 def _large_worker(rank, nranks, uid, q):
     """The metric's size on registered buffers: 256 MiB fp32 per rank, every rank's sendbuff and recvbuff in
     separate torch allocations registered with ncclCommRegister, bit-exact vs the oracle at full size."""
