@@ -121,10 +121,10 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
     if (npk) {
       // variant (NCCL_AMD_COPY_VARIANT): 0 (default) nt loads + system-scope write-through buffer stores
       // (sc0|sc1), 2 packs per thread (8 KiB tiles), tiles mapped XCD-contiguous; 10 the same with the identity
-      // tile mapping (the round-3 default); 1 plain/plain U4, 2 plain/global-nt U4, 3 nt/global-nt U8, 9 nt/global-nt
+      // tile mapping (the round-3 default); 11 / 12 the default with 4 / 1 packs per thread; 1 plain/plain U4, 2 plain/global-nt U4, 3 nt/global-nt U8, 9 nt/global-nt
       // U4 (the round-1/2 default); nt loads with U4 buffer stores under cache policy 4 sc0|sc1, 5 sc1, 6 sc1|nt,
       // 7 nt, 8 none (scripts/copy_policy_probe.hip, copy_shape_probe.hip, load_policy_probe.hip)
-      int U = var == 3 ? 8 : (var == 0 || var > 9) ? 2 : 4;
+      int U = var == 3 ? 8 : var == 12 ? 1 : (var == 0 || var == 10 || var > 12) ? 2 : 4;
       uint64_t tiles = (npk + 256 * U - 1) / (256 * U);
       // one 16 KiB tile per workgroup by default: measured best on 256 MiB with buffers rotated past the
       // 256 MiB Infinity Cache (6.48 TB/s vs 6.26 for a 2048-block grid-stride; scripts/copy_variants.hip)
@@ -145,6 +145,8 @@ ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t st
         case 9: NCCL_AMD_LAUNCH((copyKernel<4, true, -1>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
         case 4: NCCL_AMD_LAUNCH((copyKernel<4, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
         case 10: NCCL_AMD_LAUNCH((copyKernel<2, true, 17>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 11: NCCL_AMD_LAUNCH((copyKernel<4, true, 17, true>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
+        case 12: NCCL_AMD_LAUNCH((copyKernel<1, true, 17, true>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
         default: NCCL_AMD_LAUNCH((copyKernel<2, true, 17, true>), dim3(grid), dim3(256), 0, stream, d, s, npk, xshift); break;
       }
       HIPCHECK(hipGetLastError());
