@@ -623,6 +623,11 @@ def main(argv=None):
     # the library names every kernel it launches in this file (read before it loads): the roofline's kernel
     # comes from the run itself
     klog = os.environ.setdefault("NCCL_AMD_KERNEL_LOG", f"/tmp/nccl_amd_bench_kernels_{os.getpid()}.log")
+    # warnings on stderr at least (the library is silent by default, as the reference is, and the GPU boxes export
+    # NCCL_DEBUG=VERSION): a failing mapping check, a remap through hipIpc handles or a clamped knob is then on record
+    # in the driver's log of a multi-GPU run
+    if os.environ.get("NCCL_DEBUG", "").upper() in ("", "NONE", "VERSION"):
+        os.environ["NCCL_DEBUG"] = "WARN"
     if os.path.exists(klog):
         os.remove(klog)
     import torch
@@ -632,12 +637,24 @@ def main(argv=None):
     dev = local % max(ndev, 1)
     torch.cuda.set_device(dev)
     dist = None
-    if n > 1:
-        import torch.distributed as dist
-        dist.init_process_group("gloo")
-        comm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
-    else:
-        comm = nccl_amd.Communicator.init_all([dev])[0]
+    try:
+        if n > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            comm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
+        else:
+            comm = nccl_amd.Communicator.init_all([dev])[0]
+    except nccl_amd.NcclError as e:
+        # e.g. the init-time mapping check failing on a new node: rank 0 still prints the line,
+        # with no rate and the library's message, so the run says why instead of ending without output
+        if rank == 0:
+            print(json.dumps({
+                "metric": METRIC, "value": 0.0, "unit": "GB/s", "n_gpus": n, "steps": args.steps, "warmup": args.warmup,
+                "ms_per_step": None, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                "data": "synthetic", "config": {"workload": "ncclAllReduce sum fp32, 256 MiB per rank", "n_ranks": n},
+                "check": "FAIL", "error": f"communicator init failed: {e} (every rank's NCCL WARN lines on stderr "
+                                          "name what failed)"}), flush=True)
+        return 1
 
     if os.path.exists(klog):  # init's own launches (the mapping check) are not the step's kernel
         os.remove(klog)

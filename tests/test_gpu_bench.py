@@ -69,3 +69,21 @@ def test_bench_one_gpu_line(built):
     assert "copyKernel" in roof["kernel"], roof
     assert 0 < roof["frac_cold"] <= 1.0 and roof["achieved_cold"] > 0
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1
+
+
+def test_bench_reports_a_failed_init(built):
+    """A communicator init that fails on every rank (here the mapping check with every rank's stores dropped, as a
+    broken cross-device mapping would) still gives the driver its one JSON line: value 0, check FAIL and the
+    library's error, and a non-zero exit — not a run that ends without output."""
+    env = dict(os.environ, NCCL_AMD_SPIN_TIMEOUT_MS="20000", NCCL_AMD_MAPCHECK_FAULT="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--quick-suite", "--no-cpu-baseline"]
+    out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=ROOT)
+    assert out.returncode != 0
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:] + out.stderr[-2000:]
+    d = json.loads(lines[0])
+    assert d["value"] == 0.0 and d["check"] == "FAIL" and "init failed" in d["error"], d
+    assert "mapping check" in d["error"] and "did not arrive" in d["error"], d
+    assert "NCCL WARN mapping check" in out.stderr, out.stderr[-3000:]  # bench.py turns on NCCL_DEBUG=WARN
