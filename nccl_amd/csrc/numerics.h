@@ -406,17 +406,23 @@ __device__ inline uint32_t fp8EncodeH2x2(fp8h2 a, fp8h2 b) {
   return __builtin_bit_cast(uint32_t, w);
 }
 
-// four fp8 VALUES (fp8RoundF results or decoded codes: exact, no rounding) -> four codes; NaN -> sign | 0x7f
+// four fp8 VALUES (fp8RoundF results or decoded codes: exact, no rounding) -> four codes; NaN -> sign | 0x7f, the
+// software encoder's (and the LL path's) NaN
 template <bool E5M2>
 __device__ inline uint32_t fp8Encode4(const float* f) {
   const int old = (int)f32AsU32(f[0]);  // high word overwritten below
   int w = E5M2 ? __builtin_amdgcn_cvt_pk_bf8_f32(f[0], f[1], old, false) : __builtin_amdgcn_cvt_pk_fp8_f32(f[0], f[1], old, false);
   w = E5M2 ? __builtin_amdgcn_cvt_pk_bf8_f32(f[2], f[3], w, true) : __builtin_amdgcn_cvt_pk_fp8_f32(f[2], f[3], w, true);
-  // the instruction encodes every NaN as 0xff: a positive NaN is 0x7f (clear bit 7 of its byte)
-  uint32_t clr = 0;
+  // the instruction encodes every NaN as 0xff (e4m3) / 0xfe (e5m2): a positive NaN clears bit 7 of its byte, and an
+  // e5m2 NaN also sets bit 0 (0xfe -> 0xff), so every path stores sign | 0x7f (tests/test_gpu_collectives.py test_single_nan_payloads)
+  uint32_t clr = 0, set = 0;
 #pragma unroll
-  for (int i = 0; i < 4; i++) clr |= f32AsU32(f[i]) - 0x7f800001u < 0x007fffffu ? 0x80u << (8 * i) : 0u;  // +NaN
-  return (uint32_t)w & ~clr;
+  for (int i = 0; i < 4; i++) {
+    const uint32_t a = f32AsU32(f[i]) & 0x7fffffffu;
+    clr |= f32AsU32(f[i]) - 0x7f800001u < 0x007fffffu ? 0x80u << (8 * i) : 0u;  // +NaN
+    if (E5M2) set |= a > 0x7f800000u ? 0x01u << (8 * i) : 0u;                      // any NaN
+  }
+  return ((uint32_t)w | set) & ~clr;
 }
 #endif
 

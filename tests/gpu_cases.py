@@ -36,9 +36,9 @@ def _raw(a: np.ndarray) -> np.ndarray:
 
 def same_bits(a: np.ndarray, b: np.ndarray, dtype: int) -> bool:
     """Bitwise equality of every element — the sign of zero included (+0 and -0 differ) — except NaN payloads: a
-    float NaN must sit where the oracle has one, its sign and payload are not compared. (NaN payload propagation is
-    the hardware's: gfx950 returns a quieted input NaN, the oracle's x86 host the same but with its own operand
-    choice when both inputs are NaN, and the reference's GPUs their own; DESIGN.md §6, unpinned corners.)"""
+    float NaN must sit where the oracle has one, its sign and payload are not compared here. (A NaN generated from
+    non-NaN inputs, or two NaNs meeting, is the hardware's: x86 and gfx950 default NaNs differ in sign. The single-NaN
+    case is compared bit for bit by test_gpu_collectives.py::test_single_nan_payloads; DESIGN.md §6.)"""
     if a.shape != b.shape:
         return False
     ua, ub = _raw(a), _raw(b)

@@ -545,6 +545,51 @@ def test_special_float_values(built, dtype):
     assert not errs, "\n".join(errs[:20])
 
 
+def test_single_nan_payloads(built):
+    """Where exactly one rank contributes a NaN (the others finite or infinite), Sum / Prod / Avg return that NaN
+    quieted, sign and payload kept, on every path (LL, one-shot, direct) — bit for bit the oracle's result — for every
+    float type; fp8 NaN is sign | 0x7f on every path (round 4: the packed e5m2 encode gave 0x7e / 0xfe). Elements
+    where a NaN is also produced from non-NaN inputs (Inf - Inf, 0 x Inf) are excluded: the default NaN and what
+    happens when two NaNs meet are the hardware's."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0, 0])
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    errs = []
+    for dtype in (7, 8, 6, 9, 10, 11):
+        es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+        vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+        for count in (4096 // es * 3 + 3, 600_000 // es, 4_000_000 // es):  # LL, one-shot, direct at n = 3
+            for op in (0, 1, 4):
+                ins = _with_specials(G.make_inputs(3, dtype, count, seed=11 + op), dtype)
+                want = G._raw(G.expected("allreduce", ins, dtype, op, 0, "")[0])
+                bufs = [torch.from_numpy(np.ascontiguousarray(x).view(vt).copy()).cuda() for x in ins]
+                outs = [torch.empty_like(b) for b in bufs]
+                with nccl_amd.group():
+                    for r, (c, st) in enumerate(zip(comms, streams)):
+                        c.all_reduce_raw(bufs[r].data_ptr(), outs[r].data_ptr(), count, dtype, op, st.cuda_stream)
+                torch.cuda.synchronize()
+                f = np.stack([G.oracle.to_f32(dtype, x) for x in ins])
+                one = np.isnan(f).sum(0) == 1
+                if op == 1:  # 0 x Inf makes a NaN of its own
+                    one &= ~(np.isinf(f).any(0) & (f == 0).any(0))
+                else:        # Inf - Inf makes a NaN of its own
+                    one &= ~((f == np.inf).any(0) & (f == -np.inf).any(0))
+                assert one.sum() > 0
+                for r in range(3):
+                    got = outs[r].cpu().numpy().view(want.dtype)
+                    bad = np.nonzero(got[one] != want[one])[0]
+                    if bad.size:
+                        errs.append(f"dtype {dtype} op {op} count {count} rank {r}: {bad.size} of {one.sum()} single-NaN "
+                                    f"elements differ, e.g. {hex(int(got[one][bad[0]]))} vs {hex(int(want[one][bad[0]]))}")
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
 @pytest.mark.parametrize("env", [{"NCCL_AMD_AG_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"},
                                  {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
                          ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots"])
