@@ -590,6 +590,77 @@ def test_single_nan_payloads(built):
     assert not errs, "\n".join(errs[:20])
 
 
+@pytest.mark.parametrize("dtype", [7, 8, 6, 9, 10, 11])
+def test_every_path_same_bits_with_specials(built, monkeypatch, dtype):
+    """The paths that fold in the same order (LL, LL128 class, one-shot, direct, direct with pulls, the zero-copy kernel
+    on registered buffers) must store the same bits for the same inputs — NaN sign and payload included, generated
+    NaNs too, since they run on the same hardware — for every operator, except where two NaNs meet in an add or a
+    multiply (below). The oracle comparison ignores NaN bits; this one does not (the round-4 e5m2 NaN encode differed
+    between the LL and the packed paths)."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    monkeypatch.setenv("NCCL_MULTI_RANK_GPU_ENABLE", "1")
+    torch.cuda.set_device(0)
+    es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+    vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    count = 48 * 1024 // es + 3
+    paths = {"LL": {"NCCL_PROTO": "LL"}, "LL128": {"NCCL_PROTO": "LL128"}, "ONESHOT": {"NCCL_ALGO": "ONESHOT"},
+             "DIRECT": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
+             "DIRECT_PULLS": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple", "NCCL_AMD_AG_PULL": "1",
+                              "NCCL_AMD_RS_PULL": "1"},
+             "REGISTERED": {"NCCL_PROTO": "Simple"}}
+    results = {}
+    for name, env in paths.items():
+        for k in ("NCCL_PROTO", "NCCL_ALGO", "NCCL_AMD_AG_PULL", "NCCL_AMD_RS_PULL"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        comms = nccl_amd.Communicator.init_all([0, 0, 0])
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        out = {}
+        for op in (0, 1, 2, 3, 4):
+            ins = _with_specials(G.make_inputs(3, dtype, count, seed=21 + op), dtype)
+            bufs = [torch.from_numpy(np.ascontiguousarray(x).view(vt).copy()).cuda() for x in ins]
+            outs = [torch.empty_like(b) for b in bufs]
+            hs = ([c.register_buffer(b.data_ptr(), b.numel() * es) for c, b in zip(comms, bufs)] +
+                  [c.register_buffer(o.data_ptr(), o.numel() * es) for c, o in zip(comms, outs)]
+                  if name == "REGISTERED" else [])
+            torch.cuda.synchronize()
+            with nccl_amd.group():
+                for r, (c, st) in enumerate(zip(comms, streams)):
+                    c.all_reduce_raw(bufs[r].data_ptr(), outs[r].data_ptr(), count, dtype, op, st.cuda_stream)
+            torch.cuda.synchronize()
+            out[op] = [o.cpu().numpy() for o in outs]
+            for i, h in enumerate(hs):
+                comms[i % 3].deregister_buffer(h)
+        for c in comms:
+            c.destroy()
+        results[name] = out
+    # Where two NaNs meet (two NaN inputs, or a NaN input and one made from Inf - Inf / 0 x Inf), which one an add or
+    # multiply returns depends on its operand order, which the compiler may commute (IEEE leaves the payload open):
+    # those elements are excluded for Sum / Prod / Avg. Min / Max pick by explicit selects: every element compared.
+    keep = {}
+    for op in (0, 1, 2, 3, 4):
+        f = np.stack([G.oracle.to_f32(dtype, x) for x in _with_specials(G.make_inputs(3, dtype, count, seed=21 + op),
+                                                                      dtype)])
+        if op in (2, 3):
+            keep[op] = np.ones(count, dtype=bool)
+            continue
+        made = (np.isinf(f).any(0) & (f == 0).any(0)) if op == 1 else ((f == np.inf).any(0) & (f == -np.inf).any(0))
+        keep[op] = np.isnan(f).sum(0) + made <= 1
+    errs = []
+    for name, out in results.items():
+        for op in out:
+            for r in range(3):
+                a, b = results["LL"][op][r][keep[op]], out[op][r][keep[op]]
+                if not np.array_equal(a, b):
+                    bad = np.nonzero(a != b)[0]
+                    errs.append(f"{name} vs LL, op {op}, rank {r}: {bad.size} elements differ, first at {bad[0]}: "
+                                f"{hex(int(b[bad[0]]))} vs {hex(int(a[bad[0]]))}")
+    assert not errs, "\n".join(errs[:20])
+
+
 @pytest.mark.parametrize("env", [{"NCCL_AMD_AG_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"},
                                  {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
                          ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots"])
