@@ -661,6 +661,77 @@ def test_every_path_same_bits_with_specials(built, monkeypatch, dtype):
     assert not errs, "\n".join(errs[:20])
 
 
+@pytest.mark.parametrize("coll", ["reducescatter", "reduce"])
+@pytest.mark.parametrize("dtype", [7, 9, 10, 11])
+def test_reduce_paths_same_bits_with_specials(built, monkeypatch, coll, dtype):
+    """As test_every_path_same_bits_with_specials, for ReduceScatter (LL, LL128 class, direct, pulls, registered
+    zero-copy) and Reduce (LL, direct; root 1): identical bits on every path, NaN included, outside the elements where
+    two NaNs meet in an add or multiply."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    monkeypatch.setenv("NCCL_MULTI_RANK_GPU_ENABLE", "1")
+    torch.cuda.set_device(0)
+    es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+    vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    per = 16 * 1024 // es + 8          # ReduceScatter: elements per rank block (16-byte aligned blocks)
+    count = 3 * per if coll == "reducescatter" else 48 * 1024 // es + 3
+    paths = {"LL": {"NCCL_PROTO": "LL"}, "DIRECT": {"NCCL_PROTO": "Simple"}}
+    if coll == "reducescatter":
+        paths.update({"LL128": {"NCCL_PROTO": "LL128"},
+                      "DIRECT_PULLS": {"NCCL_PROTO": "Simple", "NCCL_AMD_AG_PULL": "1", "NCCL_AMD_RS_PULL": "1"},
+                      "REGISTERED": {"NCCL_PROTO": "Simple"}})
+    results = {}
+    for name, env in paths.items():
+        for k in ("NCCL_PROTO", "NCCL_AMD_AG_PULL", "NCCL_AMD_RS_PULL"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        comms = nccl_amd.Communicator.init_all([0, 0, 0])
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        out = {}
+        for op in (0, 1, 2, 3, 4):
+            ins = _with_specials(G.make_inputs(3, dtype, count, seed=31 + op), dtype)
+            bufs = [torch.from_numpy(np.ascontiguousarray(x).view(vt).copy()).cuda() for x in ins]
+            outs = [torch.zeros(per if coll == "reducescatter" else count, dtype=bufs[0].dtype, device="cuda")
+                    for _ in bufs]
+            hs = ([(c, c.register_buffer(b.data_ptr(), b.numel() * es)) for c, b in zip(comms, bufs)] +
+                  [(c, c.register_buffer(o.data_ptr(), o.numel() * es)) for c, o in zip(comms, outs)]
+                  if name == "REGISTERED" else [])
+            torch.cuda.synchronize()
+            with nccl_amd.group():
+                for r, (c, st) in enumerate(zip(comms, streams)):
+                    if coll == "reducescatter":
+                        c.reduce_scatter_raw(bufs[r].data_ptr(), outs[r].data_ptr(), per, dtype, op, st.cuda_stream)
+                    else:
+                        c.reduce_raw(bufs[r].data_ptr(), outs[r].data_ptr(), count, dtype, op, 1, st.cuda_stream)
+            torch.cuda.synchronize()
+            out[op] = {r: outs[r].cpu().numpy() for r in (range(3) if coll == "reducescatter" else [1])}
+            for c, h in hs:
+                c.deregister_buffer(h)
+        for c in comms:
+            c.destroy()
+        results[name] = out
+    errs = []
+    for op in (0, 1, 2, 3, 4):
+        f = np.stack([G.oracle.to_f32(dtype, x) for x in _with_specials(G.make_inputs(3, dtype, count, seed=31 + op),
+                                                                      dtype)])
+        if op in (2, 3):
+            keep = np.ones(count, dtype=bool)
+        else:
+            made = (np.isinf(f).any(0) & (f == 0).any(0)) if op == 1 else ((f == np.inf).any(0) & (f == -np.inf).any(0))
+            keep = np.isnan(f).sum(0) + made <= 1
+        for name, out in results.items():
+            for r, b in out[op].items():
+                k = keep[r * per:(r + 1) * per] if coll == "reducescatter" else keep
+                a = results["LL"][op][r]
+                if not np.array_equal(a[k], b[k]):
+                    bad = np.nonzero(a[k] != b[k])[0]
+                    errs.append(f"{coll} {name} vs LL, op {op}, rank {r}: {bad.size} elements differ, e.g. "
+                                f"{hex(int(b[k][bad[0]]))} vs {hex(int(a[k][bad[0]]))}")
+    assert not errs, "\n".join(errs[:20])
+
+
 @pytest.mark.parametrize("env", [{"NCCL_AMD_AG_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"},
                                  {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
                          ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots"])
