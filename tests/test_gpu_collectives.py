@@ -732,6 +732,39 @@ def test_reduce_paths_same_bits_with_specials(built, monkeypatch, coll, dtype):
     assert not errs, "\n".join(errs[:20])
 
 
+@pytest.mark.parametrize("algo", ["RING", "TREE", "REF_ORDER"])
+def test_reference_algorithms_with_specials(built, monkeypatch, algo):
+    """NaN / +-Inf / +-0 / subnormal / max-finite inputs through the reference's ring and chain (pipe.h) and the
+    reference-partition direct kernel, every float type and operator, vs the oracle's ring / chain / partition fold
+    (signed zeros compared bitwise, NaN positions)."""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    monkeypatch.setenv("NCCL_MULTI_RANK_GPU_ENABLE", "1")
+    if algo == "REF_ORDER":
+        monkeypatch.setenv("NCCL_AMD_REF_ORDER", "1")
+    else:
+        monkeypatch.setenv("NCCL_ALGO", algo)
+    monkeypatch.setenv("NCCL_BUFFSIZE", "16384")
+    monkeypatch.setenv("NCCL_MAX_CTAS", "5")
+    torch.cuda.set_device(0)
+    comms = nccl_amd.Communicator.init_all([0, 0, 0])
+    cs = list(zip(comms, [torch.cuda.Stream() for _ in range(3)]))
+    errs = []
+    for dtype in (7, 8, 6, 9, 10, 11):
+        es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+        count = 200_000 // es + 5
+        for op in (0, 1, 2, 3, 4):
+            ins = _with_specials(G.make_inputs(3, dtype, count, seed=41 + op), dtype)
+            errs += G.run_case(cs, "allreduce", dtype, op, count, 0, seed=0, inputs=ins,
+                               algo="" if algo == "REF_ORDER" else algo)
+        if errs:
+            break
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
 @pytest.mark.parametrize("env", [{"NCCL_AMD_AG_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"},
                                  {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
                          ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots"])
