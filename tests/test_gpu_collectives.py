@@ -765,6 +765,97 @@ def test_reference_algorithms_with_specials(built, monkeypatch, algo):
     assert not errs, "\n".join(errs[:20])
 
 
+@pytest.mark.parametrize("dtype", [7, 9, 11, 1])
+def test_execution_modes_same_bits(built, monkeypatch, dtype):
+    """One AllReduce, the same special-value inputs, five ways: eager out of place (the reference), in place, inside a
+    group next to a second op (the batched kernel), on symmetric-window buffers (the zero-copy pull kernel), and from
+    misaligned base pointers — identical bits, NaN included (outside the elements where two NaNs meet in an add or
+    multiply), at an LL size and at a staged size. (hipGraph replay: test_gpu_api.py.)"""
+    torch = _torch()
+    import nccl_amd
+    from tests import gpu_cases as G
+    monkeypatch.setenv("NCCL_MULTI_RANK_GPU_ENABLE", "1")
+    torch.cuda.set_device(0)
+    n = 3
+    es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
+    vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    comms = nccl_amd.Communicator.init_all([0] * n)
+    streams = [torch.cuda.Stream() for _ in range(n)]
+    WIN = 8 << 20
+    wbufs = [torch.zeros(WIN, dtype=torch.uint8, device="cuda") for _ in range(n)]
+    with nccl_amd.group():
+        wins = [c.register_window(b.data_ptr(), WIN) for c, b in zip(comms, wbufs)]
+    errs = []
+    for count in (2048 // es * 3 + 1, 3_000_000 // es):
+        for op in (0, 1, 2, 3, 4):
+            ins = _with_specials(G.make_inputs(n, dtype, count, seed=51 + op), dtype) if dtype != 1 else \
+                G.make_inputs(n, dtype, count, seed=51 + op)
+            host = [np.ascontiguousarray(x).view(vt) for x in ins]
+
+            def dev(x, extra=0):
+                t = torch.zeros(x.size + extra, dtype=torch.from_numpy(x[:1]).dtype, device="cuda")
+                t[extra:].copy_(torch.from_numpy(x.copy()))
+                return t
+
+            def run(mode):
+                sends = [dev(h) for h in host]
+                recvs = [torch.zeros_like(t) for t in sends]
+                sp = [t.data_ptr() for t in sends]
+                rp = [t.data_ptr() for t in recvs]
+                if mode == "inplace":
+                    rp = sp
+                if mode == "misaligned":  # a base 1 element past a 16-byte boundary on every rank
+                    sends = [dev(h, 1) for h in host]
+                    recvs = [torch.zeros_like(t) for t in sends]
+                    sp = [t.data_ptr() + es for t in sends]
+                    rp = [t.data_ptr() + es for t in recvs]
+                if mode == "window":
+                    for w, h in zip(wbufs, host):
+                        w[:h.nbytes].copy_(torch.from_numpy(h.view(np.uint8).copy()))
+                    sp = [w.data_ptr() for w in wbufs]
+                    rp = [w.data_ptr() + WIN // 2 for w in wbufs]
+                extra = [torch.zeros(4096, dtype=torch.float32, device="cuda") for _ in range(n)]
+                torch.cuda.synchronize()
+
+                def issue():
+                    with nccl_amd.group():
+                        for r, (c, st) in enumerate(zip(comms, streams)):
+                            c.all_reduce_raw(sp[r], rp[r], count, dtype, op, st.cuda_stream)
+                            if mode == "group":
+                                c.all_reduce_raw(extra[r].data_ptr(), extra[r].data_ptr(), 4096, 7, 0, st.cuda_stream)
+                issue()
+                torch.cuda.synchronize()
+                if mode == "inplace":
+                    return [t.cpu().numpy() for t in sends]
+                if mode == "misaligned":
+                    return [t.cpu().numpy()[1:] for t in recvs]
+                if mode == "window":
+                    return [w[WIN // 2:WIN // 2 + count * es].cpu().numpy().view(vt) for w in wbufs]
+                return [t.cpu().numpy() for t in recvs]
+
+            ref = run("eager")
+            f = np.stack([G.oracle.to_f32(dtype, x) for x in ins]) if dtype != 1 else None
+            if f is None or op in (2, 3):
+                keep = np.ones(count, dtype=bool)
+            else:
+                made = (np.isinf(f).any(0) & (f == 0).any(0)) if op == 1 else ((f == np.inf).any(0) & (f == -np.inf).any(0))
+                keep = np.isnan(f).sum(0) + made <= 1
+            for mode in ("inplace", "group", "window", "misaligned"):
+                got = run(mode)
+                for r in range(n):
+                    a, b = ref[r][keep], got[r][keep]
+                    if not np.array_equal(a, b):
+                        bad = np.nonzero(a != b)[0]
+                        errs.append(f"count {count} op {op} {mode} rank {r}: {bad.size} differ, e.g. "
+                                    f"{hex(int(b[bad[0]]))} vs {hex(int(a[bad[0]]))}")
+    with nccl_amd.group():
+        for c, w in zip(comms, wins):
+            c.deregister_window(w)
+    for c in comms:
+        c.destroy()
+    assert not errs, "\n".join(errs[:20])
+
+
 @pytest.mark.parametrize("env", [{"NCCL_AMD_AG_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"},
                                  {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
                          ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots"])
