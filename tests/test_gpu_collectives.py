@@ -517,6 +517,26 @@ def _with_specials(inputs, dtype):
     return out
 
 
+def _int_view(dtype):
+    """The integer type of dtype's width: raw element bits on the host and in torch."""
+    from tests import gpu_cases as G
+    return {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize]
+
+
+def _comparable(ins, dtype, op):
+    """Elements whose result bits are defined for Sum / Prod / Avg: at most one NaN arises in the fold (one NaN input
+    and no NaN made from Inf - Inf / 0 x Inf, or none at all). Where two NaNs meet, which one an add or multiply returns
+    depends on its operand order, which the compiler may commute (IEEE leaves the payload open). Min / Max (explicit
+    selects) and integer types: every element."""
+    from tests import gpu_cases as G
+    count = ins[0].size
+    if op in (2, 3) or dtype not in G.FLOAT_TYPES:
+        return np.ones(count, dtype=bool)
+    f = np.stack([G.oracle.to_f32(dtype, x) for x in ins])
+    made = (np.isinf(f).any(0) & (f == 0).any(0)) if op == 1 else ((f == np.inf).any(0) & (f == -np.inf).any(0))
+    return np.isnan(f).sum(0) + made <= 1
+
+
 @pytest.mark.parametrize("dtype", [7, 8, 6, 9, 10, 11])
 def test_special_float_values(built, dtype):
     """NaN / ±Inf / ±0 / subnormal / max-finite inputs, combined across 3 ranks, through every path (LL,
@@ -561,7 +581,7 @@ def test_single_nan_payloads(built):
     errs = []
     for dtype in (7, 8, 6, 9, 10, 11):
         es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
-        vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+        vt = _int_view(dtype)
         for count in (4096 // es * 3 + 3, 600_000 // es, 4_000_000 // es):  # LL, one-shot, direct at n = 3
             for op in (0, 1, 4):
                 ins = _with_specials(G.make_inputs(3, dtype, count, seed=11 + op), dtype)
@@ -572,12 +592,7 @@ def test_single_nan_payloads(built):
                     for r, (c, st) in enumerate(zip(comms, streams)):
                         c.all_reduce_raw(bufs[r].data_ptr(), outs[r].data_ptr(), count, dtype, op, st.cuda_stream)
                 torch.cuda.synchronize()
-                f = np.stack([G.oracle.to_f32(dtype, x) for x in ins])
-                one = np.isnan(f).sum(0) == 1
-                if op == 1:  # 0 x Inf makes a NaN of its own
-                    one &= ~(np.isinf(f).any(0) & (f == 0).any(0))
-                else:        # Inf - Inf makes a NaN of its own
-                    one &= ~((f == np.inf).any(0) & (f == -np.inf).any(0))
+                one = _comparable(ins, dtype, op) & (np.isnan(np.stack([G.oracle.to_f32(dtype, x) for x in ins])).sum(0) == 1)
                 assert one.sum() > 0
                 for r in range(3):
                     got = outs[r].cpu().numpy().view(want.dtype)
@@ -603,7 +618,7 @@ def test_every_path_same_bits_with_specials(built, monkeypatch, dtype):
     monkeypatch.setenv("NCCL_MULTI_RANK_GPU_ENABLE", "1")
     torch.cuda.set_device(0)
     es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
-    vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    vt = _int_view(dtype)
     count = 48 * 1024 // es + 3
     paths = {"LL": {"NCCL_PROTO": "LL"}, "LL128": {"NCCL_PROTO": "LL128"}, "ONESHOT": {"NCCL_ALGO": "ONESHOT"},
              "DIRECT": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
@@ -637,18 +652,8 @@ def test_every_path_same_bits_with_specials(built, monkeypatch, dtype):
         for c in comms:
             c.destroy()
         results[name] = out
-    # Where two NaNs meet (two NaN inputs, or a NaN input and one made from Inf - Inf / 0 x Inf), which one an add or
-    # multiply returns depends on its operand order, which the compiler may commute (IEEE leaves the payload open):
-    # those elements are excluded for Sum / Prod / Avg. Min / Max pick by explicit selects: every element compared.
-    keep = {}
-    for op in (0, 1, 2, 3, 4):
-        f = np.stack([G.oracle.to_f32(dtype, x) for x in _with_specials(G.make_inputs(3, dtype, count, seed=21 + op),
-                                                                      dtype)])
-        if op in (2, 3):
-            keep[op] = np.ones(count, dtype=bool)
-            continue
-        made = (np.isinf(f).any(0) & (f == 0).any(0)) if op == 1 else ((f == np.inf).any(0) & (f == -np.inf).any(0))
-        keep[op] = np.isnan(f).sum(0) + made <= 1
+    keep = {op: _comparable(_with_specials(G.make_inputs(3, dtype, count, seed=21 + op), dtype), dtype, op)
+            for op in (0, 1, 2, 3, 4)}
     errs = []
     for name, out in results.items():
         for op in out:
@@ -673,7 +678,7 @@ def test_reduce_paths_same_bits_with_specials(built, monkeypatch, coll, dtype):
     monkeypatch.setenv("NCCL_MULTI_RANK_GPU_ENABLE", "1")
     torch.cuda.set_device(0)
     es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
-    vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    vt = _int_view(dtype)
     per = 16 * 1024 // es + 8          # ReduceScatter: elements per rank block (16-byte aligned blocks)
     count = 3 * per if coll == "reducescatter" else 48 * 1024 // es + 3
     paths = {"LL": {"NCCL_PROTO": "LL"}, "DIRECT": {"NCCL_PROTO": "Simple"}}
@@ -714,13 +719,7 @@ def test_reduce_paths_same_bits_with_specials(built, monkeypatch, coll, dtype):
         results[name] = out
     errs = []
     for op in (0, 1, 2, 3, 4):
-        f = np.stack([G.oracle.to_f32(dtype, x) for x in _with_specials(G.make_inputs(3, dtype, count, seed=31 + op),
-                                                                      dtype)])
-        if op in (2, 3):
-            keep = np.ones(count, dtype=bool)
-        else:
-            made = (np.isinf(f).any(0) & (f == 0).any(0)) if op == 1 else ((f == np.inf).any(0) & (f == -np.inf).any(0))
-            keep = np.isnan(f).sum(0) + made <= 1
+        keep = _comparable(_with_specials(G.make_inputs(3, dtype, count, seed=31 + op), dtype), dtype, op)
         for name, out in results.items():
             for r, b in out[op].items():
                 k = keep[r * per:(r + 1) * per] if coll == "reducescatter" else keep
@@ -778,7 +777,7 @@ def test_execution_modes_same_bits(built, monkeypatch, dtype):
     torch.cuda.set_device(0)
     n = 3
     es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
-    vt = {1: np.uint8, 2: np.int16, 4: np.int32, 8: np.int64}[es]
+    vt = _int_view(dtype)
     comms = nccl_amd.Communicator.init_all([0] * n)
     streams = [torch.cuda.Stream() for _ in range(n)]
     WIN = 8 << 20
@@ -834,12 +833,7 @@ def test_execution_modes_same_bits(built, monkeypatch, dtype):
                 return [t.cpu().numpy() for t in recvs]
 
             ref = run("eager")
-            f = np.stack([G.oracle.to_f32(dtype, x) for x in ins]) if dtype != 1 else None
-            if f is None or op in (2, 3):
-                keep = np.ones(count, dtype=bool)
-            else:
-                made = (np.isinf(f).any(0) & (f == 0).any(0)) if op == 1 else ((f == np.inf).any(0) & (f == -np.inf).any(0))
-                keep = np.isnan(f).sum(0) + made <= 1
+            keep = _comparable(ins, dtype, op)
             for mode in ("inplace", "group", "window", "misaligned"):
                 got = run(mode)
                 for r in range(n):
