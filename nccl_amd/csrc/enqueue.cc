@@ -177,14 +177,15 @@ void loadTuning(CommTuning* t) {
 // saturation, enqueue.cc:2091-2105; tuning.cc:243-400). The links bound those plans on the 8-GPU node: a rank
 // sends 2S/n over each of its n-1 links, taking 2S/n / B_link, while its local HBM moves (2 + 4(n-1)/n) S
 // (staged path), so keeping the links busy takes (3n - 2) B_link of HBM copy traffic, and a
-// workgroup copies at most R_cu ≈ 50 GB/s (profiles/r02_wg_rate_probe.txt). With B_link ≈ 64 GB/s per
-// direction and 2x headroom, rounded up to a power of two (>= 32): 32 channels at n = 3..4, 64 at n = 5..8 —
+// workgroup copies at most R_cu ≈ 50 GB/s (profiles/r02_wg_rate_probe.txt; a local-copy rate, an upper bound for
+// remote stores). With B_link = 76.8 GB/s per direction (153.6 GB/s per link read as bidirectional)
+// and 2x headroom, rounded up to a power of two (>= 32): 32 channels at n = 3..4, 64 at n = 5..7, 128 at n = 8 —
 // the rest of the chip stays free for the compute a collective overlaps. n = 2 keeps every channel (one link,
 // nothing to overlap in the bench). NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS / config.maxCTAs overrule it, as does
 // NCCL_AMD_LINK_CHANNELS (0 = no budget).
 int linkChannelBudget(int n) {
   if (n < 3) return 0;
-  const double bLinkGBps = 64.0, cuGBps = 50.0, headroom = 2.0;
+  const double bLinkGBps = 76.8, cuGBps = 50.0, headroom = 2.0;
   const double need = (3.0 * n - 2.0) * bLinkGBps / cuGBps * headroom;
   int c = 32;
   while (c < need && c < NCCL_AMD_MAX_CHANNELS) c *= 2;
