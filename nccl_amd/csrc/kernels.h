@@ -321,6 +321,69 @@ __device__ __forceinline__ void copyRange(void* dst, const void* src, uint64_t n
   }
 }
 
+// One source copied to several destinations with ONE read of it: an optional local copy (dstLocal, plain stores)
+// and nPush remote copies (system-scope write-through stores, one buffer resource per destination and batch).
+// copyRange per destination read the source once per destination — nontemporal loads do not keep it in L2, so
+// the AllGather publish read its block n times from HBM (PMC at n = 2: 2.96 S per rank instead of 2.5 S,
+// profiles/pmc_traffic.json) and the one-shot publish n - 1 times.
+template <typename T>
+__device__ __forceinline__ void copyRangeMulti(char* dstLocal, char* const* dstPush, int nPush, const void* src,
+                                               uint64_t nbytes, bool aligned) {
+  if (nPush == 1 && !dstLocal) return copyRange<T, true>(dstPush[0], src, nbytes, aligned);  // one destination:
+  if (nPush == 0) return dstLocal ? copyRange<T, false>(dstLocal, src, nbytes, aligned) : void();  // the plain copy
+  if (aligned) {
+    const uint64_t npk = nbytes >> 4;
+    const u32x4* s = (const u32x4*)src;
+    constexpr int U = kCopyUnroll;
+    uint64_t i = threadIdx.x;
+    for (; i + (U - 1) * kThreads < npk; i += U * kThreads) {
+      u32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; u++) v[u] = __builtin_nontemporal_load(s + i + u * kThreads);
+      if (dstLocal) {
+        LocalStore ls(dstLocal, i - threadIdx.x);
+#pragma unroll
+        for (int u = 0; u < U; u++) ls.put(threadIdx.x + u * kThreads, v[u]);
+      }
+      for (int p = 0; p < nPush; p++) {
+        u32x4* d = (u32x4*)dstPush[p];
+        if (NCCL_AMD_BUFFER_STORES) {
+          const __amdgpu_buffer_rsrc_t rd = remoteRsrc(d + (i - threadIdx.x));
+#pragma unroll
+          for (int u = 0; u < U; u++) storeRemoteAt(rd, (uint32_t)((threadIdx.x + u * kThreads) * 16), v[u]);
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; u++) storeRemote(d + i + u * kThreads, v[u]);
+        }
+      }
+    }
+    for (; i < npk; i += kThreads) {
+      const u32x4 v = __builtin_nontemporal_load(s + i);
+      if (dstLocal) __builtin_nontemporal_store(v, (u32x4*)dstLocal + i);
+      for (int p = 0; p < nPush; p++) {
+        u32x4* d = (u32x4*)dstPush[p];
+        if (NCCL_AMD_BUFFER_STORES) storeRemoteAt(remoteRsrc(d + (i - threadIdx.x)), threadIdx.x * 16u, v);
+        else storeRemote(d + i, v);
+      }
+    }
+    const uint64_t done = npk << 4;
+    const uint64_t tail = (nbytes - done) / sizeof(T);
+    if (threadIdx.x < tail) {
+      const T x = ((const T*)((const char*)src + done))[threadIdx.x];
+      if (dstLocal) ((T*)(dstLocal + done))[threadIdx.x] = x;
+      for (int p = 0; p < nPush; p++) storeRemoteElt((T*)(dstPush[p] + done) + threadIdx.x, x);
+    }
+  } else {
+    const uint64_t n = nbytes / sizeof(T);
+    const T* s = (const T*)src;
+    for (uint64_t i = threadIdx.x; i < n; i += kThreads) {
+      const T x = s[i];
+      if (dstLocal) ((T*)dstLocal)[i] = x;
+      for (int p = 0; p < nPush; p++) storeRemoteElt((T*)dstPush[p] + i, x);
+    }
+  }
+}
+
 template <typename T>
 union PackU {
   u32x4 v;
@@ -786,9 +849,8 @@ struct Channel {
     __syncthreads();
     if (COLL == COLL_AG) {
       const char* src = (const char*)a.sendbuff + lo * ts;
-      for (int i = 0; i < sh.nPush; i++) copyRange<T, true>(sh.pushPtr[i], src, nelem * ts, aligned);
       char* dst = (char*)a.recvbuff + ((uint64_t)me * a.chunk + lo) * ts;
-      if (dst != src) copyRange<T, false>(dst, src, nelem * ts, aligned);
+      copyRangeMulti<T>(dst != src ? dst : nullptr, sh.pushPtr, sh.nPush, src, nelem * ts, aligned);
     } else {
       char* dstLocal = nullptr;
       if (COLL == COLL_RS) dstLocal = (char*)a.recvbuff + lo * ts;
@@ -831,11 +893,14 @@ struct Channel {
     uint64_t lo, hi;
     sliceRange(a, cl, step, a.count, lo, hi);
     const char* src = (const char*)a.sendbuff + lo * ts;
-    for (int k = 1; k < n; k++) {
-      int p = peerAt(k);
-      int slot = (int)(ctr(CTR_SEND_RS, p) % nSlots);
-      copyRange<T, true>(dc.staging[p] + stagingOffset(dc, c, STG_RS, slot, me), src, (hi - lo) * ts, aligned);
+    if (threadIdx.x == 0) {
+      for (int k = 1; k < n; k++) {
+        int p = peerAt(k);
+        sh.pushPtr[k - 1] = dc.staging[p] + stagingOffset(dc, c, STG_RS, (int)(ctr(CTR_SEND_RS, p) % nSlots), me);
+      }
     }
+    __syncthreads();
+    copyRangeMulti<T>(nullptr, sh.pushPtr, n - 1, src, (hi - lo) * ts, aligned);
     if (tid < NCCL_AMD_MAX_RANKS) {
       bool act = tid < n && tid != me;
       sh.sigVal[tid] = act ? ctr(CTR_SEND_RS, tid) + 1 : 0;

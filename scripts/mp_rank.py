@@ -1,8 +1,9 @@
 """One rank of a 2-process AllReduce on the one-GPU box, rendezvous through a file (no launcher, so one
 of the two processes can run under rocprofv3 without any process being spawned from a profiled one).
-usage: mp_rank.py RANK UIDFILE [ITERS] [staged|sym|reg] — rank 1 creates the ncclUniqueId and writes it to
-UIDFILE; `sym` puts both buffers in a symmetric window, `reg` registers them with ncclCommRegister (zero-copy
-kernels either way)."""
+usage: mp_rank.py RANK UIDFILE [ITERS] [staged|sym|reg|rs|ag|ring|reforder] — rank 1 creates the ncclUniqueId and
+writes it to UIDFILE; `sym` puts both buffers in a symmetric window, `reg` registers them with ncclCommRegister
+(zero-copy kernels either way); `rs` / `ag` run ReduceScatter (S in, S/2 out) / AllGather (S/2 in, S out) on the
+staged path; `ring` / `reforder` the AllReduce with NCCL_ALGO=RING / NCCL_AMD_REF_ORDER=1 at K = 32 reference parts."""
 import os
 import sys
 import time
@@ -28,10 +29,14 @@ def main():
                 raise TimeoutError("no unique id")
             time.sleep(0.05)
         uid = open(path, "rb").read()
+    mode = sys.argv[4] if len(sys.argv) > 4 else "staged"
+    if mode == "ring":
+        os.environ.update(NCCL_ALGO="RING", NCCL_AMD_REF_NCHANNELS="32")
+    if mode == "reforder":
+        os.environ.update(NCCL_AMD_REF_ORDER="1", NCCL_AMD_REF_NCHANNELS="32")
     torch.cuda.set_device(0)
     comm = nccl_amd.Communicator.init(2, rank, uid)
     S = 256 << 20
-    mode = sys.argv[4] if len(sys.argv) > 4 else "staged"
     if mode == "sym":
         win_t = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
         win = comm.register_window(win_t.data_ptr(), 2 * S)
@@ -44,10 +49,22 @@ def main():
     if mode == "reg":
         regs = [comm.register_buffer(x.data_ptr(), S), comm.register_buffer(y.data_ptr(), S)]
     s = torch.cuda.current_stream()
+    if mode == "ag":
+        y = torch.empty(S // 4, dtype=torch.float32, device="cuda")
     for _ in range(2 + iters):
-        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), S // 4, 7, 0, s.cuda_stream)
+        if mode == "rs":
+            comm.reduce_scatter_raw(x.data_ptr(), y.data_ptr(), S // 8, 7, 0, s.cuda_stream)
+        elif mode == "ag":
+            comm.all_gather_raw(x.data_ptr(), y.data_ptr(), S // 8, 7, s.cuda_stream)
+        else:
+            comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), S // 4, 7, 0, s.cuda_stream)
     torch.cuda.synchronize()
-    ok = bool((y == 3.0).all())
+    if mode == "rs":
+        ok = bool((y[:S // 8] == 3.0).all())
+    elif mode == "ag":
+        ok = bool((y[:S // 8] == 1.0).all()) and bool((y[S // 8:] == 2.0).all())
+    else:
+        ok = bool((y == 3.0).all())
     print(f"rank {rank}: ok={ok} async={comm.async_error()}", flush=True)
     if mode == "sym":
         comm.deregister_window(win)
