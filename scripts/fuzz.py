@@ -207,12 +207,17 @@ def main():
             mis = rng.choice([0, 0, 0, 1, 3])
             inplace = mis == 0 and rng.random() < 0.25
             root = rng.randrange(n)
-            errs = G.run_case(cs, coll, dt, op, count, mis, seed=rng.randrange(1 << 30), inplace=inplace, root=root)
+            seed = rng.randrange(1 << 30)
+            ins, special = None, dt in G.FLOAT_TYPES and rng.random() < 0.3
+            if special:  # NaN / +-Inf / +-0 / subnormals / max-finite at every 37th element (oracle: NaN positions)
+                from tests.test_gpu_collectives import _with_specials
+                ins = _with_specials(G.make_inputs(n, dt, count, seed), dt)
+            errs = G.run_case(cs, coll, dt, op, count, mis, seed=seed, inplace=inplace, root=root, inputs=ins)
             total += 1
             done += 1
             if errs:
                 failures.append(f"n={n} env={env} {coll} dt={dt} op={op} count={count} mis={mis} inplace={inplace} "
-                                f"root={root}: {errs[:3]}")
+                                f"root={root} specials={special}: {errs[:3]}")
                 break
         for c in comms:
             c.destroy()
