@@ -829,6 +829,10 @@ def main(argv=None):
             out["xgmi_links"] = ({"wt_uncached_write_per_link_GBps": pr.get("wt_uncached_write_per_link_GBps"),
                                   "read_per_link_GBps": pr.get("read_per_link_GBps"),
                                   "wt_uncached_write_fanout_GBps": pr.get("wt_uncached_write_fanout_GBps"),
+                                  # the fan-out rate by workgroup count: what one channel sustains across the links,
+                                  # the constant behind the n >= 3 CU budget (enqueue.cc linkChannelBudget)
+                                  "wt_uncached_write_fanout_by_workgroups_GBps":
+                                      pr.get("wt_uncached_write_fanout_by_workgroups_GBps"),
                                   "source": "tests/native/xgmi_probe on rank 0 (GPU 0 -> each peer GPU)"}
                                  if pr else {"skipped": "the ranks share one GPU: no link to measure"})
             runs = {json.dumps(r["env"], sort_keys=True): r for r in extra.get("suite", {}).get("staged_tuning", {}).get("runs", [])}

@@ -26,20 +26,30 @@ struct Targets {
   int n;
 };
 
-// workgroup b moves its share of pair (b % n): a grid-stride copy of `vecs` 16-byte vectors per pair
+// workgroup b moves its share of pair (b % n): a grid-stride copy of `vecs` 16-byte vectors per pair, 4 vectors per
+// thread in flight (loads first, then stores), as the collective kernels keep them (kernels.h kFoldUnroll)
 template <bool WT>
 __global__ void __launch_bounds__(512) copyPairs(Targets t, size_t vecs) {
+  constexpr int U = 4;
   const int pair = blockIdx.x % t.n;
   const size_t wgPerPair = gridDim.x / t.n;
   const size_t w = blockIdx.x / t.n;
   u32x4* d = t.dst[pair];
   const u32x4* s = t.src[pair];
-  for (size_t i = w * blockDim.x + threadIdx.x; i < vecs; i += wgPerPair * blockDim.x) {
-    u32x4 v = __builtin_nontemporal_load(s + i);
-    if (WT)  // the collective kernels' remote store: write-through at system scope (kernels.h storeRemote)
-      asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(d + i), "v"(v) : "memory");
-    else
-      __builtin_nontemporal_store(v, d + i);
+  for (size_t b = w * blockDim.x * U + threadIdx.x; b < vecs; b += wgPerPair * blockDim.x * U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (b + u * blockDim.x < vecs) v[u] = __builtin_nontemporal_load(s + b + u * blockDim.x);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const size_t i = b + u * blockDim.x;
+      if (i >= vecs) continue;
+      if (WT)  // the collective kernels' remote store: write-through at system scope (kernels.h storeRemote)
+        asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(d + i), "v"(v[u]) : "memory");
+      else
+        __builtin_nontemporal_store(v[u], d + i);
+    }
   }
 }
 
@@ -83,7 +93,7 @@ int main(int argc, char** argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   // first: the first peer (GPU 1 + first) of the npeers consecutive ones
-  auto run = [&](bool write, int npeers, bool wt = false, int first = 0) -> double {
+  auto run = [&](bool write, int npeers, bool wt = false, int first = 0, int wgs = 0) -> double {
     Targets t = {};
     t.n = npeers;
     for (int k = 0; k < npeers; k++) {
@@ -97,7 +107,7 @@ int main(int argc, char** argv) {
         t.dst[k] = (u32x4*)mine;
       }
     }
-    const int grid = (2 * cus / npeers) * npeers;
+    const int grid = wgs > 0 ? (wgs < npeers ? npeers : wgs / npeers * npeers) : (2 * cus / npeers) * npeers;
     auto launch = [&]() {
       if (wt) hipLaunchKernelGGL(copyPairs<true>, dim3(grid), dim3(512), 0, s, t, bytes / 16);
       else hipLaunchKernelGGL(copyPairs<false>, dim3(grid), dim3(512), 0, s, t, bytes / 16);
@@ -135,10 +145,22 @@ int main(int argc, char** argv) {
   }
   wl += "]";
   rl += "]";
+  // the fan-out in the collective's store flavour driven by 8 ... 256 workgroups of 512 threads: the rate one
+  // workgroup sustains across the links (enqueue.cc linkChannelBudget assumes the local-copy ~50 GB/s)
+  std::string gw = "{";
+  int first = 1;
+  for (int g : {8, 16, 32, 64, 128, 256}) {
+    snprintf(num, sizeof(num), "%s\"%d\": %.1f", first ? "" : ", ", g, run(true, all, true, 0, g));
+    gw += num;
+    first = 0;
+  }
+  gw += "}";
   printf("{\"method\": \"CU copy kernel on GPU 0, 16-byte nontemporal vectors, %zu MiB per peer, %d iters%s\", "
          "\"peers\": %d, \"write_1link_GBps\": %.1f, \"read_1link_GBps\": %.1f, \"write_fanout_GBps\": %.1f, "
          "\"read_fanin_GBps\": %.1f, \"wt_uncached_write_1link_GBps\": %.1f, \"wt_uncached_write_fanout_GBps\": %.1f, "
-         "\"wt_uncached_write_per_link_GBps\": %s, \"read_per_link_GBps\": %s, \"wrong_bytes\": %zu}\n",
-         mib, iters, loop ? ", LOOPBACK on one GPU" : "", all, w1, r1, wa, ra, u1, ua, wl.c_str(), rl.c_str(), wrong);
+         "\"wt_uncached_write_per_link_GBps\": %s, \"read_per_link_GBps\": %s, "
+         "\"wt_uncached_write_fanout_by_workgroups_GBps\": %s, \"wrong_bytes\": %zu}\n",
+         mib, iters, loop ? ", LOOPBACK on one GPU" : "", all, w1, r1, wa, ra, u1, ua, wl.c_str(), rl.c_str(), gw.c_str(),
+         wrong);
   return wrong ? 1 : 0;
 }

@@ -46,6 +46,9 @@ def test_xgmi_probe_loopback(built):
     # one rate per link of GPU 0 (the bench line's xgmi_links at N > 1)
     assert len(rep["wt_uncached_write_per_link_GBps"]) == rep["peers"] == len(rep["read_per_link_GBps"])
     assert all(x > 0 for x in rep["wt_uncached_write_per_link_GBps"] + rep["read_per_link_GBps"])
+    # the fan-out by workgroup count (the CU budget's per-channel rate)
+    assert sorted(int(g) for g in rep["wt_uncached_write_fanout_by_workgroups_GBps"]) == [8, 16, 32, 64, 128, 256]
+    assert all(x > 0 for x in rep["wt_uncached_write_fanout_by_workgroups_GBps"].values())
 
 
 def test_store_atomicity_probe_one_gpu(built):
