@@ -379,6 +379,9 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     capturing = hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
     (void)hipGetLastError();
   }
+  // graph references whose graphs are gone are dropped BEFORE the lookup: dropping one may free a registration the
+  // lookup would otherwise hand back
+  if (capturing) regDrainGraphReleases(comm);
   if (comm->regs.empty() && !capturing) return false;
   RegAlloc* rs = send ? regFind(comm, send, sendBytes, capturing) : nullptr;
   RegAlloc* rr = regFind(comm, recv, recvBytes, capturing);
@@ -390,7 +393,6 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     // deems unsafe among the calls below)
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     (void)hipThreadExchangeStreamCaptureMode(&mode);
-    regDrainGraphReleases(comm);
     RegAlloc* x = nullptr;
     ncclResult_t rsRes = ncclSuccess, rrRes = ncclSuccess;
     if (send && rs) {

@@ -268,7 +268,15 @@ def _graph_lifetime_worker(rank, nranks, uid, q):
         if not ok:
             errs.append(f"rank {rank}: capture after the release differs")
         zc = _zero_copy_lines(logf, pos)
-        del g2
+        # the next capture right after the graph is gone, with no blocking call between: the capture itself drops
+        # the released references before it looks the buffers up (it must not hand back a registration it frees)
+        g2.reset()
+        torch.cuda.synchronize()
+        time.sleep(0.3)
+        g3, ok = capture_and_check(702)
+        if not ok:
+            errs.append(f"rank {rank}: capture right after the graph's release differs")
+        del g3
         comm.destroy()
         q.put((rank, (errs, held, released, peer_unmaps, len(zc))))
     except Exception as e:
