@@ -306,14 +306,22 @@ struct GraphRelease {
   ncclComm* comm;
   uint64_t tag;
 };
-static std::mutex gGraphRelMu;
-static std::vector<GraphRelease> gGraphRel;
+// never destroyed: the runtime may destroy a leftover executable graph, and so run graphReleaseFn, while the
+// process exits, after this library's static destructors
+static std::mutex& graphRelMu() {
+  static std::mutex* m = new std::mutex();
+  return *m;
+}
+static std::vector<GraphRelease>& graphRel() {
+  static std::vector<GraphRelease>* v = new std::vector<GraphRelease>();
+  return *v;
+}
 
 static void graphReleaseFn(void* p) {
   GraphRelease* g = (GraphRelease*)p;
   {
-    std::lock_guard<std::mutex> lk(gGraphRelMu);
-    gGraphRel.push_back(*g);
+    std::lock_guard<std::mutex> lk(graphRelMu());
+    graphRel().push_back(*g);
   }
   delete g;
 }
@@ -348,12 +356,13 @@ static void graphHold(ncclComm* comm, RegAlloc* ra, hipStream_t stream, bool cou
 void regDrainGraphReleases(ncclComm* comm) {
   std::vector<uint64_t> tags;
   {
-    std::lock_guard<std::mutex> lk(gGraphRelMu);
-    for (size_t i = 0; i < gGraphRel.size();)
-      if (gGraphRel[i].comm == comm) {
-        tags.push_back(gGraphRel[i].tag);
-        gGraphRel[i] = gGraphRel.back();
-        gGraphRel.pop_back();
+    std::lock_guard<std::mutex> lk(graphRelMu());
+    std::vector<GraphRelease>& rel = graphRel();
+    for (size_t i = 0; i < rel.size();)
+      if (rel[i].comm == comm) {
+        tags.push_back(rel[i].tag);
+        rel[i] = rel.back();
+        rel.pop_back();
       } else {
         i++;
       }
@@ -428,9 +437,9 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
 void windowsFree(ncclComm* comm, bool notifyPeers) {
   (void)hipSetDevice(comm->device);
   {  // graph releases still queued for this communicator: every registration goes below anyway
-    std::lock_guard<std::mutex> lk(gGraphRelMu);
-    gGraphRel.erase(std::remove_if(gGraphRel.begin(), gGraphRel.end(), [&](const GraphRelease& g) { return g.comm == comm; }),
-                    gGraphRel.end());
+    std::lock_guard<std::mutex> lk(graphRelMu());
+    std::vector<GraphRelease>& rel = graphRel();
+    rel.erase(std::remove_if(rel.begin(), rel.end(), [&](const GraphRelease& g) { return g.comm == comm; }), rel.end());
   }
   for (ncclWindow_vidmem* w : comm->windows) windowRelease(comm, w);
   comm->windows.clear();
