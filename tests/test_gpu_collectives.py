@@ -565,6 +565,33 @@ def test_special_float_values(built, dtype):
     assert not errs, "\n".join(errs[:20])
 
 
+def _single_nan_errors(comms, streams, dtype, count, op, seed, algo=""):
+    """AllReduce of special-value inputs on comms (3 ranks in this process); the elements where exactly one NaN arises
+    in the fold must equal the oracle's bits (algo: the oracle's fold order, as gpu_cases.expected)."""
+    import torch
+    import nccl_amd
+    from tests import gpu_cases as G
+    vt = _int_view(dtype)
+    ins = _with_specials(G.make_inputs(3, dtype, count, seed=seed), dtype)
+    want = G._raw(G.expected("allreduce", ins, dtype, op, 0, algo)[0])
+    bufs = [torch.from_numpy(np.ascontiguousarray(x).view(vt).copy()).cuda() for x in ins]
+    outs = [torch.empty_like(b) for b in bufs]
+    with nccl_amd.group():
+        for r, (c, st) in enumerate(zip(comms, streams)):
+            c.all_reduce_raw(bufs[r].data_ptr(), outs[r].data_ptr(), count, dtype, op, st.cuda_stream)
+    torch.cuda.synchronize()
+    one = _comparable(ins, dtype, op) & (np.isnan(np.stack([G.oracle.to_f32(dtype, x) for x in ins])).sum(0) == 1)
+    assert one.sum() > 0
+    errs = []
+    for r in range(3):
+        got = outs[r].cpu().numpy().view(want.dtype)
+        bad = np.nonzero(got[one] != want[one])[0]
+        if bad.size:
+            errs.append(f"dtype {dtype} op {op} count {count} rank {r}: {bad.size} of {one.sum()} single-NaN elements "
+                        f"differ, e.g. {hex(int(got[one][bad[0]]))} vs {hex(int(want[one][bad[0]]))}")
+    return errs
+
+
 def test_single_nan_payloads(built):
     """Where exactly one rank contributes a NaN (the others finite or infinite), Sum / Prod / Avg return that NaN
     quieted, sign and payload kept, on every path (LL, one-shot, direct) — bit for bit the oracle's result — for every
@@ -581,25 +608,9 @@ def test_single_nan_payloads(built):
     errs = []
     for dtype in (7, 8, 6, 9, 10, 11):
         es = np.dtype(G.oracle.NP_STORAGE[dtype]).itemsize
-        vt = _int_view(dtype)
         for count in (4096 // es * 3 + 3, 600_000 // es, 4_000_000 // es):  # LL, one-shot, direct at n = 3
             for op in (0, 1, 4):
-                ins = _with_specials(G.make_inputs(3, dtype, count, seed=11 + op), dtype)
-                want = G._raw(G.expected("allreduce", ins, dtype, op, 0, "")[0])
-                bufs = [torch.from_numpy(np.ascontiguousarray(x).view(vt).copy()).cuda() for x in ins]
-                outs = [torch.empty_like(b) for b in bufs]
-                with nccl_amd.group():
-                    for r, (c, st) in enumerate(zip(comms, streams)):
-                        c.all_reduce_raw(bufs[r].data_ptr(), outs[r].data_ptr(), count, dtype, op, st.cuda_stream)
-                torch.cuda.synchronize()
-                one = _comparable(ins, dtype, op) & (np.isnan(np.stack([G.oracle.to_f32(dtype, x) for x in ins])).sum(0) == 1)
-                assert one.sum() > 0
-                for r in range(3):
-                    got = outs[r].cpu().numpy().view(want.dtype)
-                    bad = np.nonzero(got[one] != want[one])[0]
-                    if bad.size:
-                        errs.append(f"dtype {dtype} op {op} count {count} rank {r}: {bad.size} of {one.sum()} single-NaN "
-                                    f"elements differ, e.g. {hex(int(got[one][bad[0]]))} vs {hex(int(want[one][bad[0]]))}")
+                errs += _single_nan_errors(comms, streams, dtype, count, op, 11 + op)
     for c in comms:
         c.destroy()
     assert not errs, "\n".join(errs[:20])
@@ -757,6 +768,9 @@ def test_reference_algorithms_with_specials(built, monkeypatch, algo):
             ins = _with_specials(G.make_inputs(3, dtype, count, seed=41 + op), dtype)
             errs += G.run_case(cs, "allreduce", dtype, op, count, 0, seed=0, inputs=ins,
                                algo="" if algo == "REF_ORDER" else algo)
+            if op in (0, 1, 4):  # and the single-NaN elements bit for bit
+                errs += _single_nan_errors(comms, [st for _, st in cs], dtype, count, op, 41 + op,
+                                           "" if algo == "REF_ORDER" else algo)
         if errs:
             break
     for c in comms:
