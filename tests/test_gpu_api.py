@@ -564,6 +564,26 @@ def test_nonblocking_init_from_one_thread(built):
     assert not errs, errs
 
 
+def test_nonblocking_init_reports_a_failed_mapping_check(built, monkeypatch):
+    """A non-blocking init whose mapping check fails (every rank's stores dropped, NCCL_AMD_MAPCHECK_FAULT=1):
+    ncclCommGetAsyncError turns from ncclInProgress to ncclSystemError on both ranks, and the handles still destroy
+    cleanly (reference: a failed non-blocking init is reported through the async error, init.cc:3449)."""
+    import time
+    import torch
+    import nccl_amd
+    torch.cuda.set_device(0)
+    monkeypatch.setenv("NCCL_AMD_MAPCHECK_FAULT", "1")
+    uid = nccl_amd.get_unique_id()
+    cfg = nccl_amd.Config.default(blocking=0)
+    comms = [nccl_amd.Communicator.init(2, r, uid, cfg) for r in range(2)]
+    t0 = time.time()
+    while any(c.async_error() == 7 for c in comms) and time.time() - t0 < 60:
+        time.sleep(0.05)
+    assert [c.async_error() for c in comms] == [2, 2]
+    for c in comms:
+        c.destroy()
+
+
 def test_communicator_churn_releases_resources(built):
     """Create, use and destroy communicators many times (2 ranks in one process, then windows too):
     device memory must return to where it started — staging, flags, counters, LL areas, IPC maps,
