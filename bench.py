@@ -338,45 +338,74 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
     if selected("staged_tuning"):
         trace("staged_tuning")
         # --- staged-path tuning matrix at the headline size (data for the next tuning round: knobs are read
-        #     at communicator init, so each setting gets its own communicator). Every column's result must equal the
-        #     default column's bit for bit (same fold order), which checks the fence-free release over the links ---
+        #     at communicator init, so each setting gets its own communicator, all created up front). The columns are
+        #     timed in interleaved rounds (column order rotated per round) and reported as median / min / max over
+        #     the rounds, so a 5 % effect is not lost in one column's drift between repetitions. Every column's result
+        #     must equal the default column's bit for bit (same fold order), which checks the fence-free release over
+        #     the links and the eager zero-copy kernel ---
         S = (16 if quick else 256) * MIB
         c = S // 4
         xs = torch.empty(c, dtype=torch.float32, device="cuda").uniform_(-1, 1)
         ys = torch.empty_like(xs)
-        tuning = []
         knobs = ("NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_AG_PULL",
-                 "NCCL_AMD_RS_PULL", "NCCL_AMD_P2P_FENCE")
+                 "NCCL_AMD_RS_PULL", "NCCL_AMD_P2P_FENCE", "NCCL_AMD_EAGER_REGISTER")
         saved = {k: os.environ.get(k) for k in knobs}
         # (the staging slab is capped at 1 GiB per rank, so slot sizes scale with channels x slots x n:
         #  default 128 KiB slots at n = 8, 256 KiB with 128 channels)
-        ref = None
-        for env in ({}, {"NCCL_AMD_P2P_FENCE": "0"}, {"NCCL_AMD_P2P_FENCE": "1"}, {"NCCL_MAX_CTAS": "256"},
-                    {"NCCL_AMD_SLOT_BYTES": "32768"}, {"NCCL_AMD_SLOT_BYTES": "65536"},
-                    {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_AMD_NSLOTS": "4"}, {"NCCL_MAX_CTAS": "128"},
-                    {"NCCL_MAX_CTAS": "64"}, {"NCCL_MAX_CTAS": "32"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"}, {"NCCL_AMD_AG_PULL": "1"},
-                    {"NCCL_AMD_RS_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}):
+        envs = [{}, {"NCCL_AMD_P2P_FENCE": "0"}, {"NCCL_AMD_P2P_FENCE": "1"}, {"NCCL_MAX_CTAS": "256"},
+                {"NCCL_AMD_SLOT_BYTES": "32768"}, {"NCCL_AMD_SLOT_BYTES": "65536"},
+                {"NCCL_AMD_NSLOTS": "3"}, {"NCCL_AMD_NSLOTS": "4"}, {"NCCL_MAX_CTAS": "128"},
+                {"NCCL_MAX_CTAS": "64"}, {"NCCL_MAX_CTAS": "32"}, {"NCCL_AMD_MIN_CHANNEL_BYTES": "32768"},
+                {"NCCL_AMD_AG_PULL": "0"}, {"NCCL_AMD_RS_PULL": "1"}, {"NCCL_AMD_AG_PULL": "0", "NCCL_AMD_RS_PULL": "1"},
+                {"NCCL_AMD_EAGER_REGISTER": "1"}]
+        if os.environ.get("BENCH_TUNING_COLS"):  # diagnostics: a subset of the columns, by index
+            envs = [envs[int(i)] for i in os.environ["BENCH_TUNING_COLS"].split(",")]
+        reps = int(os.environ.get("BENCH_TUNING_REPS", "3"))
+        comms = []
+        for env in envs:
             for k in knobs:
                 os.environ.pop(k, None)
             os.environ.update(env)
-            cm = nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank))
-            trace(f"staged_tuning {env or 'default'}")
-            ms = tmax(_tm(lambda: cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, sp), stream, 10))
-            torch.cuda.synchronize()
-            if ref is None:
-                ref = ys.clone()
-                same = True
-            else:
-                same = bool(torch.equal(ys, ref))
-            tuning.append({"env": env or "default", "ms": round(ms, 4),
-                           "busbw_GBps": round(S / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
-                           "check": "pass (= default, bitwise)" if agree(same) else "FAIL"})
-            cm.destroy()
+            comms.append(nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank)))
         for k, v in saved.items():
             os.environ.pop(k, None)
             if v is not None:
                 os.environ[k] = v
-        out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}", "runs": tuning}
+        times = [[] for _ in envs]
+        same = [True] * len(envs)
+        ref = None
+        for rep in range(reps):
+            for j in range(len(envs)):
+                i = (j + rep) % len(envs)
+                cm = comms[i]
+                trace(f"staged_tuning rep {rep} {envs[i] or 'default'}")
+                ms = tmax(_tm(lambda: cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, sp), stream, 10))
+                torch.cuda.synchronize()
+                times[i].append(ms)
+                if i == 0 and ref is None:
+                    ref = ys.clone()
+                elif ref is not None:
+                    same[i] = same[i] and bool(torch.equal(ys, ref))
+        tuning = []
+        for i, env in enumerate(envs):
+            med = statistics.median(times[i])
+            tuning.append({"env": env or "default", "ms": round(med, 4), "ms_min": round(min(times[i]), 4),
+                           "ms_max": round(max(times[i]), 4), "reps": len(times[i]),
+                           "busbw_GBps": round(S / (med * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
+                           "check": "pass (= default, bitwise)" if agree(same[i]) else "FAIL"})
+        torch.cuda.synchronize()
+        for cm in comms:
+            cm.destroy()
+        out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}",
+                                "method": f"{reps} interleaved rounds (column order rotated per round), 10 AllReduces "
+                                          "per column per round, max over ranks; ms = median over rounds",
+                                "runs": tuning}
+        dflt = tuning[0] if not envs[0] else None
+        eager = next((r for r in tuning if r["env"] == {"NCCL_AMD_EAGER_REGISTER": "1"}), None)
+        if eager is not None:  # the unregistered buffers of the headline, registered on first use
+            out["eager_zero_copy"] = {"env": "NCCL_AMD_EAGER_REGISTER=1", "ms": eager["ms"], "ms_min": eager["ms_min"],
+                                      "ms_max": eager["ms_max"], "busbw_GBps": eager["busbw_GBps"],
+                                      "default_ms": dflt["ms"] if dflt else None, "check": eager["check"]}
         del xs, ys, ref
 
     if selected("xgmi_probe"):
@@ -811,8 +840,10 @@ def main(argv=None):
     if not args.no_extra and n > 1 and os.environ.get("BENCH_HOST_STAGED") == "first":
         run_host_staged()
 
-    cpu = None  # the contract's CPU baseline is an N=1 figure (rank 0 only)
-    if n == 1 and rank == 0 and not args.no_cpu_baseline:
+    # the host-core baseline on rank 0 at every N (north_star: "in the same run"), while the other ranks wait at the
+    # barrier below — it never overlaps a timed part of any rank
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
         try:
             cpu = cpu_baseline(count, args.cpu_seconds)
         except Exception as e:  # the baseline is reported, never required

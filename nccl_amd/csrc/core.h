@@ -198,7 +198,10 @@ struct RegAlloc {
   bool imported[NCCL_AMD_MAX_RANKS]; // mapped by rank r's fd server (released by an RPC at deregistration)
   bool usable;         // every peer maps it: collectives on it may run zero-copy
   int localRefs, graphRefs;
+  bool eagerRef;       // held by the eager registration cache (NCCL_AMD_EAGER_REGISTER=1, register.cc)
+  uint64_t lastUse;    // the comm's registration clock at its last collective (eager cache eviction order)
 };
+enum RegRefKind { REF_LOCAL = 0, REF_GRAPH = 1, REF_EAGER = 2 };
 struct RegHandle {  // what ncclCommRegister returns
   void* buff;
   size_t size;
@@ -238,8 +241,16 @@ struct CommTuning {
   int refProto;             // ... of this protocol (NCCL_PROTO_LL 0, LL128 1, SIMPLE 2: the one NCCL_PROTO names)
   int64_t refChunkBytes;    // that protocol's ring chunk (NCCL_BUFFSIZE / NCCL_LL_BUFFSIZE / NCCL_LL128_BUFFSIZE)
   int refChannels;          // NCCL_AMD_REF_NCHANNELS: the reference run's channel count K (0: the channel cap), <= 64
+  int eagerRegister;        // NCCL_AMD_EAGER_REGISTER: unregistered buffers are registered on first use (register.cc)
+  int64_t eagerBytes;       // NCCL_AMD_EAGER_REGISTER_BYTES: ... for collectives of at least this many bytes
+  int eagerMax;             // NCCL_AMD_EAGER_REGISTER_MAX: eager registrations kept past a blocking entry point
+  // size table (NCCL_AMD_SIZE_TABLE, enqueue.cc sizeTable): per rank count, the upper ends of the LL, LL128-class
+  // and one-shot ranges in bytes (0 = the built-in default); loaded once at init and agreed with rank 0's
+  int64_t tableLL[NCCL_AMD_MAX_RANKS + 1], tableLL128[NCCL_AMD_MAX_RANKS + 1], tableOneShot[NCCL_AMD_MAX_RANKS + 1];
 };
 void loadTuning(CommTuning* t);  // enqueue.cc
+// the size table's defaults for n ranks, then NCCL_AMD_SIZE_TABLE's rows over them (enqueue.cc; false: a bad file)
+bool loadSizeTable(CommTuning* t, const char* path);
 void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known
 int linkChannelBudget(int nranks);                  // enqueue.cc: CU budget of large n >= 3 plans
 void resolveLinkChannels(CommTuning* t, int nranks, bool userMaxCTAs);
@@ -306,6 +317,13 @@ struct ncclComm {
   std::vector<ncclamd::IpcMapping> ipcMaps;
   std::vector<ncclamd::RegHandle*> regHandles;     // ncclCommRegister handles
   std::vector<ncclamd::RegAlloc*> regs;            // registered allocations (register.cc)
+  // registrations no collective may use any more (stale, or their last graph reference gone inside a capture): their
+  // peers' RELEASE requests go out at this rank's next blocking entry point, never inside a collective (register.cc)
+  std::vector<ncclamd::RegAlloc*> regRetired;
+  uint64_t regClock = 0;     // registration uses (RegAlloc::lastUse)
+  uint64_t regGen = 0;       // this comm's identity for graph-release tokens (0 until the first graph hold)
+  bool warnedEagerCap = false;
+  std::vector<std::pair<uint64_t, uint64_t>> eagerFailed;  // (base, buffer id) whose eager registration failed
 
   std::vector<ncclamd::UserRedOp> userOps;
   std::atomic<int> asyncResult{ncclSuccess};
@@ -404,7 +422,7 @@ bool llPlan(const CollInfo& info, LLOp* op);                  // LL eligibility 
 enum TuneAlgo { TUNE_DEFAULT = 0, TUNE_LL = 1, TUNE_ONESHOT = 2, TUNE_DIRECT = 3, TUNE_LL128 = 4 };
 ncclResult_t tunerLoad(ncclComm* comm);
 void tunerUnload(ncclComm* comm);
-void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int* algo, int* nch);
+void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int regBuff, int* algo, int* nch);
 // the engine's cost model (tuner.cc): µs of fixed latency + µs of the busiest resource's transfer time
 enum ModelAlgo { MODEL_COPY, MODEL_LL, MODEL_LL128, MODEL_ONESHOT, MODEL_DIRECT, MODEL_SYM, MODEL_RING, MODEL_CHAIN };
 struct ModelCost {
@@ -443,12 +461,16 @@ ncclWindow_vidmem* findSymWindow(ncclComm* comm, const void* p, size_t bytes);
 // nullptr) and [recv, +recvBytes) lie in allocations every peer maps — registered with ncclCommRegister, or,
 // under stream capture with NCCL_GRAPH_REGISTER=1, registered here on the fly. rmtSend[r] / rmtRecv[r] = the
 // buffers as mapped in rank r's process (mine: the buffers themselves).
+// With `eager` (NCCL_AMD_EAGER_REGISTER=1 and an eligible op), unregistered allocations are registered here too.
 bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
-               size_t recvBytes, const char** rmtSend, char** rmtRecv);
+               size_t recvBytes, const char** rmtSend, char** rmtRecv, bool eager = false);
 // release every window and IPC mapping (destroy: also asks peers to unmap this rank's registrations; abort: not)
 void windowsFree(ncclComm* comm, bool notifyPeers);
-// graph-held registration references whose graphs are gone (register.cc): dropped at this comm's blocking calls
-void regDrainGraphReleases(ncclComm* comm);
+// A blocking entry point's registration upkeep (register.cc): graph-held references whose graphs are gone are
+// dropped, stale and surplus eager registrations released, and retired registrations' RELEASE requests sent.
+void regBlockingPoint(ncclComm* comm);
+// [p, +bytes) lies in a usable registration held by an ncclCommRegister handle or the eager cache (no side effects)
+bool regCovers(ncclComm* comm, const void* p, size_t bytes);
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
 ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);
 ncclResult_t launchCopy(void* dst, const void* src, size_t bytes, hipStream_t stream, int variant, int64_t gridCap,

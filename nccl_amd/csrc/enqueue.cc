@@ -5,6 +5,9 @@
 // count==0 no-op, nRanks==1 → ncclLaunchOneRank), :2479-2583 (hostToDevRedOp), src/misc/argcheck.cc:
 // 12-45, 201-254 (pointer / comm / argument checks), src/graph/tuning.cc (algorithm cost model —
 // replaced by the small MI355X table in choosePlan()).
+#include <errno.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -86,8 +89,13 @@ void loadTuning(CommTuning* t) {
   // tested; kept across devices until a multi-GPU run shows the drain suffices over xGMI.
   // Resolved by resolveFence() once the peer table is known.
   t->p2pFence = (int)paramInt("NCCL_AMD_P2P_FENCE", -1);
+  // Gather direction: phase C of the staged AllReduce / AllGather PULLS each owner's reduced
+  // block from the owner's staging (one published copy read by every peer over its link) — the north star's
+  // peer-mapped reads, and on the n = 8 rehearsal 1.585 vs 1.867 ms for the push gather
+  // (profiles/r04d_scale_rehearsal_n8_onegpu.json). NCCL_AMD_AG_PULL=0 restores the push gather (n-1 remote
+  // writes per reduced block). The scatter stays a push unless NCCL_AMD_RS_PULL=1 (no measured gain at n = 8).
   t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (t->p2pFence == 0 ? 8 : 0) |
-                  (paramInt("NCCL_AMD_AG_PULL", 0) ? 16 : 0) | (paramInt("NCCL_AMD_RS_PULL", 0) ? 32 : 0);
+                  (paramInt("NCCL_AMD_AG_PULL", 1) ? 16 : 0) | (paramInt("NCCL_AMD_RS_PULL", 0) ? 32 : 0);
   if (const char* algo = paramStr("NCCL_ALGO")) {
     if (!strcasecmp(algo, "ONESHOT")) t->algo = FORCE_ONESHOT;
     else if (!strcasecmp(algo, "DIRECT")) t->algo = FORCE_DIRECT;
@@ -131,6 +139,15 @@ void loadTuning(CommTuning* t) {
   t->localRegister = (int)paramInt("NCCL_LOCAL_REGISTER", 1);
   t->graphRegister = (int)paramInt("NCCL_GRAPH_REGISTER", 1);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
+  // Eager registration (register.cc regLookup): collectives of at least eagerBytes whose staged plan would be direct
+  // register their unregistered allocations on first use and run the zero-copy kernel. Opt-in: a
+  // peer's mapping keeps a freed allocation's memory until this rank's next blocking call releases it.
+  t->eagerRegister = (int)paramInt("NCCL_AMD_EAGER_REGISTER", 0);
+  t->eagerBytes = paramInt("NCCL_AMD_EAGER_REGISTER_BYTES", 1 << 20);
+  t->eagerMax = (int)paramInt("NCCL_AMD_EAGER_REGISTER_MAX", 64);
+  if (t->eagerMax < 1) t->eagerMax = 1;
+  // the size table's ranges (per rank count; NCCL_AMD_SIZE_TABLE overrides rows, the three knobs below all rows)
+  (void)loadSizeTable(t, paramStr("NCCL_AMD_SIZE_TABLE"));
   t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks; 2 MiB at 2 ranks)
   t->llBytes = paramInt("NCCL_AMD_LL_BYTES", 0);  // 0: size table default (256 KiB / nRanks)
   t->llChannelBytes = paramInt("NCCL_AMD_LL_CHANNEL_BYTES", 4096);
@@ -171,6 +188,83 @@ void loadTuning(CommTuning* t) {
     t->refChunkBytes = paramInt("NCCL_LL128_BUFFSIZE", 120 * 640 * 8 * 8) / 8 / 16 * 15 / 1920 * 1920;
     if (t->refChunkBytes < 1920) t->refChunkBytes = 1920;
   }
+}
+
+// ---- the size table (reference: the per-(algorithm, protocol) latency / bandwidth tables and the cost model that
+// picks the cheapest, src/graph/tuning.cc:148-212, 630-655). One node, one mesh: what the table decides here is
+// where LL ends, where the LL128 class ends and where one-shot gives way to the direct kernel, per rank count.
+// Built-in rows (one-GPU rehearsal crossovers): LL up to max(16 KiB, 256 KiB / n), the LL128 class
+// (when enabled) up to max(64 KiB, 1 MiB / n), one-shot up to 2 MiB / n (2 MiB at n = 2). NCCL_AMD_SIZE_TABLE=<file>
+// replaces rows without a rebuild, so the crossovers an 8-GPU sweep measures can be adopted as data:
+//   # nranks  ll      ll128   oneshot      (bytes; K / M / G suffixes; '-' keeps the built-in value)
+//   8         48K     -       512K
+//   *         -       -       1M           ('*': every rank count; later lines override earlier ones)
+// Rank 0's table is the communicator's (the tuning block is agreed at init), so every rank plans alike.
+static int64_t parseBytes(const char* tok, bool* ok) {
+  *ok = true;
+  if (!strcmp(tok, "-")) return 0;
+  char* end = nullptr;
+  const double v = strtod(tok, &end);
+  if (end == tok || v < 0) {
+    *ok = false;
+    return 0;
+  }
+  double m = 1;
+  if (*end == 'k' || *end == 'K') m = 1024.0, end++;
+  else if (*end == 'm' || *end == 'M') m = 1024.0 * 1024, end++;
+  else if (*end == 'g' || *end == 'G') m = 1024.0 * 1024 * 1024, end++;
+  if (*end == 'b' || *end == 'B') end++;
+  if (*end != '\0') *ok = false;
+  return (int64_t)(v * m);
+}
+
+bool loadSizeTable(CommTuning* t, const char* path) {
+  for (int n = 0; n <= NCCL_AMD_MAX_RANKS; n++) {
+    const int64_t d = n > 0 ? n : 1;
+    t->tableLL[n] = std::max<int64_t>(16 << 10, ((int64_t)256 << 10) / d);
+    t->tableLL128[n] = std::max<int64_t>(64 << 10, ((int64_t)1 << 20) / d);
+    t->tableOneShot[n] = n == 2 ? ((int64_t)2 << 20) : ((int64_t)2 << 20) / d;
+  }
+  if (path == nullptr || path[0] == '\0') return true;
+  FILE* f = fopen(path, "r");
+  if (f == nullptr) {
+    WARN("NCCL_AMD_SIZE_TABLE=%s: cannot open (%s); using the built-in size table", path, strerror(errno));
+    return false;
+  }
+  char line[512];
+  int lineNo = 0, rows = 0;
+  bool good = true;
+  while (fgets(line, sizeof(line), f)) {
+    lineNo++;
+    if (char* hash = strchr(line, '#')) *hash = '\0';
+    char a[64], b[64], c[64], d[64], extra[8];
+    const int k = sscanf(line, "%63s %63s %63s %63s %7s", a, b, c, d, extra);
+    if (k <= 0) continue;  // blank or comment
+    bool okB = false, okC = false, okD = false;
+    int lo = 0, hi = 0;
+    if (k == 4) {
+      const int64_t vb = parseBytes(b, &okB), vc = parseBytes(c, &okC), vd = parseBytes(d, &okD);
+      char* end = nullptr;
+      const long nr = strtol(a, &end, 10);
+      if (!strcmp(a, "*")) lo = 1, hi = NCCL_AMD_MAX_RANKS;
+      else if (end != a && *end == '\0' && nr >= 1 && nr <= NCCL_AMD_MAX_RANKS) lo = hi = (int)nr;
+      if (lo && okB && okC && okD) {
+        for (int n = lo; n <= hi; n++) {
+          if (vb) t->tableLL[n] = vb;
+          if (vc) t->tableLL128[n] = vc;
+          if (vd) t->tableOneShot[n] = vd;
+        }
+        rows++;
+        continue;
+      }
+    }
+    WARN("NCCL_AMD_SIZE_TABLE=%s:%d: expected 'nranks|* ll ll128 oneshot' (bytes, K/M/G, '-' = built-in); line ignored",
+         path, lineNo);
+    good = false;
+  }
+  fclose(f);
+  INFO("NCCL_AMD_SIZE_TABLE=%s: %d rows applied", path, rows);
+  return good;
 }
 
 // CU budget of the large staged and zero-copy plans at n >= 3 (reference: channels and threads shrink below
@@ -352,6 +446,23 @@ static uint32_t refSubCount(ncclComm* comm, const RingParts& r, uint64_t chunk, 
   return g < 1 ? 1 : (uint32_t)g;
 }
 
+// The plugin's regBuff (reference enqueue.cc:2141-2147): both buffers registered (ncclCommRegister, a window, or the
+// eager cache), or a capture with NCCL_GRAPH_REGISTER on. Asked only when a tuner plugin is loaded.
+static int tunerRegBuff(ncclComm* comm, const CollInfo& info) {
+  const int n = comm->nRanks;
+  const size_t ts = (size_t)typeSize(info.datatype);
+  size_t sb = info.count * ts, rb = info.count * ts;
+  if (info.func == FUNC_REDUCESCATTER) sb *= n;
+  if (info.func == FUNC_ALLGATHER) rb *= n;
+  const bool sendOk = regCovers(comm, info.sendbuff, sb) || findSymWindow(comm, info.sendbuff, sb);
+  const bool recvOk = info.recvbuff == nullptr || regCovers(comm, info.recvbuff, rb) || findSymWindow(comm, info.recvbuff, rb);
+  if (sendOk && recvOk) return 1;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(info.stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+  (void)hipGetLastError();
+  return capturing && comm->tune.graphRegister ? 1 : 0;
+}
+
 // LL eligibility and channel plan of one AllReduce, ReduceScatter, AllGather or Reduce (reference tuning: LL for
 // the smallest sizes, or as NCCL_PROTO dictates). Every rank must take the same decision from the same
 // inputs, so it depends only on what all ranks share — count, type, op and the agreed knobs — never on the
@@ -377,8 +488,8 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   // (default 256 KiB / n: 128 KiB at n=2, 32 KiB at n=8; for ReduceScatter / AllGather that is per rank
   // block, i.e. 256 KiB of total data at any n, the same per-rank link bytes). LL64 lines carry 64/56 of
   // it, so the LL128 class takes the next range (default up to 1 MiB / n) before one-shot / direct.
-  const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : std::max<size_t>(16 << 10, ((size_t)256 << 10) / n);
-  const size_t ll64Lim = t.ll128Bytes > 0 ? (size_t)t.ll128Bytes : std::max<size_t>(64 << 10, ((size_t)1 << 20) / n);
+  const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : (size_t)t.tableLL[n];
+  const size_t ll64Lim = t.ll128Bytes > 0 ? (size_t)t.ll128Bytes : (size_t)t.tableLL128[n];
   const bool sized = t.algo == FORCE_NONE;
   int proto = -1;
   if (!t.simpleOn) {  // only LL-class protocols enabled: the range's protocol, else whichever fits
@@ -391,7 +502,8 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   }
   int tuned = TUNE_DEFAULT, tunedNch = 0;
   if (comm->tunerLoaded) {  // an external tuner plugin may overrule the size table (tuner.cc)
-    tunerPick(comm, info.func, blocked ? bytes * n : bytes, 1, (fits ? 1 : 0) | (fits64 ? 2 : 0), &tuned, &tunedNch);
+    tunerPick(comm, info.func, blocked ? bytes * n : bytes, 1, (fits ? 1 : 0) | (fits64 ? 2 : 0), tunerRegBuff(comm, info),
+              &tuned, &tunedNch);
     if (tuned != TUNE_DEFAULT) proto = (fits && tuned == TUNE_LL) ? LLP_LL : (fits64 && tuned == TUNE_LL128) ? LLP_LL64 : -1;
   }
   if (proto < 0) return false;
@@ -514,9 +626,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     // 2 MiB there (one-GPU rehearsal, fp16: 2 MiB one-shot 14.1 us vs direct 16.0, 4 MiB 23.1 vs 17.7;
     // profiles/r02_scale_rehearsal_n2_onegpu.json)
     size_t bytes = count * (size_t)ts;
-    size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes
-                 : n == 2                    ? ((size_t)2 << 20)
-                                             : ((size_t)2 << 20) / n;
+    size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes : (size_t)comm->tune.tableOneShot[n];
     oneShot = comm->tune.algo == FORCE_ONESHOT || (comm->tune.algo == FORCE_NONE && bytes <= lim);
   }
   // NCCL_AMD_REF_ORDER: AllReduce always on the direct kernel in the reference's partition (below)
@@ -530,7 +640,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   if (comm->tunerLoaded) {  // external tuner plugin: one-shot (TREE/SIMPLE) vs direct (RING/SIMPLE), channels
     int tuned = TUNE_DEFAULT;
     tunerPick(comm, info.func, count * (size_t)ts * (info.func == FUNC_ALLGATHER || info.func == FUNC_REDUCESCATTER ? n : 1),
-              1, false, &tuned, &tunedNch);
+              1, false, tunerRegBuff(comm, info), &tuned, &tunedNch);
     if (tuned == TUNE_ONESHOT && info.func == FUNC_ALLREDUCE) oneShot = true;
     if (tuned == TUNE_DIRECT) oneShot = false;
   }
@@ -636,7 +746,10 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
         recvPtr[r] = wr->peerPtr[r] + ((char*)info.recvbuff - (char*)wr->userPtr);
       }
     } else if (regLookup(comm, info.stream, info.func == FUNC_ALLGATHER ? nullptr : info.sendbuff, sb,
-                         info.recvbuff, rb, sendPtr, recvPtr)) {
+                         info.recvbuff, rb, sendPtr, recvPtr,
+                         // eager registration (NCCL_AMD_EAGER_REGISTER=1): ops of at least eagerBytes whose staged
+                         // plan would be the direct kernel, decided from what every rank shares (bytes, the table)
+                         comm->tune.eagerRegister && !oneShotAR && std::max(sb, rb) >= (size_t)comm->tune.eagerBytes)) {
       regMode = 1;  // my buffers as mapped in each peer; the kernel exchanges them at entry
       if (info.func == FUNC_ALLGATHER) sendPtr[comm->rank] = (const char*)info.sendbuff;
     }

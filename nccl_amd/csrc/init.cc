@@ -449,7 +449,7 @@ NCCL_EXPORT ncclResult_t ncclCommFinalize(ncclComm_t comm) {
   HIPCHECK(hipSetDevice(comm->device));
   HIPCHECK(hipDeviceSynchronize());
   ipcDrainReleases();  // a blocking entry point: peers' deregistered buffers are unmapped here (ipc.cc)
-  regDrainGraphReleases(comm);  // and this rank's registrations whose graphs are gone are released (register.cc)
+  regBlockingPoint(comm);  // and this rank's graph-released, stale, surplus eager and retired registrations (register.cc)
   if (comm->bootstrap) NCCLCHECK(bootstrapBarrier(comm->bootstrap));
   comm->finalized = true;
   return ncclSuccess;

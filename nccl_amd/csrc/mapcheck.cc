@@ -195,7 +195,10 @@ static ncclResult_t mapRound(const std::vector<ncclComm*>& comms, uint64_t nonce
     (void)hipSetDevice(comms[i]->device);
     if (hipDeviceSynchronize() != hipSuccess) res = ncclUnhandledCudaError;
   }
-  NCCLCHECK(localBarrier(comms[0]));
+  // a failed barrier (the bootstrap is broken) still frees the probe buffers below, and then skips the closing
+  // all-gather, which could only fail the same way
+  const ncclResult_t bres = localBarrier(comms[0]);
+  if (bres != ncclSuccess && res == ncclSuccess) res = bres;
   for (size_t i = 0; i < comms.size() && res == ncclSuccess; i++) {
     ncclComm* c = comms[i];
     MapCheckObs obs;
@@ -226,6 +229,7 @@ static ncclResult_t mapRound(const std::vector<ncclComm*>& comms, uint64_t nonce
       (void)hipSetDevice(comms[i]->device);
       (void)hipFree(outs[i]);
     }
+  if (bres != ncclSuccess) return bres;
   for (ncclComm* c : comms) fail[c->rank].err = (int32_t)res;
   // every rank learns every rank's row (a rank whose own view is clean still learns that it must remap or fail)
   if (comms[0]->bootstrap) NCCLCHECK(bootstrapAllGather(comms[0]->bootstrap, fail.data(), sizeof(MapFail)));

@@ -234,8 +234,9 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
   return ncclSuccess;
 }
 
-// Find or create the registration of the allocation holding [buff, +size) and take a reference on it.
-static ncclResult_t regAcquire(ncclComm* comm, const void* buff, size_t size, bool graph, RegAlloc** out) {
+// Find or create the registration of the allocation holding [buff, +size) and take a reference of `kind` on it
+// (an eager reference is one flag: the cache holds an allocation at most once).
+static ncclResult_t regAcquire(ncclComm* comm, const void* buff, size_t size, int kind, RegAlloc** out) {
   hipDeviceptr_t base = nullptr;
   size_t allocSize = 0;
   HIPCHECK(hipMemGetAddressRange(&base, &allocSize, (hipDeviceptr_t)buff));
@@ -251,23 +252,39 @@ static ncclResult_t regAcquire(ncclComm* comm, const void* buff, size_t size, bo
     NCCLCHECK(regCreate(comm, (uint64_t)base, allocSize, id, &ra));
     comm->regs.push_back(ra);
   }
-  if (graph) ra->graphRefs++;
-  else ra->localRefs++;
+  if (kind == REF_GRAPH) ra->graphRefs++;
+  else if (kind == REF_LOCAL) ra->localRefs++;
+  else ra->eagerRef = true;
   *out = ra;
   return ncclSuccess;
 }
 
-static void regPut(ncclComm* comm, RegAlloc* ra, bool graph) {
-  if (graph) ra->graphRefs--;
-  else ra->localRefs--;
-  if (ra->localRefs > 0 || ra->graphRefs > 0) return;
+// No collective may use `ra` any more: unlink it now, send its peers RELEASE at the next blocking entry point
+// (regBlockingPoint) — never from inside a collective, where the socket round trips to every peer's fd server do not
+// belong.
+static void regRetire(ncclComm* comm, RegAlloc* ra) {
+  comm->regs.erase(std::find(comm->regs.begin(), comm->regs.end(), ra));
+  comm->regRetired.push_back(ra);
+}
+
+// Drop a reference of `kind`; the last one releases the registration (deferred: retired instead).
+static void regPut(ncclComm* comm, RegAlloc* ra, int kind, bool defer = false) {
+  if (kind == REF_GRAPH) ra->graphRefs--;
+  else if (kind == REF_LOCAL) ra->localRefs--;
+  else ra->eagerRef = false;
+  if (ra->localRefs > 0 || ra->graphRefs > 0 || ra->eagerRef) return;
+  if (defer) {
+    regRetire(comm, ra);
+    return;
+  }
   comm->regs.erase(std::find(comm->regs.begin(), comm->regs.end(), ra));
   regRelease(comm, ra);
 }
 
-// The usable registration holding [p, +bytes), or nullptr. A registration whose allocation was freed and its
-// range handed out again (another buffer id) is never used; an automatic (graph) one is dropped then.
-static RegAlloc* regFind(ncclComm* comm, const void* p, size_t bytes, bool capturing) {
+// The usable registration holding [p, +bytes), or nullptr. `automatic`: registrations held only by graphs or by
+// the eager cache count too (a capture, or an eager collective). A registration whose allocation was freed and its
+// range handed out again (another buffer id) is never used; one no ncclCommRegister handle holds is retired then.
+static RegAlloc* regFind(ncclComm* comm, const void* p, size_t bytes, bool automatic) {
   const uint64_t a = (uint64_t)p;
   uint64_t id = 0;
   bool haveId = false;
@@ -280,15 +297,14 @@ static RegAlloc* regFind(ncclComm* comm, const void* p, size_t bytes, bool captu
     }
     if (id != ra->bufferId) {  // stale: the registered allocation is gone
       if (ra->localRefs == 0) {
-        INFO("rank %d: allocation %lx was freed and re-allocated since a captured collective registered it",
-             comm->rank, (unsigned long)ra->base);
-        ra->graphRefs = 1;
-        regPut(comm, ra, true);
+        INFO("rank %d: allocation %lx was freed and re-allocated since it was registered automatically", comm->rank,
+             (unsigned long)ra->base);
+        regRetire(comm, ra);
         i--;
       }
       continue;
     }
-    if (!ra->usable || (ra->localRefs == 0 && !capturing)) return nullptr;  // automatic ones: captures only
+    if (!ra->usable || (ra->localRefs == 0 && !automatic)) return nullptr;
     return ra;
   }
   return nullptr;
@@ -299,11 +315,13 @@ static RegAlloc* regFind(ncclComm* comm, const void* p, size_t bytes, bool captu
 // instantiated from it are gone (scripts/user_object_probe.hip: on torch's HIP runtime and on /opt/rocm's, the
 // executable keeps it after hipGraphDestroy — PyTorch destroys the hipGraph_t right after instantiating it). The
 // destructor makes no HIP call; it queues (comm, tag), and the next blocking call on that communicator drops the
-// reference (regDrainGraphReleases) — the last one sends the peers RELEASE, as ncclCommDeregister does (the reference
+// reference (regBlockingPoint) — the last one sends the peers RELEASE, as ncclCommDeregister does (the reference
 // ties graph registrations to the graph the same way, src/register/register.cc graph cleanup). Tags are unique in the
-// process, so a token that outlives its communicator matches nothing.
+// process; a token carries its communicator's generation, and a token whose communicator is gone is discarded when
+// its graph dies instead of being queued for ever.
 struct GraphRelease {
-  ncclComm* comm;
+  ncclComm* comm;  // nullptr: inert (the graph never took ownership; the reference stays until comm destroy)
+  uint64_t gen;
   uint64_t tag;
 };
 // never destroyed: the runtime may destroy a leftover executable graph, and so run graphReleaseFn, while the
@@ -316,18 +334,29 @@ static std::vector<GraphRelease>& graphRel() {
   static std::vector<GraphRelease>* v = new std::vector<GraphRelease>();
   return *v;
 }
+static std::vector<uint64_t>& liveGens() {  // generations of the communicators that hold graph references
+  static std::vector<uint64_t>* v = new std::vector<uint64_t>();
+  return *v;
+}
 
 static void graphReleaseFn(void* p) {
   GraphRelease* g = (GraphRelease*)p;
   {
     std::lock_guard<std::mutex> lk(graphRelMu());
-    graphRel().push_back(*g);
+    const std::vector<uint64_t>& live = liveGens();
+    if (g->comm && std::find(live.begin(), live.end(), g->gen) != live.end()) graphRel().push_back(*g);
   }
   delete g;
 }
 
+size_t regGraphReleasesQueued() {  // tests (register.cc's own): tokens waiting for a drain, every communicator
+  std::lock_guard<std::mutex> lk(graphRelMu());
+  return graphRel().size();
+}
+
 // Take a graph reference on `ra` (unless regAcquire just took it: `counted`) for the graph being captured on `stream`.
-// Without a user object (a runtime that refuses one) the reference stays until the communicator is destroyed.
+// Without a user object (a runtime that refuses one, or refuses to let the graph retain it) the reference stays until
+// the communicator is destroyed.
 static void graphHold(ncclComm* comm, RegAlloc* ra, hipStream_t stream, bool counted) {
   if (!counted) ra->graphRefs++;
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
@@ -340,26 +369,41 @@ static void graphHold(ncclComm* comm, RegAlloc* ra, hipStream_t stream, bool cou
     (void)hipGetLastError();
     return;
   }
-  GraphRelease* tok = new GraphRelease{comm, ra->tag};
+  if (comm->regGen == 0) {
+    static std::atomic<uint64_t> nextGen{1};
+    comm->regGen = nextGen++;
+    std::lock_guard<std::mutex> lk(graphRelMu());
+    liveGens().push_back(comm->regGen);
+  }
+  GraphRelease* tok = new GraphRelease{comm, comm->regGen, ra->tag};
   hipUserObject_t obj = nullptr;
   if (hipUserObjectCreate(&obj, tok, graphReleaseFn, 1, hipUserObjectNoDestructorSync) != hipSuccess) {
     (void)hipGetLastError();
     delete tok;
     return;
   }
-  if (hipGraphRetainUserObject(g, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
+  const bool failRetain = paramInt("NCCL_AMD_TEST_RETAIN_FAIL", 0) != 0;  // tests: the runtime refuses the retain
+  if (failRetain || hipGraphRetainUserObject(g, obj, 1, hipGraphUserObjectMove) != hipSuccess) {
     (void)hipGetLastError();
-    (void)hipUserObjectRelease(obj, 1);  // its destructor queues the release of the reference taken above
+    // The graph does not own the object, so releasing it runs the destructor now: make the token inert first, or the
+    // next drain would drop the reference the captured zero-copy kernel still relies on and a later replay would
+    // hand the peers unmapped addresses. The reference then lives until the communicator is destroyed.
+    tok->comm = nullptr;
+    INFO("rank %d: a graph could not retain the release object of allocation %lx; its registration is kept until the "
+         "communicator is destroyed", comm->rank, (unsigned long)ra->base);
+    (void)hipUserObjectRelease(obj, 1);
   }
 }
 
-void regDrainGraphReleases(ncclComm* comm) {
+// Drop the graph references whose graphs are gone. `defer` (inside a captured collective): a registration whose last
+// reference goes is retired, its RELEASE requests sent at the next blocking entry point.
+static void regDrainGraphReleases(ncclComm* comm, bool defer) {
   std::vector<uint64_t> tags;
   {
     std::lock_guard<std::mutex> lk(graphRelMu());
     std::vector<GraphRelease>& rel = graphRel();
     for (size_t i = 0; i < rel.size();)
-      if (rel[i].comm == comm) {
+      if (rel[i].comm == comm && rel[i].gen == comm->regGen) {
         tags.push_back(rel[i].tag);
         rel[i] = rel.back();
         rel.pop_back();
@@ -370,30 +414,71 @@ void regDrainGraphReleases(ncclComm* comm) {
   for (uint64_t tag : tags)
     for (RegAlloc* ra : comm->regs)
       if (ra->tag == tag && ra->graphRefs > 0) {
-        const bool last = ra->graphRefs == 1 && ra->localRefs == 0;
+        const bool last = ra->graphRefs == 1 && ra->localRefs == 0 && !ra->eagerRef;
         if (last)
           INFO("rank %d: automatic registration of allocation %lx released (its graphs are gone)", comm->rank,
                (unsigned long)ra->base);
-        regPut(comm, ra, true);
+        regPut(comm, ra, REF_GRAPH, defer);
         break;
       }
 }
 
+// Eager registration (NCCL_AMD_EAGER_REGISTER=1; reference: IPC registration of a collective's buffers,
+// src/register/coll_reg.cc:326-395, which NCCL does on request or under capture): planColl decides which ops qualify
+// from what every rank shares (bytes, the size table), so every rank takes the same kernel. At blocking entry points:
+void regBlockingPoint(ncclComm* comm) {
+  regDrainGraphReleases(comm, false);
+  // eager cache upkeep: registrations whose allocation is gone go first (nothing of ours can use them: the range was
+  // freed), then the least recently used beyond NCCL_AMD_EAGER_REGISTER_MAX, after this device's work is done (a
+  // queued kernel may still hand the peers their addresses)
+  std::vector<RegAlloc*> eager;
+  const std::vector<RegAlloc*> regs = comm->regs;  // regPut below may unlink entries
+  for (RegAlloc* ra : regs) {
+    if (!ra->eagerRef) continue;
+    if (bufferIdOf((const void*)ra->base) != ra->bufferId) {
+      INFO("rank %d: eager registration of allocation %lx released (the allocation is gone)", comm->rank,
+           (unsigned long)ra->base);
+      regPut(comm, ra, REF_EAGER, true);
+      continue;
+    }
+    eager.push_back(ra);
+  }
+  if ((int)eager.size() > comm->tune.eagerMax) {
+    std::sort(eager.begin(), eager.end(), [](const RegAlloc* a, const RegAlloc* b) { return a->lastUse < b->lastUse; });
+    const size_t drop = eager.size() - (size_t)comm->tune.eagerMax;
+    (void)hipSetDevice(comm->device);
+    (void)hipDeviceSynchronize();
+    for (size_t i = 0; i < drop; i++) regPut(comm, eager[i], REF_EAGER, true);
+    INFO("rank %d: %zu eager registrations released (cache bound %d)", comm->rank, drop, comm->tune.eagerMax);
+  }
+  std::vector<RegAlloc*> retired;
+  retired.swap(comm->regRetired);
+  for (RegAlloc* ra : retired) regRelease(comm, ra);
+}
+
+bool regCovers(ncclComm* comm, const void* p, size_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  for (const RegAlloc* ra : comm->regs)
+    if (ra->usable && (ra->localRefs > 0 || ra->eagerRef) && a >= ra->base && a + bytes <= ra->base + ra->size) return true;
+  return false;
+}
+
 bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
-               size_t recvBytes, const char** rmtSend, char** rmtRecv) {
+               size_t recvBytes, const char** rmtSend, char** rmtRecv, bool eager) {
   if (comm->nRanks == 1) return false;
   bool capturing = false;
-  if (comm->tune.graphRegister) {
+  if (comm->tune.graphRegister || eager) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     capturing = hipStreamIsCapturing(stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
     (void)hipGetLastError();
+    if (capturing && !comm->tune.graphRegister) return false;  // NCCL_GRAPH_REGISTER=0: captures stay staged
   }
   // graph references whose graphs are gone are dropped BEFORE the lookup: dropping one may free a registration the
-  // lookup would otherwise hand back
-  if (capturing) regDrainGraphReleases(comm);
-  if (comm->regs.empty() && !capturing) return false;
-  RegAlloc* rs = send ? regFind(comm, send, sendBytes, capturing) : nullptr;
-  RegAlloc* rr = regFind(comm, recv, recvBytes, capturing);
+  // lookup would otherwise hand back (deferred: no RELEASE round trips inside the collective)
+  if (capturing) regDrainGraphReleases(comm, true);
+  if (comm->regs.empty() && !capturing && !eager) return false;
+  RegAlloc* rs = send ? regFind(comm, send, sendBytes, capturing || eager) : nullptr;
+  RegAlloc* rr = regFind(comm, recv, recvBytes, capturing || eager);
   if (capturing) {
     // NCCL_GRAPH_REGISTER (reference enqueue.cc:283, coll_reg.cc:383-387): a captured collective registers its
     // buffers itself and holds them for the graph's lifetime (graphHold; a registration whose range is freed and
@@ -406,13 +491,13 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     ncclResult_t rsRes = ncclSuccess, rrRes = ncclSuccess;
     if (send && rs) {
       graphHold(comm, rs, stream, false);
-    } else if (send && (rsRes = regAcquire(comm, send, sendBytes, true, &x)) == ncclSuccess) {
+    } else if (send && (rsRes = regAcquire(comm, send, sendBytes, REF_GRAPH, &x)) == ncclSuccess) {
       graphHold(comm, x, stream, true);
       rs = x->usable ? x : nullptr;
     }
     if (rr) {
       graphHold(comm, rr, stream, false);
-    } else if ((rrRes = regAcquire(comm, recv, recvBytes, true, &x)) == ncclSuccess) {
+    } else if ((rrRes = regAcquire(comm, recv, recvBytes, REF_GRAPH, &x)) == ncclSuccess) {
       graphHold(comm, x, stream, true);
       rr = x->usable ? x : nullptr;
     }
@@ -425,8 +510,46 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
            "NCCL_GRAPH_REGISTER=0 on every rank to avoid it)", comm->rank, (int)(rsRes != ncclSuccess ? rsRes : rrRes));
     (void)hipThreadExchangeStreamCaptureMode(&mode);
     (void)hipGetLastError();
+  } else if (eager) {
+    // first use of an unregistered allocation: map it into every peer now (one dma-buf export + one IMPORT request per
+    // peer process, once per allocation); later collectives find it in comm->regs. A failure is remembered per
+    // allocation and said once; this rank then runs the staged kernel, and if its peers registered theirs every rank
+    // stops with the kernel-mismatch error (kernels.h WaitProbe) instead of waiting for the spin timeout.
+    auto acquire = [&](const void* b, size_t bytes) -> RegAlloc* {
+      hipDeviceptr_t base = nullptr;
+      size_t allocSize = 0;
+      if (hipMemGetAddressRange(&base, &allocSize, (hipDeviceptr_t)b) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      const std::pair<uint64_t, uint64_t> key((uint64_t)base, bufferIdOf(b));
+      if (std::find(comm->eagerFailed.begin(), comm->eagerFailed.end(), key) != comm->eagerFailed.end()) return nullptr;
+      RegAlloc* y = nullptr;
+      ncclResult_t res = regAcquire(comm, b, bytes, REF_EAGER, &y);
+      if (res != ncclSuccess) {
+        comm->eagerFailed.push_back(key);
+        WARN("rank %d: eager registration of allocation %lx failed (%d): this rank runs its collectives on it staged; "
+             "if its peers registered theirs, they stop with a kernel-mismatch error (NCCL_AMD_EAGER_REGISTER=0 on "
+             "every rank avoids it)", comm->rank, (unsigned long)key.first, (int)res);
+        return nullptr;
+      }
+      if ((int)comm->regs.size() > comm->tune.eagerMax && !comm->warnedEagerCap) {
+        comm->warnedEagerCap = true;
+        INFO("rank %d: %zu registrations exceed NCCL_AMD_EAGER_REGISTER_MAX=%d; the least recently used are released at "
+             "the next blocking call (ncclCommRegister / Deregister / Finalize / Destroy)", comm->rank,
+             comm->regs.size(), comm->tune.eagerMax);
+      }
+      return y->usable ? y : nullptr;
+    };
+    if (send && !rs) rs = acquire(send, sendBytes);
+    else if (rs && !rs->eagerRef && rs->localRefs == 0) rs->eagerRef = true;  // a graph's registration, now cached
+    if (!rr) rr = acquire(recv, recvBytes);
+    else if (!rr->eagerRef && rr->localRefs == 0) rr->eagerRef = true;
   }
   if (!rr || (send && !rs)) return false;
+  const uint64_t use = ++comm->regClock;
+  rr->lastUse = use;
+  if (rs) rs->lastUse = use;
   for (int r = 0; r < comm->nRanks; r++) {
     rmtSend[r] = send ? (const char*)(rs->rmt[r] + ((uint64_t)send - rs->base)) : nullptr;
     rmtRecv[r] = (char*)(rr->rmt[r] + ((uint64_t)recv - rr->base));
@@ -436,10 +559,13 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
 
 void windowsFree(ncclComm* comm, bool notifyPeers) {
   (void)hipSetDevice(comm->device);
-  {  // graph releases still queued for this communicator: every registration goes below anyway
+  {  // graph releases still queued for this communicator: every registration goes below anyway; tokens of its graphs
+     // that die later are discarded (its generation is no longer live)
     std::lock_guard<std::mutex> lk(graphRelMu());
     std::vector<GraphRelease>& rel = graphRel();
     rel.erase(std::remove_if(rel.begin(), rel.end(), [&](const GraphRelease& g) { return g.comm == comm; }), rel.end());
+    std::vector<uint64_t>& live = liveGens();
+    if (comm->regGen) live.erase(std::remove(live.begin(), live.end(), comm->regGen), live.end());
   }
   for (ncclWindow_vidmem* w : comm->windows) windowRelease(comm, w);
   comm->windows.clear();
@@ -451,6 +577,8 @@ void windowsFree(ncclComm* comm, bool notifyPeers) {
   // left, and its ipcServerStop drops every mapping it held for us anyway), so a peer whose communicator lives on
   // does not keep this rank's registered allocations — graph auto-registrations included — mapped until then
   // (the reference drops them with the registration, src/register/register.cc). Abort sends nothing.
+  for (RegAlloc* ra : comm->regRetired) comm->regs.push_back(ra);
+  comm->regRetired.clear();
   for (RegAlloc* ra : comm->regs) {
     if (notifyPeers) regRelease(comm, ra);
     else delete ra;
@@ -467,7 +595,7 @@ using namespace ncclamd;
 NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, size_t size, void** handle) {
   NCCLCHECK(commCheck(comm, "ncclCommRegister", "comm"));
   ipcDrainReleases();
-  regDrainGraphReleases(comm);
+  regBlockingPoint(comm);
   if (handle == nullptr) {
     WARN("ncclCommRegister : handle argument is NULL");
     return ncclInvalidArgument;
@@ -486,7 +614,7 @@ NCCL_EXPORT ncclResult_t ncclCommRegister(const ncclComm_t comm, void* buff, siz
   if (comm->tune.localRegister && comm->nRanks > 1) {
     DeviceRestore restore;
     HIPCHECK(hipSetDevice(comm->device));
-    ncclResult_t res = regAcquire(comm, buff, size, false, &h->ra);
+    ncclResult_t res = regAcquire(comm, buff, size, REF_LOCAL, &h->ra);
     if (res != ncclSuccess) {
       delete h;
       return res;
@@ -501,7 +629,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommRegister, const ncclComm_t, void*, size_t, void
 NCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle) {
   NCCLCHECK(commCheck(comm, "ncclCommDeregister", "comm"));
   ipcDrainReleases();
-  regDrainGraphReleases(comm);
+  regBlockingPoint(comm);
   if (handle == nullptr) return ncclSuccess;  // reference commDeregister: NULL reg is a no-op
   auto it = std::find(comm->regHandles.begin(), comm->regHandles.end(), (RegHandle*)handle);
   if (it == comm->regHandles.end()) {
@@ -514,8 +642,8 @@ NCCL_EXPORT ncclResult_t ncclCommDeregister(const ncclComm_t comm, void* handle)
     // collectives enqueued on the buffer may still run: wait for them before the peers unmap it
     DeviceRestore restore;
     HIPCHECK(hipSetDevice(comm->device));
-    if (h->ra->localRefs == 1 && h->ra->graphRefs == 0) HIPCHECK(hipDeviceSynchronize());
-    regPut(comm, h->ra, false);
+    if (h->ra->localRefs == 1 && h->ra->graphRefs == 0 && !h->ra->eagerRef) HIPCHECK(hipDeviceSynchronize());
+    regPut(comm, h->ra, REF_LOCAL);
   }
   delete h;
   return ncclSuccess;
@@ -526,7 +654,7 @@ NCCL_EXPORT ncclResult_t ncclCommWindowRegister(ncclComm_t comm, void* buff, siz
                                                 int winFlags) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowRegister", "comm"));
   ipcDrainReleases();
-  regDrainGraphReleases(comm);
+  regBlockingPoint(comm);
   if (win == nullptr) {
     WARN("ncclCommWindowRegister : win argument is NULL");
     return ncclInvalidArgument;
@@ -547,7 +675,7 @@ NCCL_ALIAS(ncclResult_t, ncclCommWindowRegister, ncclComm_t, void*, size_t, nccl
 NCCL_EXPORT ncclResult_t ncclCommWindowDeregister(ncclComm_t comm, ncclWindow_t win) {
   NCCLCHECK(commCheck(comm, "ncclCommWindowDeregister", "comm"));
   ipcDrainReleases();
-  regDrainGraphReleases(comm);
+  regBlockingPoint(comm);
   if (win == nullptr) return ncclSuccess;
   auto it = std::find(comm->windows.begin(), comm->windows.end(), win);
   if (it == comm->windows.end() || win->comm != comm) {

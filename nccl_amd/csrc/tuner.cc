@@ -186,7 +186,8 @@ ModelCost modelCost(ModelAlgo a, CollFunc func, int n, size_t bytes) {
 
 // Ask the plugin. `algo` (in: the engine's default choice, out: the plugin's) and `nch` (out: channel
 // override or 0). llMask: 1 = the LL kernel can take this collective, 2 = the LL64 (LL128-class) one can.
-void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int* algo, int* nch) {
+// regBuff: the reference's (enqueue.cc:2141-2147), computed by the caller.
+void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int llMask, int regBuff, int* algo, int* nch) {
   const bool llOk = (llMask & 1) != 0, ll128Ok = (llMask & 2) != 0;
   *nch = 0;
   if (!comm->tunerLoaded) return;
@@ -214,9 +215,9 @@ void tunerPick(ncclComm* comm, CollFunc func, size_t bytes, int numPipeOps, int 
   memcpy(before, table, sizeof(table));
   int ch = 0;
   ncclResult_t r;
-  if (gVersion == 6) r = gV6->getCollInfo(comm->tunerCtx, f, bytes, numPipeOps, (float**)table, NCCL_NUM_ALGORITHMS, NCCL_NUM_PROTOCOLS, 0, &ch);
-  else if (gVersion == 5) r = gV5->getCollInfo(comm->tunerCtx, f, bytes, numPipeOps, (float**)table, NCCL_NUM_ALGORITHMS, NCCL_NUM_PROTOCOLS, 0, &ch);
-  else r = gV4->getCollInfo(comm->tunerCtx, f, bytes, numPipeOps, (float**)table, NCCL_NUM_ALGORITHMS, NCCL_NUM_PROTOCOLS, 0, &ch);
+  if (gVersion == 6) r = gV6->getCollInfo(comm->tunerCtx, f, bytes, numPipeOps, (float**)table, NCCL_NUM_ALGORITHMS, NCCL_NUM_PROTOCOLS, regBuff, &ch);
+  else if (gVersion == 5) r = gV5->getCollInfo(comm->tunerCtx, f, bytes, numPipeOps, (float**)table, NCCL_NUM_ALGORITHMS, NCCL_NUM_PROTOCOLS, regBuff, &ch);
+  else r = gV4->getCollInfo(comm->tunerCtx, f, bytes, numPipeOps, (float**)table, NCCL_NUM_ALGORITHMS, NCCL_NUM_PROTOCOLS, regBuff, &ch);
   if (r != ncclSuccess) return;  // reference: fall back to the default tuning
   if (ch > 0) *nch = ch;
   if (!memcmp(before, table, sizeof(table))) return;  // table untouched: keep the engine's size table

@@ -37,7 +37,7 @@ def settings(rng):
     if rng.random() < 0.3:
         env["NCCL_MAX_CTAS"] = str(rng.choice([1, 3, 7, 32, 64]))
     if rng.random() < 0.3:
-        env["NCCL_AMD_AG_PULL"] = "1"
+        env["NCCL_AMD_AG_PULL"] = "0"  # the push gather (pull is the default)
     if rng.random() < 0.3:
         env["NCCL_AMD_RS_PULL"] = "1"
     if rng.random() < 0.2:

@@ -1,9 +1,11 @@
-"""One rank of a 2-process AllReduce on the one-GPU box, rendezvous through a file (no launcher, so one
-of the two processes can run under rocprofv3 without any process being spawned from a profiled one).
+"""One rank of an n-process AllReduce on the one-GPU box (n = $NRANKS, default 2), rendezvous through a file (no
+launcher, so one of the processes can run under rocprofv3 without any process being spawned from a profiled one).
 usage: mp_rank.py RANK UIDFILE [ITERS] [staged|sym|reg|rs|ag|ring|reforder] — rank 1 creates the ncclUniqueId and
 writes it to UIDFILE; `sym` puts both buffers in a symmetric window, `reg` registers them with ncclCommRegister
-(zero-copy kernels either way); `rs` / `ag` run ReduceScatter (S in, S/2 out) / AllGather (S/2 in, S out) on the
-staged path; `ring` / `reforder` the AllReduce with NCCL_ALGO=RING / NCCL_AMD_REF_ORDER=1 at K = 32 reference parts."""
+(zero-copy kernels either way), `eager` leaves them unregistered with NCCL_AMD_EAGER_REGISTER=1; `push` is the staged
+AllReduce with the push gather (NCCL_AMD_AG_PULL=0); `rs` / `ag` run ReduceScatter (S in, S/n out) / AllGather (S/n in,
+S out) on the staged path; `ring` / `reforder` the AllReduce with NCCL_ALGO=RING / NCCL_AMD_REF_ORDER=1 at K = 32
+reference parts."""
 import os
 import sys
 import time
@@ -34,8 +36,13 @@ def main():
         os.environ.update(NCCL_ALGO="RING", NCCL_AMD_REF_NCHANNELS="32")
     if mode == "reforder":
         os.environ.update(NCCL_AMD_REF_ORDER="1", NCCL_AMD_REF_NCHANNELS="32")
+    if mode == "eager":
+        os.environ.update(NCCL_AMD_EAGER_REGISTER="1")
+    if mode == "push":
+        os.environ.update(NCCL_AMD_AG_PULL="0")
+    n = int(os.environ.get("NRANKS", "2"))
     torch.cuda.set_device(0)
-    comm = nccl_amd.Communicator.init(2, rank, uid)
+    comm = nccl_amd.Communicator.init(n, rank, uid)
     S = 256 << 20
     if mode == "sym":
         win_t = torch.empty(2 * S, dtype=torch.uint8, device="cuda")
@@ -51,20 +58,22 @@ def main():
     s = torch.cuda.current_stream()
     if mode == "ag":
         y = torch.empty(S // 4, dtype=torch.float32, device="cuda")
+    blk = S // 4 // n  # elements of one rank block
     for _ in range(2 + iters):
         if mode == "rs":
-            comm.reduce_scatter_raw(x.data_ptr(), y.data_ptr(), S // 8, 7, 0, s.cuda_stream)
+            comm.reduce_scatter_raw(x.data_ptr(), y.data_ptr(), blk, 7, 0, s.cuda_stream)
         elif mode == "ag":
-            comm.all_gather_raw(x.data_ptr(), y.data_ptr(), S // 8, 7, s.cuda_stream)
+            comm.all_gather_raw(x.data_ptr(), y.data_ptr(), blk, 7, s.cuda_stream)
         else:
             comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), S // 4, 7, 0, s.cuda_stream)
     torch.cuda.synchronize()
+    total = float(n * (n + 1) // 2)
     if mode == "rs":
-        ok = bool((y[:S // 8] == 3.0).all())
+        ok = bool((y[:blk] == total).all())
     elif mode == "ag":
-        ok = bool((y[:S // 8] == 1.0).all()) and bool((y[S // 8:] == 2.0).all())
+        ok = all(bool((y[r * blk:(r + 1) * blk] == float(r + 1)).all()) for r in range(n))
     else:
-        ok = bool((y == 3.0).all())
+        ok = bool((y == total).all())
     print(f"rank {rank}: ok={ok} async={comm.async_error()}", flush=True)
     if mode == "sym":
         comm.deregister_window(win)

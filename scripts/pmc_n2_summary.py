@@ -1,6 +1,7 @@
 """Per-launch HBM bytes of the main library kernel in scripts/pmc_n2.sh outputs (gpurun_out/pmc2/<mode>_<counter>/):
 median over dispatches of the summed FETCH_SIZE (x2, 16-byte streaming reads, MI355X_MICROARCH.md HBM section) plus
-WRITE_SIZE, in KiB x 1024, and the ratio to S = 256 MiB. usage: pmc_n2_summary.py MODE [MODE ...]"""
+WRITE_SIZE, in KiB x 1024, and the ratio to S = 256 MiB. usage: pmc_n2_summary.py TAG [TAG ...] (TAG = the mode, or
+<mode>_n<N> for NRANKS=N runs)"""
 import csv
 import json
 import statistics as st

@@ -26,6 +26,10 @@ const char* hipGetErrorString(hipError_t) { return "stub"; }
 hipError_t hipPointerGetAttributes(hipPointerAttribute_t*, const void*) { return hipErrorInvalidValue; }
 hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned int) { return hipSuccess; }
+hipError_t hipStreamIsCapturing(hipStream_t, hipStreamCaptureStatus* st) {
+  *st = hipStreamCaptureStatusNone;
+  return hipSuccess;
+}
 }
 
 namespace ncclamd {
@@ -58,11 +62,15 @@ ncclResult_t launchSymPlan(const SymPlan& p) {
   return ncclSuccess;
 }
 ncclWindow_vidmem* findSymWindow(ncclComm*, const void*, size_t) { return nullptr; }
-bool regLookup(ncclComm*, hipStream_t, const void*, size_t, const void*, size_t, const char**, char**) { return false; }
+// eager registration (NCCL_AMD_EAGER_REGISTER=1) of an eligible op succeeds: the plan shows the zero-copy kernel
+bool regLookup(ncclComm*, hipStream_t, const void*, size_t, const void*, size_t, const char**, char**, bool eager) {
+  return eager;
+}
 bool groupActive() { return false; }
 ncclResult_t groupDeferColl(const CollInfo&) { return ncclSuccess; }
 void groupRecordError(ncclResult_t) {}
-void tunerPick(ncclComm*, CollFunc, size_t, int, int, int*, int* nch) { *nch = 0; }
+void tunerPick(ncclComm*, CollFunc, size_t, int, int, int, int*, int* nch) { *nch = 0; }
+bool regCovers(ncclComm*, const void*, size_t) { return false; }
 ncclResult_t commCheck(const ncclComm*, const char*, const char*) { return ncclSuccess; }
 void ipcDrainReleases() {}
 }  // namespace ncclamd

@@ -26,7 +26,7 @@ def test_bench_two_ranks_quick(built):
     env = dict(os.environ, NCCL_AMD_SPIN_TIMEOUT_MS="20000")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "3", "--warmup", "1", "--quick-suite", "--no-cpu-baseline"]
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--quick-suite", "--cpu-seconds", "1"]
     out = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=280, cwd=ROOT)
     assert out.returncode == 0, out.stdout[-3000:] + out.stderr[-3000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
@@ -43,12 +43,19 @@ def test_bench_two_ranks_quick(built):
     assert 0.5 < roof["achieved"] / d["busbw_GBps"] < 2.0   # per-launch event time vs the whole step's wall time
     assert "hbm" in roof and roof["hbm"]["peak"] == 8000.0
     assert roof["kernel"] and "ncclamd::collKernel<float, 0, 0>" in roof["kernel"], roof["kernel"]
+    # every N line carries the host-core baseline (rank 0, same run) and the PMC traffic
+    assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1, d["cpu_baseline"]
+    assert roof["traffic"] and roof["traffic"] > 0, roof
     s = d["suite"]
     assert "error" not in s, s
     assert s["rs_ag_bf16"]["check"] == "pass" and s["reduce_int32"]["check"].startswith("pass")
     assert s["symmetric_window"]["check"].startswith("pass")
     assert s["registered"]["check"].startswith("pass")
     assert all(r["check"].startswith("pass") for r in s["staged_tuning"]["runs"]), s["staged_tuning"]
+    # every column timed in >= 3 interleaved rounds, median with its spread
+    assert all(r["reps"] >= 3 and r["ms_min"] <= r["ms"] <= r["ms_max"] for r in s["staged_tuning"]["runs"])
+    # the unregistered headline buffers registered on first use, bitwise = the staged result
+    assert s["eager_zero_copy"]["check"].startswith("pass") and s["eager_zero_copy"]["ms"] > 0, s["eager_zero_copy"]
     assert s["group_aggregation"]["aggregated_us_per_group"] > 0
     # the link probe and the fence on / off column at the top level of the N > 1 line
     assert "xgmi_links" in d and d["p2p_fence"]["check"] == "pass", (d.get("xgmi_links"), d.get("p2p_fence"))

@@ -119,6 +119,9 @@ MP_CASES = [(2, {}), (4, {}), (8, {}),
             (2, {"NCCL_ALGO": "DIRECT"}),
             (3, {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
             (4, {"NCCL_AMD_AG_PULL": "1"}),
+            # the push gather (the default before round 5; NCCL_AMD_AG_PULL=0 keeps it)
+            (4, {"NCCL_AMD_AG_PULL": "0"}),
+            (3, {"NCCL_AMD_AG_PULL": "0", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}),
             (3, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "1"}),
             (4, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"}),
             (4, {"NCCL_ALGO": "RING"}), (3, {"NCCL_ALGO": "TREE", "NCCL_AMD_SLOT_BYTES": "4096"}),
@@ -635,6 +638,7 @@ def test_every_path_same_bits_with_specials(built, monkeypatch, dtype):
              "DIRECT": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
              "DIRECT_PULLS": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple", "NCCL_AMD_AG_PULL": "1",
                               "NCCL_AMD_RS_PULL": "1"},
+             "DIRECT_PUSH": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple", "NCCL_AMD_AG_PULL": "0"},
              "REGISTERED": {"NCCL_PROTO": "Simple"}}
     results = {}
     for name, env in paths.items():
@@ -696,6 +700,7 @@ def test_reduce_paths_same_bits_with_specials(built, monkeypatch, coll, dtype):
     if coll == "reducescatter":
         paths.update({"LL128": {"NCCL_PROTO": "LL128"},
                       "DIRECT_PULLS": {"NCCL_PROTO": "Simple", "NCCL_AMD_AG_PULL": "1", "NCCL_AMD_RS_PULL": "1"},
+                      "DIRECT_PUSH": {"NCCL_PROTO": "Simple", "NCCL_AMD_AG_PULL": "0"},
                       "REGISTERED": {"NCCL_PROTO": "Simple"}})
     results = {}
     for name, env in paths.items():
@@ -865,8 +870,9 @@ def test_execution_modes_same_bits(built, monkeypatch, dtype):
 
 
 @pytest.mark.parametrize("env", [{"NCCL_AMD_AG_PULL": "1"}, {"NCCL_AMD_RS_PULL": "1", "NCCL_AMD_AG_PULL": "1"},
-                                 {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
-                         ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots"])
+                                 {"NCCL_AMD_AG_PULL": "1", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"},
+                                 {"NCCL_AMD_AG_PULL": "0", "NCCL_AMD_SLOT_BYTES": "4096", "NCCL_AMD_NSLOTS": "2"}],
+                         ids=["ag_pull", "both_pulls", "ag_pull_tiny_slots", "push_tiny_slots"])
 def test_pull_modes_interleaved_with_reduce(built, env):
     """Pull-mode gathers after Reduces on the same communicator: a Reduce pushes to its root only, so the
     per-pair AG sequences diverge; the pull gather must run on its own sequence (found by scripts/fuzz.py:

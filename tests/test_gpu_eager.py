@@ -1,0 +1,238 @@
+"""GPU tests of eager zero-copy (NCCL_AMD_EAGER_REGISTER=1): unregistered buffers of large
+collectives are registered on first use — the allocation holding them is mapped into every peer process once
+(reference: IPC registration of a collective's buffers, src/register/coll_reg.cc:326-395; the read-mode P2P transport,
+src/transport/p2p.cc:326-343) — and the collective runs the zero-copy kernel that reads the peers' HBM. Results must be
+bit-identical to the oracle, also across free → re-allocate at the same address; the memory a peer's mapping keeps
+alive after the owner frees it is measured and must come back at the next blocking calls. Also the
+graph-registration retain failure path. Every rank is a process on the box's one GPU (dma-buf IPC)."""
+import os
+import re
+import time
+
+import numpy as np
+import pytest
+
+from tests.test_gpu_register import _spawn, _trace_env, _zero_copy_lines
+
+os.environ.setdefault("NCCL_AMD_SPIN_TIMEOUT_MS", "30000")
+pytestmark = pytest.mark.gpu
+MIB = 1 << 20
+
+
+def _eager_worker(rank, nranks, uid, q):
+    try:
+        os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
+        logf = _trace_env(f"eager{nranks}")
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.Stream()
+        sp = s.cuda_stream
+        count = 3 << 20  # 12 MiB fp32: above every one-shot range
+        errs = []
+
+        def check(name, out, want):
+            got = out.cpu().numpy()
+            if comm.async_error():
+                errs.append(f"rank {rank} {name}: async error {comm.async_error()}")
+            elif not G.same_bits(got, want, 7):
+                bad = np.nonzero(got != want)[0]
+                errs.append(f"rank {rank} {name}: {bad.size} elements differ, first {bad[:4].tolist()}")
+
+        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+        x = torch.empty(count, dtype=torch.float32, device="cuda")
+        y = torch.empty(count, dtype=torch.float32, device="cuda")
+        rs = torch.empty(count // nranks, dtype=torch.float32, device="cuda")
+        z = torch.empty(count * nranks, dtype=torch.float32, device="cuda")
+        for it in range(3):  # the first round registers, the next two find the registrations
+            ins = G.make_inputs(nranks, 7, count, seed=900 + it)
+            x.copy_(torch.from_numpy(ins[rank]))
+            torch.cuda.synchronize()
+            comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, sp)
+            comm.reduce_scatter_raw(x.data_ptr(), rs.data_ptr(), count // nranks, 7, 0, sp)
+            comm.all_gather_raw(x.data_ptr(), z.data_ptr(), count, 7, sp)
+            comm.all_reduce_raw(x.data_ptr(), x.data_ptr(), count, 7, 1, sp)  # in place, prod
+            s.synchronize()
+            check(f"round {it} allreduce", y, oracle.all_reduce(ins, 7, 0))
+            check(f"round {it} reducescatter", rs, oracle.reduce_scatter(ins, 7, 0)[rank])
+            check(f"round {it} allgather", z, oracle.all_gather(ins))
+            check(f"round {it} in-place prod", x, oracle.all_reduce(ins, 7, 1))
+        text = open(logf).read()[pos:]
+        zc = len(_zero_copy_lines(logf, pos))
+        regs = text.count("registered allocation")
+        # free x and allocate the same size again: the caching allocator's segment goes back to the runtime and the
+        # new one (usually at the same address) has another buffer id, so the stale registration is never used
+        old_ptr = x.data_ptr()
+        del x
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        x = torch.empty(count, dtype=torch.float32, device="cuda")
+        same_addr = x.data_ptr() == old_ptr
+        pos = os.path.getsize(logf)
+        ins = G.make_inputs(nranks, 7, count, seed=990)
+        x.copy_(torch.from_numpy(ins[rank]))
+        torch.cuda.synchronize()
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, sp)
+        s.synchronize()
+        check("after re-allocation", y, oracle.all_reduce(ins, 7, 0))
+        text2 = open(logf).read()[pos:]
+        restaged = "freed and re-allocated" in text2 and text2.count("registered allocation") == 1
+        # small ops stay on their kernels: the one-shot / LL ranges are not registered
+        pos = os.path.getsize(logf)
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), 1024, 7, 0, sp)
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), (256 << 10) // 4, 7, 0, sp)
+        s.synchronize()
+        small_zc = len(_zero_copy_lines(logf, pos))
+        comm.destroy()
+        q.put((rank, (errs, zc, regs, same_addr, restaged, small_zc)))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0, False, False, 0)))
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_eager_zero_copy_multi_process(built, nranks):
+    """Every AllReduce / ReduceScatter / AllGather of 12 MiB on plain torch allocations runs zero-copy, bit-exact vs
+    the oracle; the allocations are registered once (four: x, y, the ReduceScatter and AllGather outputs), and a
+    freed and re-allocated buffer is registered again and stays bit-exact."""
+    res = _spawn(_eager_worker, nranks)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:20])
+    for r, (_, zc, regs, same_addr, restaged, small_zc) in res.items():
+        assert zc == 12, f"rank {r}: {zc} zero-copy plans for 12 eligible collectives"
+        assert regs == 4, f"rank {r}: {regs} registrations (want 4: one per allocation, once)"
+        if same_addr:
+            assert restaged, f"rank {r}: the re-allocated buffer at the same address was not registered anew"
+        assert small_zc == 0, f"rank {r}: a one-shot / LL-range op ran zero-copy"
+
+
+def _pinning_worker(rank, nranks, uid, q):
+    """What a peer's mapping costs: rank r's 1 GiB pair is freed by its owner while the peers still map it, so the
+    device's free memory stays down until the owner's next blocking call (RELEASE to the peers) and the peers' next
+    blocking call (unmap). All ranks share the one GPU, so hipMemGetInfo sees every rank's memory."""
+    try:
+        os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.Stream()
+        sp = s.cuda_stream
+        tiny = torch.zeros(256, dtype=torch.float32, device="cuda")
+
+        def sync():  # a small (LL) AllReduce as a barrier across the processes
+            comm.all_reduce_raw(tiny.data_ptr(), tiny.data_ptr(), 256, 7, 0, sp)
+            s.synchronize()
+
+        def blocking_call():
+            h = comm.register_buffer(tiny.data_ptr(), tiny.numel() * 4)
+            comm.deregister_buffer(h)
+
+        count = (512 * MIB) // 4
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        sync()
+        free0 = torch.cuda.mem_get_info()[0]
+        sync()
+        x = torch.ones(count, dtype=torch.float32, device="cuda")
+        y = torch.empty_like(x)
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, sp)
+        s.synchronize()
+        ok = bool((y == float(nranks)).all())
+        del x, y
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        sync()
+        time.sleep(0.2)
+        free1 = torch.cuda.mem_get_info()[0]
+        sync()
+        blocking_call()  # this rank's eager registrations of freed allocations: RELEASE to the peers
+        sync()
+        blocking_call()  # what the peers released: unmapped here
+        sync()
+        time.sleep(0.2)
+        free2 = torch.cuda.mem_get_info()[0]
+        sync()
+        comm.destroy()
+        q.put((rank, (ok, free0, free1, free2)))
+    except Exception as e:
+        q.put((rank, (False, repr(e), 0, 0)))
+
+
+def test_eager_registration_memory_pinning(built):
+    """DESIGN.md §10.3's measured cost: with 2 ranks each freeing a 512 MiB send / receive pair (1 GiB per rank) that
+    the other maps, how much device memory stays held after the free, and that it all comes back after one blocking
+    call on each side."""
+    res = _spawn(_pinning_worker, 2)
+    for r, (ok, free0, free1, free2) in res.items():
+        assert ok is True, f"rank {r}: {free0}"
+    free0, free1, free2 = res[0][1], res[0][2], res[0][3]
+    held = (free0 - free1) / (1 << 30)
+    back = (free2 - free1) / (1 << 30)
+    print(f"eager pinning: {held:.3f} GiB held after both ranks freed 1 GiB each; {back:.3f} GiB back after the "
+          f"blocking calls (free {free0 / (1 << 30):.2f} -> {free1 / (1 << 30):.2f} -> {free2 / (1 << 30):.2f} GiB)")
+    assert free2 >= free0 - 256 * MIB, (free0, free1, free2)
+
+
+def _retain_fail_worker(rank, nranks, uid, q):
+    """when the runtime refuses to let the capturing graph retain the release object, releasing the object
+    runs its destructor at once. The token must be inert: the next blocking call must not drop the reference the
+    captured zero-copy kernel relies on (the peers would unmap the buffers and a later replay would fault)."""
+    try:
+        os.environ["NCCL_AMD_TEST_RETAIN_FAIL"] = "1"
+        logf = _trace_env(f"retainfail{nranks}")
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = nccl_amd.dedicated_stream(0)
+        count = 3 << 20
+        x = torch.empty(count, dtype=torch.float32, device="cuda")
+        y = torch.empty(count, dtype=torch.float32, device="cuda")
+        dummy = torch.empty(4096, dtype=torch.uint8, device="cuda")
+        g = torch.cuda.CUDAGraph()
+        torch.cuda.synchronize()
+        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+        with torch.cuda.graph(g, stream=s):
+            comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+        errs = []
+        for it in range(2):
+            h = comm.register_buffer(dummy.data_ptr(), dummy.numel())  # blocking calls: drains on both ranks
+            comm.deregister_buffer(h)
+            torch.cuda.synchronize()
+            comm.all_reduce_raw(dummy.data_ptr(), dummy.data_ptr(), 16, 7, 0, s.cuda_stream)  # every rank past it
+            torch.cuda.synchronize()
+            h = comm.register_buffer(dummy.data_ptr(), dummy.numel())  # ... and the peers' releases, if any
+            comm.deregister_buffer(h)
+            ins = G.make_inputs(nranks, 7, count, seed=720 + it)
+            x.copy_(torch.from_numpy(ins[rank]))
+            torch.cuda.synchronize()
+            with torch.cuda.stream(s):
+                g.replay()
+            torch.cuda.synchronize()
+            if comm.async_error() or not G.same_bits(y.cpu().numpy(), oracle.all_reduce(ins, 7, 0), 7):
+                errs.append(f"rank {rank} replay {it}: differs (async {comm.async_error()})")
+                break
+        text = open(logf).read()[pos:]
+        inert = text.count("could not retain the release object")
+        released = text.count("automatic registration of allocation")
+        zc = len(re.findall(r"AllReduce: registered zero-copy", text))
+        del g
+        comm.destroy()
+        q.put((rank, (errs, inert, released, zc)))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0, 0)))
+
+
+def test_graph_retain_failure_keeps_the_registration(built):
+    res = _spawn(_retain_fail_worker, 2)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad[:20])
+    for r, (_, inert, released, zc) in res.items():
+        assert inert == 2, f"rank {r}: {inert} inert tokens (want 2: x and y)"
+        assert released == 0, f"rank {r}: a registration the graph still uses was released"
+        assert zc >= 1, f"rank {r}: the capture did not run zero-copy"

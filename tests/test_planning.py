@@ -364,3 +364,73 @@ def test_reference_partition_is_clamped_and_decoupled(exe, built):
             assert p["sub"] == 1 or -(-ck // p["sub"]) * 4 >= (16 << 10) - 16, (count, n, p)
             if n >= 3:  # the CU budget of the default plan at n >= 3 (linkChannelBudget: 32 at n = 3, 128 at n = 8)
                 assert p["nch"] <= max({3: 32, 8: 128}[n], p["refnch"])
+
+
+def test_size_table_file(exe, tmp_path):
+    """the LL / LL128-class / one-shot crossovers come from a per-n table that
+    NCCL_AMD_SIZE_TABLE=<file> overrides (reference: the tuning tables behind the cost model, src/graph/tuning.cc:
+    148-212, 630-655), so a measured 8-GPU sweep is adopted without a rebuild. The built-in rows are pinned by
+    test_allreduce_size_table; here the file's syntax, precedence and error handling."""
+    t = tmp_path / "table.txt"
+    t.write_text("# nranks ll ll128 oneshot\n"
+                 "*   -    -     1M      # every n: one-shot to 1 MiB\n"
+                 "8   48K  -     512K    # n = 8 row overrides the '*' row\n"
+                 "2   64k  2M    -\n")
+    tab = dict(NCCL_AMD_SIZE_TABLE=str(t))
+    # n = 8: LL to 48 KiB (built-in 32 KiB), one-shot to 512 KiB (built-in 256 KiB)
+    assert plan(exe, 8, "ar", 7, (48 << 10) // 4, **tab)["algo"] == "ll"
+    assert plan(exe, 8, "ar", 7, (48 << 10) // 4 + 4, **tab)["algo"] == "oneshot"
+    assert plan(exe, 8, "ar", 7, (512 << 10) // 4, **tab)["algo"] == "oneshot"
+    assert plan(exe, 8, "ar", 7, (512 << 10) // 4 + 4, **tab)["algo"] == "direct"
+    assert plan(exe, 8, "ar", 7, (512 << 10) // 4)["algo"] == "direct"          # built-in: 256 KiB
+    # n = 4 takes the '*' row: one-shot to 1 MiB (built-in 512 KiB), LL unchanged (64 KiB)
+    assert plan(exe, 4, "ar", 7, (1 << 20) // 4, **tab)["algo"] == "oneshot"
+    assert plan(exe, 4, "ar", 7, (64 << 10) // 4, **tab)["algo"] == "ll"
+    assert plan(exe, 4, "ar", 7, (64 << 10) // 4 + 4, **tab)["algo"] == "oneshot"
+    # n = 2: LL to 64 KiB (built-in 128 KiB); its '-' one-shot keeps the '*' row's 1 MiB
+    assert plan(exe, 2, "ar", 7, (64 << 10) // 4 + 4, **tab)["algo"] == "oneshot"
+    assert plan(exe, 2, "ar", 7, (2 << 20) // 4, **tab)["algo"] == "direct"
+    # the LL128 class range (when enabled) from the table: n = 2 up to 2 MiB, within the line area (~896 KiB)
+    assert plan(exe, 2, "ar", 7, (768 << 10) // 4, NCCL_AMD_LL128=1, **tab)["algo"] == "ll128"
+    assert plan(exe, 2, "ar", 7, (768 << 10) // 4, NCCL_AMD_LL128=1)["algo"] == "oneshot"   # built-in: 512 KiB
+    # the explicit knobs still win over the table
+    assert plan(exe, 8, "ar", 7, (512 << 10) // 4, NCCL_AMD_ONESHOT_BYTES=1 << 20, **tab)["algo"] == "oneshot"
+    assert plan(exe, 8, "ar", 7, (40 << 10) // 4, NCCL_AMD_LL_BYTES=1024, **tab)["algo"] == "oneshot"
+
+
+def test_size_table_bad_lines_are_ignored(exe, tmp_path):
+    t = tmp_path / "bad.txt"
+    t.write_text("8 48K\n"              # too few columns
+                 "x 1K 1K 1K\n"         # not a rank count
+                 "99 1K 1K 1K\n"        # out of range
+                 "8 1Q 1K 1K\n"         # bad size
+                 "8 - - 512K\n")        # the one good row
+    e = dict(NCCL_AMD_SIZE_TABLE=str(t), NCCL_DEBUG="WARN")
+    assert plan(exe, 8, "ar", 7, (512 << 10) // 4, **e)["algo"] == "oneshot"
+    assert plan(exe, 8, "ar", 7, (32 << 10) // 4, **e)["algo"] == "ll"          # built-in LL row kept
+    out = subprocess.run([exe, "8", "ar", "7", "1000"], env=dict(os.environ, **e), capture_output=True, text=True)
+    assert out.stderr.count("line ignored") + out.stdout.count("line ignored") == 4, out.stdout + out.stderr
+    # an unreadable file: the built-in table, with a warning
+    assert plan(exe, 8, "ar", 7, (256 << 10) // 4, NCCL_AMD_SIZE_TABLE=str(tmp_path / "none"))["algo"] == "oneshot"
+
+
+def test_eager_registration_eligibility(exe):
+    """with NCCL_AMD_EAGER_REGISTER=1 an unregistered collective of at least
+    NCCL_AMD_EAGER_REGISTER_BYTES whose staged plan would be the direct kernel registers its allocations on first use
+    and runs the zero-copy kernel (the stub's registration always succeeds). The decision uses only what every rank
+    shares (bytes, the size table), so every rank takes the same kernel."""
+    on = dict(NCCL_AMD_EAGER_REGISTER=1)
+    S = (256 << 20) // 4
+    assert plan(exe, 2, "ar", 7, S)["algo"] == "direct"                       # default: off
+    assert plan(exe, 2, "ar", 7, S, **on)["algo"] == "sym"
+    assert plan(exe, 8, "ar", 7, S, **on)["algo"] == "sym"
+    assert plan(exe, 8, "rs", 7, S // 8, **on)["algo"] == "sym"
+    assert plan(exe, 8, "ag", 7, S // 8, **on)["algo"] == "sym"
+    assert plan(exe, 8, "reduce", 7, S, **on)["algo"] == "direct"            # Reduce keeps the staged path
+    assert plan(exe, 2, "ar", 7, (1 << 20) // 4, **on)["algo"] == "oneshot"  # one-shot range: staged
+    assert plan(exe, 8, "ar", 7, (1 << 20) // 4, **on)["algo"] == "sym"      # above n = 8's one-shot range
+    assert plan(exe, 8, "ar", 7, (512 << 10) // 4, **on)["algo"] == "direct" # below the 1 MiB default threshold
+    assert plan(exe, 8, "ar", 7, (512 << 10) // 4, NCCL_AMD_EAGER_REGISTER_BYTES=256 << 10, **on)["algo"] == "sym"
+    assert plan(exe, 2, "ar", 7, 1000, **on)["algo"] == "ll"                 # LL range: untouched
+    assert plan(exe, 1, "ar", 7, S, **on)["algo"] == "copy"                  # one rank: nothing to register
+    assert plan(exe, 2, "ar", 7, S, NCCL_ALGO="RING", **on)["algo"] == "ring"  # forced reference algorithms win
