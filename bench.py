@@ -45,12 +45,16 @@ def bus_factor(coll: str, n: int) -> float:
     return 1.0
 
 
-def hbm_bytes_per_rank(coll: str, n: int, S: int) -> int:
-    """Algorithmic local-HBM bytes per launch per rank of this engine."""
+def hbm_bytes_per_rank(coll: str, n: int, S: int, pull_gather: bool = True) -> int:
+    """Algorithmic local-HBM bytes per launch per rank of this engine. Staged AllReduce: the scatter
+    reads (n-1)/n S and writes it into the owners' staging, the fold reads S/n + (n-1)/n S and writes S/n; the push
+    gather writes n-1 copies of the block and reads (n-1)/n S back (2S + 4(n-1)/n S), the pull gather (default) writes
+    ONE copy and reads the peers' over the links (3S + 2(n-1)/n S). PMC at n = 2/4/8: 1.004 / 1.002 / 1.005 x the
+    pull model (profiles/pmc_traffic.json)."""
     if n == 1:
         return 2 * S
     if coll == "allreduce":
-        return int(2 * S + 4 * (n - 1) * S / n)
+        return int(3 * S + 2 * (n - 1) * S / n) if pull_gather else int(2 * S + 4 * (n - 1) * S / n)
     raise ValueError(coll)
 
 
@@ -744,7 +748,7 @@ def main(argv=None):
 
     ms_per_step = wall / args.steps * 1e3
     value, algbw, busbw = rates(n, S, ms_per_step)
-    hbm_bytes = hbm_bytes_per_rank("allreduce", n, S)
+    hbm_bytes = hbm_bytes_per_rank("allreduce", n, S, pull_gather=os.environ.get("NCCL_AMD_AG_PULL", "1") != "0")
     probe_links = n > 1 and torch.cuda.device_count() >= n  # ranks on separate GPUs: links exist to measure
     # the dominant (only) kernel of a step: the first one this process launched (warm-up of the same call)
     kernels = launched_kernels(klog)

@@ -60,5 +60,15 @@ def test_rates():
     assert v2 == bus2 and abs(bus2 - S / 1e-3 / 1e9) < 1e-6
     v1, _, bus1 = bench.rates(1, 64 << 20, 1.0)
     assert bus1 == 0 and abs(v1 - 2 * (64 << 20) / 1e-3 / 1e9) < 1e-6
-    assert bench.hbm_bytes_per_rank("allreduce", 8, S) == int(2 * S + 4 * 7 * S / 8)
+    # the pull gather (default) writes one copy of each reduced block: 3S + 2(n-1)/n S; the push gather 2S + 4(n-1)/n S
+    assert bench.hbm_bytes_per_rank("allreduce", 8, S) == int(3 * S + 2 * 7 * S / 8)
+    assert bench.hbm_bytes_per_rank("allreduce", 8, S, pull_gather=False) == int(2 * S + 4 * 7 * S / 8)
+    assert bench.hbm_bytes_per_rank("allreduce", 2, S) == bench.hbm_bytes_per_rank("allreduce", 2, S, False) == 4 * S
+    # the committed PMC passes agree with the model within 1 % at every N the driver runs
+    import json
+    pmc = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
+                                      "pmc_traffic.json")))
+    for n in (2, 4, 8):
+        got = pmc[f"allreduce_f32_256MiB_n{n}"]["bytes_per_launch"]
+        assert abs(got / bench.hbm_bytes_per_rank("allreduce", n, S) - 1) < 0.01, (n, got)
     assert bench.bus_factor("reducescatter", 4) == 0.75 and bench.bus_factor("reduce", 4) == 1.0
