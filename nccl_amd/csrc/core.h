@@ -119,6 +119,7 @@ struct IpcImport {  // one mapping of a peer's allocation in this process
   int fd;
   int legacy;
   uint64_t fdDev, fdIno;  // identity of fd at import (ipcRelease closes it only if it still names that file)
+  uint64_t size;          // bytes mapped (the pending-release account, ipc.cc)
 };
 struct FdServer;
 bool ipcLegacy();

@@ -85,10 +85,24 @@ static std::mutex gPendMu;
 static std::vector<PendingRelease> gPending;
 static std::atomic<bool> gHavePending{false};
 
+// Bytes of released peer mappings waiting for a blocking entry point. A rank that only issues collectives keeps them
+// (and so the peers' freed HBM) until its next blocking call; past NCCL_AMD_PENDING_RELEASE_WARN_BYTES (4 GiB) that
+// is said once per crossing, with the calls that would return the memory.
+static uint64_t gPendingBytes = 0;
+static bool gPendingWarned = false;
+
 static void releaseLater(int device, const IpcImport& m) {
   std::lock_guard<std::mutex> g(gPendMu);
   gPending.push_back({m, device});
+  gPendingBytes += m.size;
   gHavePending.store(true, std::memory_order_release);
+  static const uint64_t warnAt = (uint64_t)paramInt("NCCL_AMD_PENDING_RELEASE_WARN_BYTES", (int64_t)4 << 30);
+  if (gPendingBytes >= warnAt && !gPendingWarned) {
+    gPendingWarned = true;
+    WARN("%.2f GiB of peers' deregistered buffers are still mapped in this process (device %d): they are unmapped at "
+         "this rank's next blocking call (ncclCommRegister / Deregister / Finalize / Destroy / Init), and until then "
+         "the peers' freed HBM stays allocated", gPendingBytes / (double)(1ull << 30), device);
+  }
 }
 
 void ipcDrainReleases() {
@@ -97,6 +111,8 @@ void ipcDrainReleases() {
   {
     std::lock_guard<std::mutex> g(gPendMu);
     batch.swap(gPending);
+    gPendingBytes = 0;
+    gPendingWarned = false;
     gHavePending.store(false, std::memory_order_release);
   }
   if (batch.empty()) return;
@@ -550,6 +566,7 @@ static ncclResult_t importFd(int fd, uint64_t size, IpcImport* out) {
     return ncclUnhandledCudaError;
   }
   out->ptr = p;
+  out->size = size;
   out->ext = em;
   return ncclSuccess;
 }

@@ -114,6 +114,11 @@ def _pinning_worker(rank, nranks, uid, q):
     blocking call (unmap). All ranks share the one GPU, so hipMemGetInfo sees every rank's memory."""
     try:
         os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
+        # ADVICE r4: released peer mappings past this many bytes are reported once (ipc.cc releaseLater)
+        os.environ["NCCL_AMD_PENDING_RELEASE_WARN_BYTES"] = str(256 * MIB)
+        logf = f"/tmp/nccl_amd_pinning_{os.getpid()}.log"
+        os.environ["NCCL_DEBUG"] = "WARN"
+        os.environ["NCCL_DEBUG_FILE"] = logf
         import torch
         import nccl_amd
         torch.cuda.set_device(0)
@@ -156,9 +161,10 @@ def _pinning_worker(rank, nranks, uid, q):
         free2 = torch.cuda.mem_get_info()[0]
         sync()
         comm.destroy()
-        q.put((rank, (ok, free0, free1, free2)))
+        warned = "still mapped in this process" in (open(logf).read() if os.path.exists(logf) else "")
+        q.put((rank, (ok, free0, free1, free2, warned)))
     except Exception as e:
-        q.put((rank, (False, repr(e), 0, 0)))
+        q.put((rank, (False, repr(e), 0, 0, False)))
 
 
 def test_eager_registration_memory_pinning(built):
@@ -166,8 +172,9 @@ def test_eager_registration_memory_pinning(built):
     the other maps, how much device memory stays held after the free, and that it all comes back after one blocking
     call on each side."""
     res = _spawn(_pinning_worker, 2)
-    for r, (ok, free0, free1, free2) in res.items():
+    for r, (ok, free0, free1, free2, warned) in res.items():
         assert ok is True, f"rank {r}: {free0}"
+        assert warned, f"rank {r}: 1 GiB of released peer mappings pending without the warning"
     free0, free1, free2 = res[0][1], res[0][2], res[0][3]
     held = (free0 - free1) / (1 << 30)
     back = (free2 - free1) / (1 << 30)

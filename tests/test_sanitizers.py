@@ -22,6 +22,7 @@ def sanitized():
 def _run(path, *args, **env):
     e = {k: v for k, v in os.environ.items() if not k.startswith("NCCL_")}
     e.update(NCCL_AMD_BOOTSTRAP_TIMEOUT_MS="20000", ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+             LSAN_OPTIONS="suppressions=" + os.path.join(ROOT, "tests", "native", "lsan.supp"),
              TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1", UBSAN_OPTIONS="print_stacktrace=1")
     e.update({k: str(v) for k, v in env.items()})
     r = subprocess.run([path, *args], env=e, capture_output=True, text=True, timeout=180)
