@@ -1,6 +1,6 @@
 #!/bin/bash
 # Reference-order parity + rate on the one-GPU box (n = 2 rehearsal): the parity tests of the reference-partition
-# paths, the rate of every mode in both orders, then a kernel trace of the default direct kernel against the
+# paths, the rate of every mode (REPS interleaved rounds each, median / min / max; both starting orders), then a kernel trace of the default direct kernel against the
 # reference-order kernel at K = 32 alone (collKernel<float,0,0> vs collKernel<float,0,5>).
 # Usage: gpurun -- 'bash scripts/ref_order_ab.sh [TAG]'   (output under gpurun_out/ref_ab_TAG)
 set -o pipefail

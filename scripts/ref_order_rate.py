@@ -1,7 +1,11 @@
 """One-GPU rehearsal of the AllReduce rate with the default direct kernel, the direct kernel on the reference's
 ring partition (NCCL_AMD_REF_ORDER=1) and the ring (NCCL_ALGO=RING), all ranks in one process, 256 MiB per rank.
-Prints one JSON line per (n, dtype, mode). usage: python scripts/ref_order_rate.py [MIB] [ITERS]"""
+Every mode is timed in REPS (default 3) interleaved rounds, the mode order rotated per round (each round creates the
+mode's communicators, times ITERS AllReduces and destroys them), so a 5 % difference is not lost in drift between
+repetitions. Prints one JSON line per (n, dtype, mode): median, min and max over the rounds.
+usage: python scripts/ref_order_rate.py [MIB] [ITERS]"""
 import json
+import statistics
 import os
 import sys
 
@@ -35,34 +39,44 @@ def main():
             order = list(MODES.items())
             if os.environ.get("REVERSE"):
                 order.reverse()
-            for mode, env in order:
-                for k in ("NCCL_AMD_REF_ORDER", "NCCL_MAX_CTAS", "NCCL_ALGO", "NCCL_AMD_REF_NCHANNELS"):
-                    os.environ.pop(k, None)
-                os.environ.update(env)
-                comms = nccl_amd.Communicator.init_all([0] * n)
-                streams = [torch.cuda.Stream() for _ in range(n)]
+            reps = int(os.environ.get("REPS", "3"))
+            times = {mode: [] for mode, _ in order}
+            errors = {mode: [] for mode, _ in order}
+            for rep in range(reps):
+                for j in range(len(order)):
+                    mode, env = order[(j + rep) % len(order)]
+                    for k in ("NCCL_AMD_REF_ORDER", "NCCL_MAX_CTAS", "NCCL_ALGO", "NCCL_AMD_REF_NCHANNELS"):
+                        os.environ.pop(k, None)
+                    os.environ.update(env)
+                    comms = nccl_amd.Communicator.init_all([0] * n)
+                    streams = [torch.cuda.Stream() for _ in range(n)]
 
-                def step():
-                    with nccl_amd.group():
-                        for c, s, (x, y) in zip(comms, streams, bufs):
-                            c.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, dt, 0, s.cuda_stream)
-                for _ in range(3):
-                    step()
-                torch.cuda.synchronize()
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(iters):
-                    step()
-                for s in streams:
-                    torch.cuda.current_stream().wait_stream(s)
-                e1.record()
-                torch.cuda.synchronize()
-                ms = e0.elapsed_time(e1) / iters
+                    def step():
+                        with nccl_amd.group():
+                            for c, s, (x, y) in zip(comms, streams, bufs):
+                                c.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, dt, 0, s.cuda_stream)
+                    for _ in range(3):
+                        step()
+                    torch.cuda.synchronize()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(iters):
+                        step()
+                    for s in streams:
+                        torch.cuda.current_stream().wait_stream(s)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    times[mode].append(e0.elapsed_time(e1) / iters)
+                    errors[mode] += [c.async_error() for c in comms if c.async_error()]
+                    for c in comms:
+                        c.destroy()
+            for mode, _ in order:
+                ms = statistics.median(times[mode])
                 print(json.dumps({"n": n, "dtype": dt, "mode": mode, "ms": round(ms, 4),
+                                  "ms_min": round(min(times[mode]), 4), "ms_max": round(max(times[mode]), 4),
+                                  "reps": len(times[mode]),
                                   "GBps_per_rank": round((mib << 20) / (ms * 1e-3) / 1e9, 1),
-                                  "async": [c.async_error() for c in comms]}), flush=True)
-                for c in comms:
-                    c.destroy()
+                                  "async": errors[mode]}), flush=True)
             del bufs
 
 
