@@ -238,6 +238,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
             torch.cuda.synchronize()
             cm.destroy()
         out["ar_fp16_sweep"] = [rows[k] for k in sorted(rows)]
+        out["size_table_row"] = size_table_row(n, out["ar_fp16_sweep"])
         for k, v in saved.items():
             os.environ.pop(k, None)
             if v is not None:
@@ -490,6 +491,31 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         del sendr, recvr, base
 
     return out
+
+
+def size_table_row(n: int, sweep: list) -> dict:
+    """The crossovers this sweep measured, as an NCCL_AMD_SIZE_TABLE row: the largest size up to
+    which LL beats one-shot and direct at every size, then the largest size above that up to which one-shot beats
+    direct at every size (LL128 left to the built-in row). `file_line` can be adopted as is:
+    NCCL_AMD_SIZE_TABLE=<file with that line>."""
+    def last_win(col, others, above=0):
+        lim = above
+        for r in sweep:
+            if r["bytes"] <= above:
+                continue
+            if col + "_us" not in r:
+                break
+            rivals = [r[o + "_us"] for o in others if o + "_us" in r]
+            if rivals and r[col + "_us"] > min(rivals):
+                break
+            lim = r["bytes"]
+        return lim
+    ll = last_win("ll", ("oneshot", "direct"))
+    one = last_win("oneshot", ("direct",), above=ll)  # = ll: no one-shot range (direct right after LL)
+    fmt = lambda b: "-" if b <= 0 else (f"{b >> 20}M" if b % (1 << 20) == 0 else f"{b >> 10}K" if b % 1024 == 0 else str(b))
+    return {"nranks": n, "ll_bytes": ll, "oneshot_bytes": one, "file_line": f"{n} {fmt(ll)} - {fmt(one)}",
+            "method": "largest size of the fp16 sweep up to which the column is the fastest of LL / one-shot / direct "
+                      "at every size (one-shot: vs direct); '-' = the built-in value"}
 
 
 def host_staged(comm, n: int, count: int, stream, dist) -> dict:

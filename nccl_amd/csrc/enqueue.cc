@@ -799,7 +799,10 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       } else {
         sp.coll = info.func == FUNC_REDUCESCATTER ? 2 /*SYM_RS*/ : 3 /*SYM_AG*/;
       }
-      if (n >= 3 && comm->tune.linkChannels > 0) maxCh = std::min(maxCh, comm->tune.linkChannels);  // CU budget
+      if (n >= 3 && comm->tune.linkChannels > 0 && tunedNch == 0) maxCh = std::min(maxCh, comm->tune.linkChannels);  // CU budget
+      // a tuner plugin's nChannels sets the zero-copy plan's channels too, as it does the staged plan's (the
+      // reference's nMaxChannels applies whichever buffers the collective runs on, enqueue.cc:2189)
+      if (tunedNch > 0) minPart = (spanBytes + tunedNch - 1) / tunedNch;
       int nch = (int)((spanBytes + minPart - 1) / minPart);
       if (nch < comm->minCTAs) nch = comm->minCTAs;
       if (nch > maxCh) nch = maxCh;

@@ -72,3 +72,24 @@ def test_rates():
         got = pmc[f"allreduce_f32_256MiB_n{n}"]["bytes_per_launch"]
         assert abs(got / bench.hbm_bytes_per_rank("allreduce", n, S) - 1) < 0.01, (n, got)
     assert bench.bus_factor("reducescatter", 4) == 0.75 and bench.bus_factor("reduce", 4) == 1.0
+
+
+def test_size_table_row_from_sweep():
+    """The N > 1 suite turns its C4 sweep into an NCCL_AMD_SIZE_TABLE row: LL up to the last size
+    where it beats one-shot and direct at every size, then one-shot up to where direct overtakes it."""
+    import bench
+    K = 1024
+    sweep = [{"bytes": b, "ll_us": ll, "oneshot_us": one, "direct_us": d}
+             for b, ll, one, d in ((8, 4, 6, 9), (4 * K, 5, 6, 9), (32 * K, 6, 7, 9), (64 * K, 9, 8, 10),
+                                   (256 * K, 20, 12, 13), (1 << 20, 60, 30, 25), (4 << 20, 200, 80, 50))]
+    row = bench.size_table_row(8, sweep)
+    assert (row["ll_bytes"], row["oneshot_bytes"]) == (32 * K, 256 * K)
+    assert row["file_line"] == "8 32K - 256K"
+    # no one-shot win right after LL: the one-shot range is empty (its limit = LL's)
+    sweep[3]["oneshot_us"] = 11   # 64 KiB: LL (9 us) now beats both, so LL extends to 64 KiB
+    sweep[4]["oneshot_us"] = 14   # 256 KiB: direct (13 us) beats one-shot
+    assert bench.size_table_row(4, sweep)["file_line"] == "4 64K - 64K"
+    # LL never wins: '-' keeps the built-in LL row
+    for r in sweep:
+        r["ll_us"] = 99
+    assert bench.size_table_row(2, sweep)["file_line"].startswith("2 - -")

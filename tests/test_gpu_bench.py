@@ -57,6 +57,8 @@ def test_bench_two_ranks_quick(built):
     # the unregistered headline buffers registered on first use, bitwise = the staged result
     assert s["eager_zero_copy"]["check"].startswith("pass") and s["eager_zero_copy"]["ms"] > 0, s["eager_zero_copy"]
     assert s["group_aggregation"]["aggregated_us_per_group"] > 0
+    # the C4 sweep's crossovers as a ready NCCL_AMD_SIZE_TABLE row
+    assert s["size_table_row"]["file_line"].startswith("2 "), s["size_table_row"]
     # the link probe and the fence on / off column at the top level of the N > 1 line
     assert "xgmi_links" in d and d["p2p_fence"]["check"] == "pass", (d.get("xgmi_links"), d.get("p2p_fence"))
     assert d["p2p_fence"]["fence_on_ms"] > 0 and d["p2p_fence"]["fence_off_ms"] > 0

@@ -138,3 +138,78 @@ def test_reference_basic_tuner_v4(built):
     for frag in ("collKernel<float, 0, 0>", "collKernel<float, 0, 1>", "collKernel<unsigned int, 0, 2>",
                  "collKernel<float, 0, 3>"):
         assert _first(seen, frag), f"want {frag} on one workgroup, launched {seen}"
+
+
+CONF_REGBUFF = """# the reference CSV's optional 9th / 10th columns: numPipeOps, regBuff
+allreduce,0,4294967295,ring,simple,6,-1,-1,-1,0
+allreduce,0,4294967295,tree,simple,4,-1,-1,-1,1
+"""
+
+
+def _regbuff_worker(plugin, conf, q):
+    try:
+        os.environ["NCCL_MULTI_RANK_GPU_ENABLE"] = "1"
+        os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "30000"
+        os.environ["NCCL_TUNER_PLUGIN"] = plugin
+        os.environ["NCCL_TUNER_CONFIG_FILE"] = conf
+        klog = f"/tmp/nccl_amd_reftuner_reg_{os.getpid()}.log"
+        if os.path.exists(klog):
+            os.remove(klog)
+        os.environ["NCCL_AMD_KERNEL_LOG"] = klog
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comms = nccl_amd.Communicator.init_all([0, 0])
+        streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+        count = 3 << 20
+        errs, launched = [], []
+        for registered in (False, True):
+            ins = G.make_inputs(2, 7, count, seed=760 + registered)
+            xs = [torch.from_numpy(a).cuda() for a in ins]
+            ys = [torch.empty_like(x) for x in xs]
+            hs = ([c.register_buffer(b.data_ptr(), count * 4) for c, x, y in zip(comms, xs, ys) for b in (x, y)]
+                  if registered else [])
+            torch.cuda.synchronize()
+            if os.path.exists(klog):
+                os.remove(klog)
+            with nccl_amd.group():
+                for c, s, x, y in zip(comms, streams, xs, ys):
+                    c.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+            torch.cuda.synchronize()
+            launched.append(open(klog).read().splitlines() if os.path.exists(klog) else [])
+            want = oracle.all_reduce(ins, 7, 0)
+            for r, y in enumerate(ys):
+                if not G.same_bits(y.cpu().numpy(), want, 7):
+                    errs.append(f"registered={registered} rank {r}: differs")
+            for i, h in enumerate(hs):
+                comms[i // 2].deregister_buffer(h)
+        for c in comms:
+            c.destroy()
+        q.put((errs, launched, ""))
+    except Exception as e:
+        q.put(([f"exception {e!r}"], [], ""))
+
+
+def test_reference_example_tuner_sees_regbuff(built, tmp_path):
+    """The plugin gets the reference's regBuff (enqueue.cc:2141-2147: both buffers registered): the example plugin's
+    regBuff column picks RING/SIMPLE on 6 channels for unregistered buffers (the staged direct kernel) and TREE/SIMPLE
+    on 4 for registered ones (the zero-copy kernel, on the plugin's 4 channels), bit-exact."""
+    plugin = os.path.join(REF, "libnccl-tuner-example.so")
+    _need(plugin)
+    conf = tmp_path / "regbuff.conf"
+    conf.write_text(CONF_REGBUFF)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_regbuff_worker, args=(plugin, str(conf), q))
+    p.start()
+    try:
+        errs, launched, _ = q.get(timeout=240)
+    except queue.Empty:
+        p.kill()
+        raise AssertionError("tuner worker timed out")
+    p.join(timeout=60)
+    assert not errs, "\n".join(errs)
+    assert any("collKernel<float, 0, 0>" in ln and " grid=6 " in ln for ln in launched[0]), launched
+    assert any("symKernel" in ln and " grid=4 " in ln for ln in launched[1]), launched
