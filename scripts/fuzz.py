@@ -2,7 +2,8 @@
 slot count, channel cap, protocol / algorithm, pull variants) and, per communicator, random collectives
 (type, op, count incl. ragged and tiny, misaligned bases, in place, root; sometimes a group of several
 collectives, so small AllReduces aggregate into LL batches between other ops; a quarter of the communicators
-in symmetric windows, a quarter on ncclCommRegister'd buffers) checked bit-exact against the CPU oracle. Usage: python scripts/fuzz.py SECONDS [SEED]. Prints one line per communicator."""
+in symmetric windows, a quarter on ncclCommRegister'd buffers; a quarter with eager registration) checked bit-exact
+against the CPU oracle. Usage: python scripts/fuzz.py SECONDS [SEED]. Prints one line per communicator."""
 import os
 import random
 import sys
@@ -19,7 +20,8 @@ from tests import gpu_cases as G  # noqa: E402
 KNOBS = ("NCCL_PROTO", "NCCL_ALGO", "NCCL_AMD_SLOT_BYTES", "NCCL_AMD_NSLOTS", "NCCL_MAX_CTAS", "NCCL_AMD_AG_PULL",
          "NCCL_AMD_RS_PULL", "NCCL_AMD_MIN_CHANNEL_BYTES", "NCCL_AMD_LL_CHANNEL_BYTES", "NCCL_AMD_LL128",
          "NCCL_AMD_LL128_CHANNEL_BYTES", "NCCL_AMD_SYM_WT", "NCCL_AMD_P2P_FENCE", "NCCL_AMD_LINK_CHANNELS",
-         "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER", "NCCL_LL_BUFFSIZE", "NCCL_LL128_BUFFSIZE", "NCCL_AMD_REF_NCHANNELS")
+         "NCCL_BUFFSIZE", "NCCL_AMD_REF_ORDER", "NCCL_LL_BUFFSIZE", "NCCL_LL128_BUFFSIZE", "NCCL_AMD_REF_NCHANNELS",
+         "NCCL_AMD_EAGER_REGISTER", "NCCL_AMD_EAGER_REGISTER_BYTES", "NCCL_AMD_EAGER_REGISTER_MAX")
 
 
 def settings(rng):
@@ -67,6 +69,12 @@ def settings(rng):
         env["NCCL_LL_BUFFSIZE"] = str(rng.choice([4096, 65536, 524288]))
     if rng.random() < 0.15:
         env["NCCL_LL128_BUFFSIZE"] = str(rng.choice([32768, 262144]))
+    if rng.random() < 0.25:  # eager zero-copy on the cases' plain torch buffers (register.cc), small thresholds too
+        env["NCCL_AMD_EAGER_REGISTER"] = "1"
+        if rng.random() < 0.6:
+            env["NCCL_AMD_EAGER_REGISTER_BYTES"] = str(rng.choice([16, 4096, 65536]))
+        if rng.random() < 0.3:
+            env["NCCL_AMD_EAGER_REGISTER_MAX"] = str(rng.choice([1, 2]))
     return env
 
 
