@@ -470,6 +470,9 @@ void windowsFree(ncclComm* comm, bool notifyPeers);
 // A blocking entry point's registration upkeep (register.cc): graph-held references whose graphs are gone are
 // dropped, stale and surplus eager registrations released, and retired registrations' RELEASE requests sent.
 void regBlockingPoint(ncclComm* comm);
+// Set by ncclGroupSimulateEnd around its planning (group.cc): an eager lookup then registers nothing and reports the
+// zero-copy plan the real group end would take (register.cc regLookup).
+extern thread_local bool tPlanOnly;
 // [p, +bytes) lies in a usable registration held by an ncclCommRegister handle or the eager cache (no side effects)
 bool regCovers(ncclComm* comm, const void* p, size_t bytes);
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)

@@ -93,7 +93,10 @@ static ncclResult_t groupSimulate(std::vector<CollInfo>& colls, float* estimated
     PlannedColl pc;
     pc.info = colls[i];
     const uint64_t opCount = pc.info.comm->opCount;  // nothing is launched: keep the op counter as it was
-    NCCLCHECK(planColl(pc.info, pc.p, pc.sp, &pc.kind));
+    tPlanOnly = true;  // and nothing is registered (eager registration, register.cc)
+    const ncclResult_t r = planColl(pc.info, pc.p, pc.sp, &pc.kind);
+    tPlanOnly = false;
+    NCCLCHECK(r);
     pc.info.comm->opCount = opCount;
     std::vector<PlannedColl>& run = open[pc.info.comm];
     if (!batchable(run, pc)) flush(pc.info.comm);

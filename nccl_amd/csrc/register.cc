@@ -446,6 +446,7 @@ void regBlockingPoint(ncclComm* comm) {
   if ((int)eager.size() > comm->tune.eagerMax) {
     std::sort(eager.begin(), eager.end(), [](const RegAlloc* a, const RegAlloc* b) { return a->lastUse < b->lastUse; });
     const size_t drop = eager.size() - (size_t)comm->tune.eagerMax;
+    DeviceRestore restore;  // the caller's current device survives the blocking call
     (void)hipSetDevice(comm->device);
     (void)hipDeviceSynchronize();
     for (size_t i = 0; i < drop; i++) regPut(comm, eager[i], REF_EAGER, true);
@@ -455,6 +456,8 @@ void regBlockingPoint(ncclComm* comm) {
   retired.swap(comm->regRetired);
   for (RegAlloc* ra : retired) regRelease(comm, ra);
 }
+
+thread_local bool tPlanOnly = false;
 
 bool regCovers(ncclComm* comm, const void* p, size_t bytes) {
   const uint64_t a = (uint64_t)p;
@@ -510,6 +513,13 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
            "NCCL_GRAPH_REGISTER=0 on every rank to avoid it)", comm->rank, (int)(rsRes != ncclSuccess ? rsRes : rrRes));
     (void)hipThreadExchangeStreamCaptureMode(&mode);
     (void)hipGetLastError();
+  } else if (eager && tPlanOnly) {
+    // ncclGroupSimulateEnd: no registration (no exports, no peer round trips); the real group end would register
+    // what is missing and run zero-copy, so the plan says so (the pointers are never used: nothing launches)
+    if (!rr || (send && !rs)) {
+      for (int r = 0; r < comm->nRanks; r++) rmtSend[r] = nullptr, rmtRecv[r] = nullptr;
+      return true;
+    }
   } else if (eager) {
     // first use of an unregistered allocation: map it into every peer now (one dma-buf export + one IMPORT request per
     // peer process, once per allocation); later collectives find it in comm->regs. A failure is remembered per

@@ -42,11 +42,19 @@ def _eager_worker(rank, nranks, uid, q):
                 bad = np.nonzero(got != want)[0]
                 errs.append(f"rank {rank} {name}: {bad.size} elements differ, first {bad[:4].tolist()}")
 
-        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
         x = torch.empty(count, dtype=torch.float32, device="cuda")
         y = torch.empty(count, dtype=torch.float32, device="cuda")
         rs = torch.empty(count // nranks, dtype=torch.float32, device="cuda")
         z = torch.empty(count * nranks, dtype=torch.float32, device="cuda")
+        # ncclGroupSimulateEnd plans the zero-copy kernel but registers nothing (no exports, no peer round trips)
+        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+        nccl_amd.group_start()
+        comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, sp)
+        est = nccl_amd.group_end(simulate=True)
+        sim_text = open(logf).read()[pos:]
+        if "registered allocation" in sim_text or "registered zero-copy" not in sim_text or est.estimated_time <= 0:
+            errs.append(f"rank {rank}: simulated group end registered something or planned no zero-copy kernel")
+        pos = os.path.getsize(logf)
         for it in range(3):  # the first round registers, the next two find the registrations
             ins = G.make_inputs(nranks, 7, count, seed=900 + it)
             x.copy_(torch.from_numpy(ins[rank]))
