@@ -93,3 +93,26 @@ def test_size_table_row_from_sweep():
     for r in sweep:
         r["ll_us"] = 99
     assert bench.size_table_row(2, sweep)["file_line"].startswith("2 - -")
+
+
+def test_scale_decisions_tool_reads_bench_lines():
+    """scripts/scale_decisions.py (the round-6 reading of the first 8-GPU SCALE record) finds bench lines wherever
+    they sit in a record and calls a difference only outside both columns' spreads."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(root, "profiles", "r05_scale_rehearsal_n8_onegpu.json")
+    out = subprocess.run([sys.executable, os.path.join(root, "scripts", "scale_decisions.py"), prof],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr
+    assert "N=8:" in out.stdout and "gather: pull (default) vs push: faster" in out.stdout, out.stdout
+    sys.path.insert(0, os.path.join(root, "scripts"))
+    import scale_decisions as sd
+    line = json.load(open(prof))
+    wrapped = {"runs": [{"parsed": {"tail": "noise\n" + json.dumps(line) + "\n"}}]}  # a driver-style record
+    assert [d["n_gpus"] for d in sd.bench_lines(wrapped)] == [8]
+    a, b = {"ms": 1.0, "ms_min": 0.95, "ms_max": 1.05}, {"ms": 1.08, "ms_min": 1.07, "ms_max": 1.09}
+    assert sd.compare(a, b).startswith("within spread")
+    b.update(ms=1.2, ms_min=1.19, ms_max=1.21)
+    assert sd.compare(a, b).startswith("faster")
