@@ -276,7 +276,10 @@ bool loadSizeTable(CommTuning* t, const char* path) {
 // and 2x headroom, rounded up to a power of two (>= 32): 32 channels at n = 3..4, 64 at n = 5..7, 128 at n = 8 —
 // the rest of the chip stays free for the compute a collective overlaps. n = 2 keeps every channel (one link,
 // nothing to overlap in the bench). NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS / config.maxCTAs overrule it, as does
-// NCCL_AMD_LINK_CHANNELS (0 = no budget).
+// NCCL_AMD_LINK_CHANNELS (0 = no budget). The (3n - 2) factor is the push gather's HBM bytes; the pull gather (the
+// default since round 5) moves (2.5n - 1) B_link's worth, so the budget keeps ≥ 20 % more headroom than it states —
+// deliberately, until the 8-GPU tuning matrix measures R_cu for link traffic (the one-GPU loopback fan-out measures
+// ≈ 23 GB/s written + 23 GB/s read per workgroup = the 50 GB/s above, gpurun_out r05 xgmi_probe loopback).
 int linkChannelBudget(int n) {
   if (n < 3) return 0;
   const double bLinkGBps = 76.8, cuGBps = 50.0, headroom = 2.0;
