@@ -517,6 +517,7 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     // ncclGroupSimulateEnd: no registration (no exports, no peer round trips); the real group end would register
     // what is missing and run zero-copy, so the plan says so (the pointers are never used: nothing launches)
     if (!rr || (send && !rs)) {
+      if (!comm->regIpcAll) return false;  // registrations would stay local (regCreate): the staged plan
       for (int r = 0; r < comm->nRanks; r++) rmtSend[r] = nullptr, rmtRecv[r] = nullptr;
       return true;
     }
