@@ -207,8 +207,15 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         # --- configs[3]: fp16 AllReduce sweep: LL vs one-shot vs direct. Protocol/algorithm knobs are read at
         #     communicator init (like the reference's NCCL_PARAMs), so each column gets its own communicator ---
         top = (16 if quick else 256) * MIB
-        buf = torch.empty(top // 2, dtype=torch.float16, device="cuda").uniform_(-1, 1)
+        # small integers (|x| <= 8 * n): every fp16 sum is exact in any fold order, so every column's result must
+        # equal base * n(n+1)/2 bit for bit — the sweep checks LL / LL128 / one-shot / ring / tree over the links
+        # (LL's 8-byte flag/data atomicity across devices) at every size it times
+        g.manual_seed(555)
+        base = torch.randint(-8, 9, (top // 2,), device="cuda", generator=g, dtype=torch.int32).to(torch.float16)
+        buf = base * (rank + 1)
+        want = base * (n * (n + 1) // 2)
         res = torch.empty_like(buf)
+        sweep_check = {}
         cols = {"ll": {"NCCL_PROTO": "LL"}, "ll128": {"NCCL_PROTO": "LL128"},
                 "oneshot": {"NCCL_ALGO": "ONESHOT", "NCCL_PROTO": "Simple"},
                 "direct": {"NCCL_ALGO": "DIRECT", "NCCL_PROTO": "Simple"},
@@ -230,7 +237,11 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                 if size <= limits.get(name, top):
                     c = size // 2
                     it = 50 if size <= 4 * MIB else 10
+                    res[:c].zero_()
                     ms = tmax(_tm(lambda: cm.all_reduce_raw(buf.data_ptr(), res.data_ptr(), c, 6, 0, sp), stream, it))
+                    torch.cuda.synchronize()
+                    if not torch.equal(res[:c], want[:c]) and name not in sweep_check:
+                        sweep_check[name] = f"FAIL at {size} bytes"
                     row = rows.setdefault(size, {"bytes": size})
                     row[name + "_us"] = round(ms * 1e3, 2)
                     row[name + "_busbw_GBps"] = round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)
@@ -238,12 +249,14 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
             torch.cuda.synchronize()
             cm.destroy()
         out["ar_fp16_sweep"] = [rows[k] for k in sorted(rows)]
+        out["ar_fp16_sweep_check"] = {name: ("pass (exact integer sums, every size)" if agree(name not in sweep_check)
+                                             else sweep_check.get(name, "FAIL on another rank")) for name in cols}
         out["size_table_row"] = size_table_row(n, out["ar_fp16_sweep"])
         for k, v in saved.items():
             os.environ.pop(k, None)
             if v is not None:
                 os.environ[k] = v
-        del buf, res
+        del buf, res, base, want
 
     if selected("group_aggregation"):
         trace("group_aggregation")

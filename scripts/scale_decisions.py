@@ -67,6 +67,10 @@ def decisions(line):
     for c in ("256", "128", "64", "32"):
         out.append(f"  channels: default vs NCCL_MAX_CTAS={c}: {compare(dflt, column(runs, {'NCCL_MAX_CTAS': c}))}")
     out.append(f"  eager zero-copy vs default: {compare(column(runs, {'NCCL_AMD_EAGER_REGISTER': '1'}), dflt)}")
+    chk = suite.get("ar_fp16_sweep_check")
+    if chk:
+        bad = {k: v for k, v in chk.items() if not v.startswith("pass")}
+        out.append(f"  C4 sweep results: {'every column exact' if not bad else bad}")
     row = suite.get("size_table_row")
     out.append(f"  size table row: {row['file_line'] if row else 'n/a'}")
     atom = suite.get("xgmi_probe", {}).get("store_atomicity")
