@@ -263,8 +263,11 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         # --- group aggregation: 32 small AllReduce ops in one ncclGroupStart/End,
         #     one LL launch vs one launch per op ---
         agg = {}
-        buf = torch.empty(32 * 4096, dtype=torch.float16, device="cuda").uniform_(-1, 1)
+        g.manual_seed(556)  # small integers: exact sums, so both columns are checked against base * n(n+1)/2
+        base = torch.randint(-8, 9, (32 * 4096,), device="cuda", generator=g, dtype=torch.int32).to(torch.float16)
+        buf = base * (rank + 1)
         res = torch.empty_like(buf)
+        okg = True
         saved = {k: os.environ.get(k) for k in ("NCCL_ALGO", "NCCL_PROTO", "NCCL_AMD_NO_AGGREGATION", "NCCL_AMD_REF_ORDER")}
         for name, env in (("aggregated", {}), ("one_launch_per_op", {"NCCL_AMD_NO_AGGREGATION": "1"})):
             for k in saved:
@@ -276,17 +279,20 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                 with nccl_amd.group():
                     for k in range(32):
                         cm.all_reduce_raw(buf.data_ptr() + k * 8192, res.data_ptr() + k * 8192, 2048, 6, 0, sp)
+            res.zero_()
             ms = tmax(_tm(grouped, stream, 20))
             agg[name + "_us_per_group"] = round(ms * 1e3, 2)
             torch.cuda.synchronize()
+            okg = okg and bool(torch.equal(res, base * (n * (n + 1) // 2)))
             cm.destroy()
         agg["config"] = "32 x ncclAllReduce fp16 4 KiB in one group"
+        agg["check"] = "pass (exact integer sums, both columns)" if agree(okg) else "FAIL"
         out["group_aggregation"] = agg
         for k, v in saved.items():
             os.environ.pop(k, None)
             if v is not None:
                 os.environ[k] = v
-        del buf, res
+        del buf, res, base
 
     if selected("reduce_int32"):
         trace("reduce_int32")
@@ -339,15 +345,25 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         lat = []
         hbuf = win_t[:S].view(torch.float16)
         hres = win_t[S:].view(torch.float16)
+        g.manual_seed(557)  # small integers in the window: every size's result checked exactly
+        hbase = torch.randint(-8, 9, (S // 2,), device="cuda", generator=g, dtype=torch.int32).to(torch.float16)
+        hbuf.copy_(hbase * (rank + 1))
+        hwant = hbase * (n * (n + 1) // 2)
+        okw = True
         size = 8
         while size <= (16 if quick else 64) * MIB:
             cc = size // 2
             it = 50 if size <= 4 * MIB else 10
+            hres[:cc].zero_()
             ms = tmax(_tm(lambda: comm.all_reduce_raw(hbuf.data_ptr(), hres.data_ptr(), cc, 6, 0, sp), stream, it))
+            torch.cuda.synchronize()
+            okw = okw and bool(torch.equal(hres[:cc], hwant[:cc]))
             lat.append({"bytes": size, "us": round(ms * 1e3, 2),
                         "busbw_GBps": round(size / (ms * 1e-3) / 1e9 * bus_factor("allreduce", n), 2)})
             size *= 4
         sym["ar_fp16_sweep"] = lat
+        sym["ar_fp16_sweep_check"] = "pass (exact integer sums, every size)" if agree(okw) else "FAIL"
+        del hbase, hwant
         out["symmetric_window"] = sym
         torch.cuda.synchronize()
         comm.deregister_window(win)

@@ -56,7 +56,8 @@ def test_bench_two_ranks_quick(built):
     assert all(r["reps"] >= 3 and r["ms_min"] <= r["ms"] <= r["ms_max"] for r in s["staged_tuning"]["runs"])
     # the unregistered headline buffers registered on first use, bitwise = the staged result
     assert s["eager_zero_copy"]["check"].startswith("pass") and s["eager_zero_copy"]["ms"] > 0, s["eager_zero_copy"]
-    assert s["group_aggregation"]["aggregated_us_per_group"] > 0
+    assert s["group_aggregation"]["aggregated_us_per_group"] > 0 and s["group_aggregation"]["check"].startswith("pass")
+    assert s["symmetric_window"]["ar_fp16_sweep_check"].startswith("pass")
     # every column of the C4 sweep checked at every size (exact integer sums)
     assert all(v.startswith("pass") for v in s["ar_fp16_sweep_check"].values()), s["ar_fp16_sweep_check"]
     # the C4 sweep's crossovers as a ready NCCL_AMD_SIZE_TABLE row
