@@ -146,14 +146,20 @@ struct LLOp {
 // The kernel arguments hold room for K ops: a lone op launches with K = 1 (88 bytes of kernel arguments
 // instead of 1.8 KiB; the host issue cost of a launch grows with its argument bytes, about 3 us at 64 B
 // vs 6.5 us at 2 KiB on the MI355X box, scripts/launch_probe.hip).
+// A batch (K > 1) also carries, per LL channel (at most 32), the bit mask of the ops that run on it: a work-group
+// reads ONE word of the argument block to find its ops, instead of every op's channel range (each op descriptor
+// its own line of the argument block, and every work-group of the launch reading them all).
+constexpr int kMaxLLChannels = 32;
 template <int K>
 struct LLArgs {
   const DevComm* comm;
   uint64_t redArg;
   const void* redArgPtr;
   int nOps;
+  uint32_t chMask[K > 1 ? kMaxLLChannels : 1];  // bit k: op k runs on this channel (K > 1 only)
   LLOp ops[K];
 };
+static_assert(kMaxLLBatch <= 32, "LLArgs::chMask holds one bit per op");
 using LLBatchArgs = LLArgs<kMaxLLBatch>;
 
 // Symmetric (window) collective arguments: every rank's buffers as mapped in this process (reference

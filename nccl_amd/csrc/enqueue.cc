@@ -934,6 +934,10 @@ ncclResult_t launchBatch(std::vector<PlannedColl>& run) {
     }
     p.ll.nOps = (int)run.size();
     p.nChannels = used < comm->llChannels ? used : comm->llChannels;
+    // per channel, the ops it runs (the kernel walks these bits in batch order)
+    std::fill(p.ll.chMask, p.ll.chMask + kMaxLLChannels, 0u);
+    for (int k = 0; k < p.ll.nOps; k++)
+      for (int j = 0; j < p.ll.ops[k].nch; j++) p.ll.chMask[(p.ll.ops[k].chOff + j) % comm->llChannels] |= 1u << k;
     TRACE("LL batch: %d ops (first %s), %d channels", p.ll.nOps, kFuncName[run[0].info.func], p.nChannels);
     return launchPlan(p);
   }

@@ -6,6 +6,8 @@
 //             [-o op: sum|max] [-t type: float|half|bf16|int] [-g 0|1 (replay a captured hipGraph)]
 //             [-c coll: ar|rs|ag|reduce (root 0)] [-H 0|1 (hold: a spin kernel occupies each stream while the timed
 //             collectives are issued, so host(us) is the pure issue cost; keep -i small, e.g. 100)]
+//             [-G K (K collectives of `bytes` per rank in every group, on K disjoint slices of the buffers: group
+//             aggregation; time(us) and host(us) are per group)]
 //
 // All ranks live in this process (ncclCommInitAll over ndev devices x ranks_per_dev; several ranks per
 // device need NCCL_MULTI_RANK_GPU_ENABLE=1). Each rank r fills its input with (r+1), so every element of
@@ -70,14 +72,14 @@ __global__ void checkKernel(const void* p, size_t n, int type, float want, size_
 }
 
 int main(int argc, char** argv) {
-  int ndevArg = 0, perDev = 1, iters = 20, warmup = 5, graph = 0, hold = 0;
+  int ndevArg = 0, perDev = 1, iters = 20, warmup = 5, graph = 0, hold = 0, perGroup = 1;
   size_t minB = 8, maxB = 64 << 20;
   double factor = 2;
   ncclRedOp_t op = ncclSum;
   ncclDataType_t type = ncclFloat32;
   char coll = 'a';  // a: AllReduce, r: ReduceScatter, g: AllGather
   int c;
-  while ((c = getopt(argc, argv, "d:r:b:e:f:i:w:o:t:g:c:H:")) != -1) {
+  while ((c = getopt(argc, argv, "d:r:b:e:f:i:w:o:t:g:c:H:G:")) != -1) {
     switch (c) {
       case 'd': ndevArg = atoi(optarg); break;
       case 'r': perDev = atoi(optarg); break;
@@ -88,6 +90,7 @@ int main(int argc, char** argv) {
       case 'w': warmup = atoi(optarg); break;
       case 'g': graph = atoi(optarg); break;
       case 'H': hold = atoi(optarg); break;
+      case 'G': perGroup = std::max(1, atoi(optarg)); break;
       case 'c': coll = !strcmp(optarg, "rs") ? 'r' : !strcmp(optarg, "ag") ? 'g' : !strcmp(optarg, "reduce") ? 'd' : 'a'; break;
       case 'o': op = !strcmp(optarg, "max") ? ncclMax : ncclSum; break;
       case 't':
@@ -114,8 +117,8 @@ int main(int argc, char** argv) {
   unsigned long long* bad = nullptr;
   for (int r = 0; r < n; r++) {
     HIPCK(hipSetDevice(devs[r]));
-    HIPCK(hipMalloc(&send[r], maxB));
-    HIPCK(hipMalloc(&recv[r], maxB));
+    HIPCK(hipMalloc(&send[r], maxB * perGroup));  // -G: K slices of the largest size
+    HIPCK(hipMalloc(&recv[r], maxB * perGroup));
     // own hardware queue per rank (ranks sharing a device must run concurrently)
     int ncu = 0;
     HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, devs[r]));
@@ -124,7 +127,8 @@ int main(int argc, char** argv) {
     HIPCK(hipExtStreamCreateWithCUMask(&streams[r], (uint32_t)mask.size(), mask.data()));
     HIPCK(hipEventCreate(&ev0[r]));
     HIPCK(hipEventCreate(&ev1[r]));
-    hipLaunchKernelGGL(fillKernel, dim3(1024), dim3(256), 0, streams[r], send[r], maxB / es, (int)type, (float)(r + 1));
+    hipLaunchKernelGGL(fillKernel, dim3(1024), dim3(256), 0, streams[r], send[r], maxB * perGroup / es, (int)type,
+                       (float)(r + 1));
   }
   HIPCK(hipSetDevice(devs[0]));
   HIPCK(hipMallocManaged(&bad, sizeof(*bad)));
@@ -134,11 +138,14 @@ int main(int argc, char** argv) {
          coll == 'r' ? "ReduceScatter" : coll == 'g' ? "AllGather" : coll == 'd' ? "Reduce (root 0)" : "AllReduce", n, ndev,
          perDev, (int)type,
          op == ncclSum ? "sum" : "max", graph ? "hipGraph replay" : "eager launches");
-  auto issue = [&](int r, size_t count) {
-    if (coll == 'r') return ncclReduceScatter(send[r], recv[r], count / n, type, op, comms[r], streams[r]);
-    if (coll == 'g') return ncclAllGather(send[r], recv[r], count / n, type, comms[r], streams[r]);
-    if (coll == 'd') return ncclReduce(send[r], recv[r], count, type, op, 0, comms[r], streams[r]);
-    return ncclAllReduce(send[r], recv[r], count, type, op, comms[r], streams[r]);
+  auto issue = [&](int r, size_t count, size_t slice = 0) {
+    const size_t off = slice * count * es;  // -G: op k of a group works on bytes [k * bytes, (k + 1) * bytes)
+    const char* sb = (const char*)send[r] + off;
+    char* rb = (char*)recv[r] + off;
+    if (coll == 'r') return ncclReduceScatter(sb, rb, count / n, type, op, comms[r], streams[r]);
+    if (coll == 'g') return ncclAllGather(sb, rb, count / n, type, comms[r], streams[r]);
+    if (coll == 'd') return ncclReduce(sb, rb, count, type, op, 0, comms[r], streams[r]);
+    return ncclAllReduce(sb, rb, count, type, op, comms[r], streams[r]);
   };
   printf("# %12s %12s %10s %10s %10s %8s %9s\n", "bytes", "count", "time(us)", "algbw", "busbw", "#wrong", "host(us)");
   const size_t step = coll == 'a' || coll == 'd' ? es : es * n;
@@ -148,7 +155,8 @@ int main(int argc, char** argv) {
     auto enqueue = [&](int iters_) {
       for (int k = 0; k < iters_; k++) {
         NCK(ncclGroupStart());
-        for (int r = 0; r < n; r++) NCK(issue(r, count));
+        for (int r = 0; r < n; r++)
+          for (int j = 0; j < perGroup; j++) NCK(issue(r, count, j));
         NCK(ncclGroupEnd());
       }
     };
@@ -192,7 +200,7 @@ int main(int argc, char** argv) {
     *bad = 0;
     for (int r = 0; r < (coll == 'd' ? 1 : n); r++) {  // Reduce: only the root's output is defined
       HIPCK(hipSetDevice(devs[r]));
-      const size_t outCount = coll == 'r' ? count / n : count;
+      const size_t outCount = (coll == 'r' ? count / n : count) * (perGroup > 1 && coll != 'g' && coll != 'r' ? perGroup : 1);
       hipLaunchKernelGGL(checkKernel, dim3(256), dim3(256), 0, streams[r], recv[r], outCount, (int)type, want,
                          coll == 'g' ? count / n : (size_t)0, bad);
       HIPCK(hipStreamSynchronize(streams[r]));
