@@ -153,6 +153,7 @@ constexpr int kMaxLLChannels = 32;
 template <int K>
 struct LLArgs {
   const DevComm* comm;
+  uint64_t* counters;  // comm->counters (device): the channels' LL epochs load beside the DevComm, not after it
   uint64_t redArg;
   const void* redArgPtr;
   int nOps;

@@ -653,6 +653,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   if (!refOrder && !ringProtoPart && llPlan(info, &p.ll.ops[0])) {
     p.algo = ALGO_LL;
     p.ll.comm = comm->devComm;
+    p.ll.counters = comm->counters;
     p.ll.redArg = p.args.redArg;
     p.ll.redArgPtr = p.args.redArgPtr;
     p.ll.nOps = 1;

@@ -1489,7 +1489,7 @@ __global__ void __launch_bounds__(kThreads) kCoResident llKernel(LLArgs<K> a) {
     __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
   }
   const Red<T, OP> fn(opArg);
-  uint64_t e64 = dc.counters[ctrIndex(c, CTR_LL, 0)];
+  uint64_t e64 = a.counters[ctrIndex(c, CTR_LL, 0)];
   __syncthreads();
   const int L = dc.llChannels;
   // the ops this channel runs, in batch order: one word of the arguments (host-built from the ops' channel
@@ -1511,7 +1511,7 @@ __global__ void __launch_bounds__(kThreads) kCoResident llKernel(LLArgs<K> a) {
                                   : llChannelOp<T, OP>(dc, fn, o, c, j, e64, abortSh);
     if (!ok) break;
   }
-  if (threadIdx.x == 0) dc.counters[ctrIndex(c, CTR_LL, 0)] = e64;
+  if (threadIdx.x == 0) a.counters[ctrIndex(c, CTR_LL, 0)] = e64;
 }
 
 // ------------------------------------------------------------------------------------ symmetric windows
@@ -1774,6 +1774,7 @@ template <typename T, int OP, int K>
 inline void launchLLK(const LaunchPlan& p) {
   LLArgs<K> a;
   a.comm = p.ll.comm;
+  a.counters = p.ll.counters;
   a.redArg = p.ll.redArg;
   a.redArgPtr = p.ll.redArgPtr;
   a.nOps = p.ll.nOps;
