@@ -1104,9 +1104,15 @@ namespace ncclamd {
 // sends only after finishing epoch e, so parity e's lines are never overwritten while still unread.
 // Fold order per element is the reference ring order of its owner block (owner+1, ..., owner): results
 // are identical to the other AllReduce paths.
-__device__ __forceinline__ uint64_t loadLL(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+// A line is read with ONE 16-byte load (the reference's ld.volatile.v4, prims_ll.h): each 8-byte half {data32, flag32}
+// is single-copy atomic, so a half whose flag matches carries its data whatever the other half shows. (Two 8-byte
+// loads, the second issued only once the first had matched, put two memory latencies on every line of the poll.)
+// The line area is uncached memory: no cached copy can be stale (loadLine16 / loadSeenLine16 below).
+__device__ __forceinline__ uint64_t llPayload(u32x4 v) { return (uint64_t)v.x | ((uint64_t)v.z << 32); }
+__device__ __forceinline__ u32x4 loadLine16(const char* p) { return *(const volatile u32x4*)p; }  // polls
+// Re-reads of lines a poll has already seen complete: uncached memory, so a plain load cannot hit a stale
+// copy; not volatile, so the loads of several peers' lines can be in flight together.
+__device__ __forceinline__ u32x4 loadSeenLine16(const char* p) { return __builtin_nontemporal_load((const u32x4*)p); }
 
 template <typename T, int OP>
 __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>& fn, const LLOp& op, int c, int j,
@@ -1193,8 +1199,8 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
     while (pending) {
       for (int q = 0; q < n; q++) {
         if (!(pending & (1u << q))) continue;
-        const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
-        if ((uint32_t)(loadLL(ln) >> 32) == flag && (uint32_t)(loadLL(ln + 1) >> 32) == flag) pending &= ~(1u << q);
+        const u32x4 v = loadLine16(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
+        if (v.y == flag && v.w == flag) pending &= ~(1u << q);
       }
       if (pending) __builtin_amdgcn_s_sleep(1);
       if (pending && (++spins & 1023) == 0) {
@@ -1219,8 +1225,7 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
         if (q == me) {
           if (dst != send) storePayload(dst, pk, payload(send, pk));
         } else {
-          const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
-          storePayload(dst, pk, (loadLL(ln) & 0xffffffffull) | (loadLL(ln + 1) << 32));
+          storePayload(dst, pk, llPayload(loadSeenLine16(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16)));
         }
       }
       continue;
@@ -1238,8 +1243,7 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
       if (q == me) {
         x.u = myV;
       } else {
-        const uint64_t* ln = (const uint64_t*)(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16);
-        x.u = (loadLL(ln) & 0xffffffffull) | (loadLL(ln + 1) << 32);
+        x.u = llPayload(loadSeenLine16(myLL + llLineOffset(dc, c, par, q) + (pk - lo) * 16));
       }
 #pragma unroll
       for (int e = 0; e < EPP; e++) {
@@ -1263,10 +1267,6 @@ __device__ __forceinline__ bool llChannelOp(const DevComm& dc, const Red<T, OP>&
 // measured for 64-byte segments (never torn) and refuted for 128-byte lines (torn in ~1.4 % of racing reads,
 // DESIGN.md §10.1). Payloads, fold order, batching, epochs and parity double-buffering are the LL kernel's;
 // the line area is its own (ll64LineOffset), so neither protocol can mistake the other's payload for a flag.
-__device__ __forceinline__ u32x4 loadLine16(const char* p) { return *(const volatile u32x4*)p; }  // polls
-// Re-reads of lines a poll has already seen complete: uncached memory, so a plain load cannot hit a stale
-// copy; not volatile, so the loads of several peers' lines can be in flight together.
-__device__ __forceinline__ u32x4 loadSeenLine16(const char* p) { return __builtin_nontemporal_load((const u32x4*)p); }
 
 template <typename T, int OP>
 __device__ __forceinline__ bool ll64ChannelOp(const DevComm& dc, const Red<T, OP>& fn, const LLOp& op, int c, int j,
