@@ -196,13 +196,14 @@ void loadTuning(CommTuning* t) {
 // Built-in rows (one-GPU rehearsal crossovers): LL up to max(16 KiB, 256 KiB / n), the LL128 class
 // (when enabled) up to max(64 KiB, 1 MiB / n), one-shot up to 2 MiB / n (2 MiB at n = 2). NCCL_AMD_SIZE_TABLE=<file>
 // replaces rows without a rebuild, so the crossovers an 8-GPU sweep measures can be adopted as data:
-//   # nranks  ll      ll128   oneshot      (bytes; K / M / G suffixes; '-' keeps the built-in value)
+//   # nranks  ll      ll128   oneshot      (bytes; K / M / G suffixes; '-' keeps the built-in value; 0 = off)
 //   8         48K     -       512K
 //   *         -       -       1M           ('*': every rank count; later lines override earlier ones)
 // Rank 0's table is the communicator's (the tuning block is agreed at init), so every rank plans alike.
+// A byte count, or -1 for '-' (keep the built-in value). 0 is a size like any other (e.g. "8 0 - -": no LL at n = 8).
 static int64_t parseBytes(const char* tok, bool* ok) {
   *ok = true;
-  if (!strcmp(tok, "-")) return 0;
+  if (!strcmp(tok, "-")) return -1;
   char* end = nullptr;
   const double v = strtod(tok, &end);
   if (end == tok || v < 0) {
@@ -215,7 +216,8 @@ static int64_t parseBytes(const char* tok, bool* ok) {
   else if (*end == 'g' || *end == 'G') m = 1024.0 * 1024 * 1024, end++;
   if (*end == 'b' || *end == 'B') end++;
   if (*end != '\0') *ok = false;
-  return (int64_t)(v * m);
+  const double bytes = v * m;
+  return bytes >= 9.0e18 ? INT64_MAX : (int64_t)bytes;  // (beyond any buffer: "always")
 }
 
 bool loadSizeTable(CommTuning* t, const char* path) {
@@ -250,9 +252,9 @@ bool loadSizeTable(CommTuning* t, const char* path) {
       else if (end != a && *end == '\0' && nr >= 1 && nr <= NCCL_AMD_MAX_RANKS) lo = hi = (int)nr;
       if (lo && okB && okC && okD) {
         for (int n = lo; n <= hi; n++) {
-          if (vb) t->tableLL[n] = vb;
-          if (vc) t->tableLL128[n] = vc;
-          if (vd) t->tableOneShot[n] = vd;
+          if (vb >= 0) t->tableLL[n] = vb;
+          if (vc >= 0) t->tableLL128[n] = vc;
+          if (vd >= 0) t->tableOneShot[n] = vd;
         }
         rows++;
         continue;

@@ -414,6 +414,19 @@ def test_size_table_bad_lines_are_ignored(exe, tmp_path):
     assert plan(exe, 8, "ar", 7, (256 << 10) // 4, NCCL_AMD_SIZE_TABLE=str(tmp_path / "none"))["algo"] == "oneshot"
 
 
+def test_size_table_zero_and_huge_sizes(exe, tmp_path):
+    # 0 is a size (no LL at n = 8: one-shot from the first byte), '-' keeps the built-in value; a size beyond any buffer
+    # saturates instead of overflowing (one-shot at every size for n = 4)
+    t = tmp_path / "edge.txt"
+    t.write_text("8 0 - -\n4 - - 1e30\n")
+    tab = dict(NCCL_AMD_SIZE_TABLE=str(t))
+    assert plan(exe, 8, "ar", 7, 8, **tab)["algo"] == "oneshot"
+    assert plan(exe, 8, "ar", 7, 8)["algo"] == "ll"
+    assert plan(exe, 8, "ar", 7, (1 << 20) // 4, **tab)["algo"] == "direct"          # its one-shot row kept
+    assert plan(exe, 4, "ar", 7, (64 << 20) // 4, **tab)["algo"] == "oneshot"
+    assert plan(exe, 4, "ar", 7, 8, **tab)["algo"] == "ll"
+
+
 def test_eager_registration_eligibility(exe):
     """with NCCL_AMD_EAGER_REGISTER=1 an unregistered collective of at least
     NCCL_AMD_EAGER_REGISTER_BYTES whose staged plan would be the direct kernel registers its allocations on first use
