@@ -530,6 +530,8 @@ def size_table_row(n: int, sweep: list) -> dict:
     direct at every size (LL128 left to the built-in row). `file_line` can be adopted as is:
     NCCL_AMD_SIZE_TABLE=<file with that line>."""
     def last_win(col, others, above=0):
+        if not any(col + "_us" in r for r in sweep):
+            return None  # not measured: keep the built-in value
         lim = above
         for r in sweep:
             if r["bytes"] <= above:
@@ -542,11 +544,12 @@ def size_table_row(n: int, sweep: list) -> dict:
             lim = r["bytes"]
         return lim
     ll = last_win("ll", ("oneshot", "direct"))
-    one = last_win("oneshot", ("direct",), above=ll)  # = ll: no one-shot range (direct right after LL)
-    fmt = lambda b: "-" if b <= 0 else (f"{b >> 20}M" if b % (1 << 20) == 0 else f"{b >> 10}K" if b % 1024 == 0 else str(b))
+    one = last_win("oneshot", ("direct",), above=ll or 0)  # = ll: no one-shot range (direct right after LL)
+    # 0 (the column never won) turns the range off; '-' (not measured) keeps the built-in value
+    fmt = lambda b: "-" if b is None else (f"{b >> 20}M" if b and b % (1 << 20) == 0 else f"{b >> 10}K" if b and b % 1024 == 0 else str(b))
     return {"nranks": n, "ll_bytes": ll, "oneshot_bytes": one, "file_line": f"{n} {fmt(ll)} - {fmt(one)}",
             "method": "largest size of the fp16 sweep up to which the column is the fastest of LL / one-shot / direct "
-                      "at every size (one-shot: vs direct); '-' = the built-in value"}
+                      "at every size (one-shot: vs direct); 0 = never, '-' = not measured (the built-in value)"}
 
 
 def host_staged(comm, n: int, count: int, stream, dist) -> dict:

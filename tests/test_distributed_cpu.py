@@ -89,10 +89,14 @@ def test_size_table_row_from_sweep():
     sweep[3]["oneshot_us"] = 11   # 64 KiB: LL (9 us) now beats both, so LL extends to 64 KiB
     sweep[4]["oneshot_us"] = 14   # 256 KiB: direct (13 us) beats one-shot
     assert bench.size_table_row(4, sweep)["file_line"] == "4 64K - 64K"
-    # LL never wins: '-' keeps the built-in LL row
+    # LL never wins: 0 turns LL off (one-shot from the first byte, here up to 32 KiB)
     for r in sweep:
         r["ll_us"] = 99
-    assert bench.size_table_row(2, sweep)["file_line"].startswith("2 - -")
+    assert bench.size_table_row(2, sweep)["file_line"] == "2 0 - 32K"
+    # a column the sweep did not measure: '-' keeps the built-in value
+    for r in sweep:
+        del r["ll_us"]
+    assert bench.size_table_row(2, sweep)["file_line"] == "2 - - 32K"
 
 
 def test_scale_decisions_tool_reads_bench_lines():
