@@ -46,6 +46,10 @@ ncclResult_t launchPlan(const LaunchPlan& p) {
     if (p.algo == ALGO_LL) {
       printf(" ops=%d grid=%d ranges=", p.ll.nOps, p.nChannels);
       for (int k = 0; k < p.ll.nOps; k++) printf("%s%d+%d", k ? "," : "", p.ll.ops[k].chOff, p.ll.ops[k].nch);
+      if (p.ll.nOps > 1) {  // per channel: the ops it runs (LLArgs::chMask)
+        printf(" masks=");
+        for (int c = 0; c < kMaxLLChannels; c++) printf("%s%x", c ? "," : "", p.ll.chMask[c]);
+      }
     } else if (p.batch.nOps > 1) {
       printf(" ops=%d grid=%d ranges=", p.batch.nOps, p.nChannels);
       for (int k = 0; k < p.batch.nOps; k++) printf("%s%d+%d", k ? "," : "", p.batch.chOff[k], p.batch.nch[k]);

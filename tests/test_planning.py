@@ -181,6 +181,8 @@ def batch(exe, n, *ops, **env):
             continue
         d = dict(t.split("=") for t in line.split())
         d["ranges"] = [tuple(int(x) for x in r.split("+")) for r in d["ranges"].split(",")]
+        if "masks" in d:
+            d["masks"] = [int(m, 16) for m in d["masks"].split(",")]
         d["ops"], d["grid"] = int(d["ops"]), int(d["grid"])
         launches.append(d)
     return launches
@@ -202,6 +204,23 @@ def test_group_batches_by_kernel_type_and_operator(exe):
         if sum(nch for _, nch in l["ranges"]) <= l["grid"]:
             used = [c for off, nch in l["ranges"] for c in range(off, off + nch)]
             assert len(used) == len(set(used)), l
+
+
+def test_ll_batch_channel_masks(exe):
+    """An LL batch's per-channel op masks (LLArgs::chMask, launchBatch) say exactly which ops each channel runs: bit k
+    of channel c is set iff c is in op k's range (mod the 32 LL channels), wrap-around included, and no channel
+    outside the grid has work."""
+    for n, ops in ((2, ["ar:7:100", "ar:7:20000", "rs:7:9000", "ag:7:3000", "ar:7:1"] * 4),
+                   (8, ["ar:7:100"] * 32), (4, ["ar:9:20000", "ar:9:12", "ar:9:30000"] * 3)):
+        ll = [l for l in batch(exe, n, *ops) if l["algo"] == "ll" and l["ops"] > 1]
+        assert ll, (n, ops)
+        for l in ll:
+            want = [0] * 32
+            for k, (off, nch) in enumerate(l["ranges"]):
+                for j in range(nch):
+                    want[(off + j) % 32] |= 1 << k
+            assert l["masks"] == want, l
+            assert all(m == 0 for m in l["masks"][l["grid"]:]), l
 
 
 def test_group_batch_limits_and_opt_out(exe):
