@@ -271,21 +271,21 @@ bool loadSizeTable(CommTuning* t, const char* path) {
 
 // CU budget of the large staged and zero-copy plans at n >= 3 (reference: channels and threads shrink below
 // saturation, enqueue.cc:2091-2105; tuning.cc:243-400). The links bound those plans on the 8-GPU node: a rank
-// sends 2S/n over each of its n-1 links, taking 2S/n / B_link, while its local HBM moves (2 + 4(n-1)/n) S
-// (staged path), so keeping the links busy takes (3n - 2) B_link of HBM copy traffic, and a
-// workgroup copies at most R_cu ≈ 50 GB/s (profiles/r02_wg_rate_probe.txt; a local-copy rate, an upper bound for
-// remote stores). With B_link = 76.8 GB/s per direction (153.6 GB/s per link read as bidirectional)
-// and 2x headroom, rounded up to a power of two (>= 32): 32 channels at n = 3..4, 64 at n = 5..7, 128 at n = 8 —
-// the rest of the chip stays free for the compute a collective overlaps. n = 2 keeps every channel (one link,
-// nothing to overlap in the bench). NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS / config.maxCTAs overrule it, as does
-// NCCL_AMD_LINK_CHANNELS (0 = no budget). The (3n - 2) factor is the push gather's HBM bytes; the pull gather (the
-// default since round 5) moves (2.5n - 1) B_link's worth, so the budget keeps ≥ 20 % more headroom than it states —
-// deliberately, until the 8-GPU tuning matrix measures R_cu for link traffic (the one-GPU loopback fan-out measures
-// ≈ 23 GB/s written + 23 GB/s read per workgroup = the 50 GB/s above, gpurun_out r05 xgmi_probe loopback).
+// sends 2S/n over each of its n-1 links, taking 2S/n / B_link, while its local HBM moves (3 + 2(n-1)/n) S (staged
+// path with the pull gather), so keeping the links busy takes (2.5n - 1) B_link of HBM traffic. A
+// workgroup of the staged kernel sustains R_wg ≈ 23 GB/s of it (n = 4 rehearsal, 4 ranks x 32 channels = 128
+// workgroups each on its own CU, far from the HBM limit: 4 x 4.5 S = 4.83 GB in 1.609 ms; the handshakes and the
+// fold's several sources halve the pure-copy rate of ≈ 40-50 GB/s per workgroup, profiles/r02_wg_rate_probe.txt).
+// With B_link = 76.8 GB/s per direction (153.6 GB/s per link read as bidirectional) and 2x headroom,
+// rounded up to a power of two (>= 32): 64 channels at n = 3..4, 128 at n = 5..8 — the rest of the chip stays free
+// for the compute a collective overlaps. n = 2 keeps every channel (one link, nothing to overlap in the bench).
+// NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS / config.maxCTAs overrule it, as does NCCL_AMD_LINK_CHANNELS (0 = no budget).
+// (Round 4's budget priced a workgroup at the pure-copy rate, 50 GB/s, and gave 32 channels at n = 3..4: its 2x
+// headroom was the staged kernel's own factor of 2, none left for remote-store latency.)
 int linkChannelBudget(int n) {
   if (n < 3) return 0;
-  const double bLinkGBps = 76.8, cuGBps = 50.0, headroom = 2.0;
-  const double need = (3.0 * n - 2.0) * bLinkGBps / cuGBps * headroom;
+  const double bLinkGBps = 76.8, wgGBps = 23.0, headroom = 2.0;
+  const double need = (2.5 * n - 1.0) * bLinkGBps / wgGBps * headroom;
   int c = 32;
   while (c < need && c < NCCL_AMD_MAX_CHANNELS) c *= 2;
   return c;

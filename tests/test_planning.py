@@ -267,11 +267,11 @@ def test_ll128_class_protocol(exe):
         assert (p["nch"] - 1) * p["part"] < lines <= p["nch"] * p["part"]
 
 
-@pytest.mark.parametrize("n,want", [(2, 256), (3, 32), (4, 32), (5, 64), (7, 64), (8, 128)])
+@pytest.mark.parametrize("n,want", [(2, 256), (3, 64), (4, 64), (5, 128), (7, 128), (8, 128)])
 def test_link_channel_budget(exe, n, want):
     """large staged plans at n >= 3 take a CU budget from the link cost model
-    (enqueue.cc linkChannelBudget: (3n-2) x 76.8 GB/s of HBM copy traffic / 50 GB/s per workgroup x 2, rounded
-    up to a power of two >= 32) instead of every channel; n = 2 keeps all of them."""
+    (enqueue.cc linkChannelBudget: (2.5n-1) x 76.8 GB/s of HBM traffic / 23 GB/s per staged-kernel workgroup x 2,
+    rounded up to a power of two >= 32) instead of every channel; n = 2 keeps all of them."""
     assert plan(exe, n, "ar", 7, (256 << 20) // 4)["nch"] == want
     if n >= 3:
         assert plan(exe, n, "rs", 9, (1 << 30) // 2 // n)["nch"] == want        # C3's ReduceScatter
@@ -381,8 +381,8 @@ def test_reference_partition_is_clamped_and_decoupled(exe, built):
             assert p["nch"] == p["refnch"] * p["sub"] and 1 <= p["nch"] <= 256
             ck = min(p["chunk"], -(-(max(p["cbdlo"], p["part"], p["cbdhi"]) // 1) // n))
             assert p["sub"] == 1 or -(-ck // p["sub"]) * 4 >= (16 << 10) - 16, (count, n, p)
-            if n >= 3:  # the CU budget of the default plan at n >= 3 (linkChannelBudget: 32 at n = 3, 128 at n = 8)
-                assert p["nch"] <= max({3: 32, 8: 128}[n], p["refnch"])
+            if n >= 3:  # the CU budget of the default plan at n >= 3 (linkChannelBudget: 64 at n = 3, 128 at n = 8)
+                assert p["nch"] <= max({3: 64, 8: 128}[n], p["refnch"])
 
 
 def test_size_table_file(exe, tmp_path):
