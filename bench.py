@@ -106,6 +106,9 @@ def _time_ms(fn, stream, iters: int, warmup: int = 3, align=None) -> float:
     skew (hundreds of us after a gloo exchange) is timed as if it were the collective's (28 us "per call" for
     4 KiB AllReduces that take 4.5 us)."""
     import torch
+    if align is not None:  # every rank's earlier kernels are done before any rank launches this measurement's
+        torch.cuda.synchronize()
+        align()
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -409,15 +412,22 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
                 os.environ[k] = v
         times = [[] for _ in envs]
         same = [True] * len(envs)
+        errors = [None] * len(envs)
         ref = None
         for rep in range(reps):
             for j in range(len(envs)):
                 i = (j + rep) % len(envs)
                 cm = comms[i]
                 trace(f"staged_tuning rep {rep} {envs[i] or 'default'}")
+                ys.fill_(float("nan"))  # a launch that does no work (an aborted communicator) cannot pass the check
                 ms = tmax(_tm(lambda: cm.all_reduce_raw(xs.data_ptr(), ys.data_ptr(), c, 7, 0, sp), stream, 10))
                 torch.cuda.synchronize()
                 times[i].append(ms)
+                err = cm.async_error()
+                if err:
+                    errors[i] = errors[i] or f"async error {err} in round {rep}"
+                    print(f"[rank {rank}] staged_tuning {envs[i] or 'default'} round {rep}: async error {err}",
+                          file=sys.stderr, flush=True)
                 if i == 0 and ref is None:
                     ref = ys.clone()
                 elif ref is not None:
@@ -428,7 +438,8 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
             tuning.append({"env": env or "default", "ms": round(med, 4), "ms_min": round(min(times[i]), 4),
                            "ms_max": round(max(times[i]), 4), "reps": len(times[i]),
                            "busbw_GBps": round(S / (med * 1e-3) / 1e9 * bus_factor("allreduce", n), 2),
-                           "check": "pass (= default, bitwise)" if agree(same[i]) else "FAIL"})
+                           "check": "pass (= default, bitwise)" if agree(same[i] and errors[i] is None) else
+                                    f"FAIL ({errors[i] or 'results differ from the default column, or an async error on another rank'})"})
         torch.cuda.synchronize()
         for cm in comms:
             cm.destroy()
