@@ -106,7 +106,9 @@ def _time_ms(fn, stream, iters: int, warmup: int = 3, align=None) -> float:
     skew (hundreds of us after a gloo exchange) is timed as if it were the collective's (28 us "per call" for
     4 KiB AllReduces that take 4.5 us)."""
     import torch
-    if align is not None:  # every rank's earlier kernels are done before any rank launches this measurement's
+    # every rank's earlier kernels are done before any rank launches this measurement's (BENCH_NO_LINEUP=1 skips it:
+    # the check that the library's co-residency cap alone keeps ranks sharing a GPU from stalling, DESIGN.md §7.2)
+    if align is not None and not os.environ.get("BENCH_NO_LINEUP"):
         torch.cuda.synchronize()
         align()
     for _ in range(warmup):

@@ -209,6 +209,18 @@ struct RegHandle {  // what ncclCommRegister returns
   RegAlloc* ra;  // nullptr when registration is disabled (NCCL_LOCAL_REGISTER=0)
 };
 
+enum CollFunc { FUNC_ALLREDUCE = 0, FUNC_REDUCESCATTER = 1, FUNC_ALLGATHER = 2, FUNC_REDUCE = 3, FUNC_COUNT = 4 };
+
+// One collective's NCCL_ALGO / NCCL_PROTO enables (reference: the algoEnable / protoEnable rows of
+// src/graph/tuning.cc:442-462), resolved onto this engine's kernels by loadTuning (enqueue.cc resolveFuncTuning).
+struct FuncTuning {
+  int algo;                 // TuneAlgoForce: exactly one implemented algorithm enabled forces it
+  int oneShotOk, directOk;  // FORCE_NONE: which SIMPLE kernels the size table may pick
+  int noAlgo;               // no enabled algorithm exists here: the collective fails (reference enqueue.cc:2052-2065)
+  int llOn, simpleOn;       // protocols
+  int ll128On;              // the LL64 line protocol (kernels.h): named in NCCL_PROTO, or NCCL_AMD_LL128=1
+};
+
 // Hot-path tuning knobs, read ONCE at communicator init (reference NCCL_PARAM caches its env reads,
 // include/param.h:21-31) and agreed across ranks (rank 0's values win), so every rank takes the same
 // algorithm/protocol decision and no getenv() runs per collective.
@@ -218,10 +230,9 @@ struct CommTuning {
   int protoFlags;           // NCCL_AMD_PROTO_FLAGS | (no release fence before data flags ? 8 : 0) | pulls
   int p2pFence;             // NCCL_AMD_P2P_FENCE: 1 fence, 0 none, -1 unset (none iff all ranks share one GPU)
   int linkChannels;         // channel budget of large plans at n >= 3 (enqueue.cc linkChannelBudget; 0 = none)
-  int algo;                 // NCCL_ALGO: TuneAlgoForce (ONESHOT, DIRECT, RING, TREE)
-  int llOn, simpleOn;       // NCCL_PROTO
-  int ll128On;              // NCCL_PROTO lists LL128, or NCCL_AMD_LL128=1: the LL64 line protocol (kernels.h)
-  int symDisable;           // NCCL_AMD_SYM_DISABLE
+  FuncTuning fn[FUNC_COUNT];  // NCCL_ALGO / NCCL_PROTO per collective (reference grammar, enqueue.cc parseEnableList)
+  int parseError;           // nonzero: NCCL_ALGO / NCCL_PROTO did not parse; every rank's init fails (ncclInvalidUsage)
+  int symDisable;          // NCCL_AMD_SYM_DISABLE
   int symOneShot;           // NCCL_AMD_SYM_ONESHOT: caller promises out-of-place window AllReduces
   int symWtPublish;         // NCCL_AMD_SYM_WT: symmetric kernels publish with write-through stores, no L2 write-back
   int localRegister;        // NCCL_LOCAL_REGISTER: ncclCommRegister maps buffers into peers (zero-copy collectives)
@@ -254,6 +265,7 @@ void loadTuning(CommTuning* t);  // enqueue.cc
 bool loadSizeTable(CommTuning* t, const char* path);
 void resolveFence(CommTuning* t, bool oneDevice);  // enqueue.cc: the fence default, once devices are known
 int linkChannelBudget(int nranks);                  // enqueue.cc: CU budget of large n >= 3 plans
+int coResidentChannelCap(int minCUs, int ranksPerGpu);  // enqueue.cc: channels that stay co-resident per launch
 void resolveLinkChannels(CommTuning* t, int nranks, bool userMaxCTAs);
 
 struct ncclCommImpl;
@@ -376,8 +388,6 @@ ncclResult_t transportRemapPeer(ncclComm* comm, int r);
 ncclResult_t launchMapCheck(const DevComm* dc, const MapCheckArgs& a, uint64_t* out, hipStream_t stream);  // kernels.hip
 
 // ---------------------------------------------------------------- enqueue (reference src/enqueue.cc)
-enum CollFunc { FUNC_ALLREDUCE = 0, FUNC_REDUCESCATTER = 1, FUNC_ALLGATHER = 2, FUNC_REDUCE = 3 };
-
 struct CollInfo {  // reference: struct ncclInfo, src/include/info.h:17-41
   CollFunc func;
   const char* opName;

@@ -209,5 +209,14 @@ __host__ __device__ inline uint64_t flagIndex(int c, int kind, int from) {
 __host__ __device__ inline uint64_t ctrIndex(int c, int kind, int peer) {
   return ((uint64_t)c * CTR_KINDS + kind) * NCCL_AMD_MAX_RANKS + peer;
 }
+// The k-th peer (k = 1 .. n-1) that channel c of rank `me` visits in a workgroup-wide multi-peer loop: the
+// staged scatter's pushes, the pull gather's reads, the zero-copy kernels' reads. Rotated by channel: with one
+// order on every channel, all of a rank's channels would sit on the SAME peer's xGMI link at step position k;
+// rotated, any n-1 consecutive channels put position k on all n-1 peers once (a Latin square), and for a fixed
+// (c, k) the ranks' choices are a shift, so every peer is also the source / target of exactly one rank.
+// Data placement and fold order never depend on it (tests/native/plan_test `peers`).
+__host__ __device__ inline int chanPeer(int me, int n, int c, int k) {
+  return (me + 1 + (k - 1 + c) % (n - 1)) % n;
+}
 
 }  // namespace ncclamd

@@ -79,6 +79,106 @@ static ncclResult_t hostToDevRedOp(ncclComm* comm, ncclRedOp_t op, ncclDataType_
   }
 }
 
+// ---- NCCL_ALGO / NCCL_PROTO (reference src/graph/tuning.cc:36-136 parseList, :440-462; names src/init.cc:52-55).
+// "[func:]list[;func:list]...": a list of names separated by commas, or "^list" for all but those; an entry without a
+// function prefix applies to every function and may only come first; names and prefixes match case-insensitively;
+// an unknown name or prefix fails init with ncclInvalidUsage. The algorithm names are the reference's plus this
+// engine's OneShot and Direct. One deviation: "^" re-enables the unlisted names at their DEFAULTS, where the
+// reference writes 1 — the same for every name but LL128, whose default here is the engine's gate (NCCL_AMD_LL128,
+// off until 64-byte lines are shown whole over xGMI), as the reference's 2 is its topology gate (tuning.cc:446,
+// 518-536): naming LL128 enables it, excluding every other protocol leaves it on as the only one.
+namespace {
+constexpr int kRefFuncs = 5, kAlgoNames = 9, kProtoNames = 3;
+enum { PROTO_LL = 0, PROTO_LL128 = 1, PROTO_SIMPLE = 2 };
+enum { ALG_TREE = 0, ALG_RING = 1, ALG_ONESHOT = 7, ALG_DIRECT = 8 };
+const char* const kRefFuncName[kRefFuncs] = {"Broadcast", "Reduce", "AllGather", "ReduceScatter", "AllReduce"};
+const char* const kAlgoName[kAlgoNames] = {"Tree", "Ring", "CollNetDirect", "CollNetChain", "NVLS", "NVLSTree", "PAT",
+                                           "OneShot", "Direct"};
+const char* const kProtoName[kProtoNames] = {"LL", "LL128", "Simple"};
+const int kRefFuncOf[FUNC_COUNT] = {4, 3, 2, 1};  // CollFunc -> the reference's ncclFunc_t row
+const char* const kForceName[] = {"", "OneShot", "Direct", "Ring", "Tree"};
+
+// the non-empty pieces of s between separators, each with its offset (strtok_r's tokens)
+std::vector<std::pair<size_t, std::string>> tokens(const std::string& s, char sep) {
+  std::vector<std::pair<size_t, std::string>> out;
+  for (size_t pos = 0; pos <= s.size();) {
+    size_t e = s.find(sep, pos);
+    if (e == std::string::npos) e = s.size();
+    if (e > pos) out.push_back({pos, s.substr(pos, e - pos)});
+    pos = e + 1;
+  }
+  return out;
+}
+}  // namespace
+
+// list: [kRefFuncs][nnames] enables, holding the defaults on entry (a "^" entry restores them, see above)
+static ncclResult_t parseEnableList(const char* var, const char* str, const char* const* names, int nnames, int* list) {
+  std::vector<int> defaults(list, list + nnames);  // row 0 = every row's default
+  for (const auto& entry : tokens(str, ';')) {
+    const auto parts = tokens(entry.second, ':');
+    std::string prefix, elems;
+    if (parts.size() >= 2) {
+      prefix = parts[0].second;
+      elems = parts[1].second;
+    } else if (parts.size() == 1) {
+      if (entry.first != 0) {  // every function before it would be overwritten
+        WARN("%s: all entries except the first must have a prefix: \"%s\"", var, str);
+        return ncclInvalidUsage;
+      }
+      elems = parts[0].second;
+    } else {
+      WARN("%s: empty entry in \"%s\"", var, str);
+      return ncclInvalidUsage;
+    }
+    const bool exclude = !elems.empty() && elems[0] == '^';
+    if (exclude) elems.erase(0, 1);
+    std::vector<int> row(nnames);
+    for (int e = 0; e < nnames; e++) row[e] = exclude ? defaults[e] : 0;
+    for (const auto& tok : tokens(elems, ',')) {
+      int e = 0;
+      while (e < nnames && strcasecmp(tok.second.c_str(), names[e]) != 0) e++;
+      if (e == nnames) {
+        WARN("%s: unrecognized element token \"%s\" when parsing \"%s\"", var, tok.second.c_str(), str);
+        return ncclInvalidUsage;
+      }
+      row[e] = exclude ? 0 : 1;
+    }
+    bool found = false;
+    for (int f = 0; f < kRefFuncs; f++) {
+      if (!prefix.empty() && strcasecmp(prefix.c_str(), kRefFuncName[f]) != 0) continue;
+      found = true;
+      for (int e = 0; e < nnames; e++) list[f * nnames + e] = row[e];
+    }
+    if (!found) {
+      WARN("%s: unrecognized prefix token \"%s\" when parsing \"%s\"", var, prefix.c_str(), str);
+      return ncclInvalidUsage;
+    }
+  }
+  return ncclSuccess;
+}
+
+// One collective's enables onto this engine's kernels. Exactly one implemented algorithm enabled (OneShot, Direct,
+// Ring or Tree) forces it, as NCCL_ALGO=<name> always did here; several leave the choice to the size table, as the
+// reference's cost model chooses among the enabled ones, restricted to the kernels that stand in for them in the
+// tuner's cost table (tuner.cc: (TREE, SIMPLE) = one-shot, (RING, SIMPLE) = direct); none — only CollNet / NVLS /
+// PAT, absent from an xGMI mesh — or no protocol leaves the collective without an algorithm (it fails, as the
+// reference's does, enqueue.cc:2052-2065).
+static void resolveFuncTuning(const int* algoOn, const int* protoOn, int ll128Default, FuncTuning* ft) {
+  memset(ft, 0, sizeof(*ft));
+  ft->llOn = protoOn[PROTO_LL] != 0;
+  ft->simpleOn = protoOn[PROTO_SIMPLE] != 0;
+  ft->ll128On = protoOn[PROTO_LL128] == 2 ? (ll128Default != 0 || (!ft->llOn && !ft->simpleOn))
+                                          : protoOn[PROTO_LL128] != 0;
+  const int one = algoOn[ALG_ONESHOT] != 0, dir = algoOn[ALG_DIRECT] != 0, ring = algoOn[ALG_RING] != 0,
+            tree = algoOn[ALG_TREE] != 0;
+  const int impl = one + dir + ring + tree;
+  ft->algo = FORCE_NONE;
+  if (impl == 1) ft->algo = one ? FORCE_ONESHOT : dir ? FORCE_DIRECT : ring ? FORCE_RING : FORCE_TREE;
+  ft->oneShotOk = one || tree;
+  ft->directOk = dir || ring;
+  ft->noAlgo = impl == 0 || (!ft->llOn && !ft->simpleOn && !ft->ll128On);
+}
+
 void loadTuning(CommTuning* t) {
   memset(t, 0, sizeof(*t));
   t->checkPointers = (int)paramInt("NCCL_CHECK_POINTERS", 0);
@@ -96,37 +196,32 @@ void loadTuning(CommTuning* t) {
   // writes per reduced block). The scatter stays a push unless NCCL_AMD_RS_PULL=1 (no measured gain at n = 8).
   t->protoFlags = (int)paramInt("NCCL_AMD_PROTO_FLAGS", 0) | (t->p2pFence == 0 ? 8 : 0) |
                   (paramInt("NCCL_AMD_AG_PULL", 1) ? 16 : 0) | (paramInt("NCCL_AMD_RS_PULL", 0) ? 32 : 0);
-  if (const char* algo = paramStr("NCCL_ALGO")) {
-    if (!strcasecmp(algo, "ONESHOT")) t->algo = FORCE_ONESHOT;
-    else if (!strcasecmp(algo, "DIRECT")) t->algo = FORCE_DIRECT;
-    else if (!strcasecmp(algo, "RING")) t->algo = FORCE_RING;
-    else if (!strcasecmp(algo, "TREE")) t->algo = FORCE_TREE;
-    else WARN("NCCL_ALGO=%s: unknown here (ONESHOT, DIRECT, RING, TREE); using the size table", algo);
+  // NCCL_ALGO / NCCL_PROTO in the reference's grammar (parseEnableList below), one enable row per collective
+  int algoOn[kRefFuncs][kAlgoNames], protoOn[kRefFuncs][kProtoNames];
+  for (int f = 0; f < kRefFuncs; f++) {
+    for (int a = 0; a < kAlgoNames; a++) algoOn[f][a] = 1;
+    // LL128: 2 = this engine's default gate (the reference's 2 is its topology gate, tuning.cc:446, 518-536): the LL128
+    // class (LL64 lines, kernels.h ll64ChannelOp) is off unless NCCL_AMD_LL128=1 or NCCL_PROTO names it, until the
+    // 8-GPU suite's probe shows 64-byte lines arrive whole over xGMI
+    for (int p = 0; p < kProtoNames; p++) protoOn[f][p] = p == PROTO_LL128 ? 2 : 1;
   }
-  t->llOn = t->simpleOn = 1;
-  // LL128 class (LL64 lines, kernels.h ll64ChannelOp): off unless asked for, like the reference on paths
-  // whose 128-byte store atomicity is unproven (tuning.cc:518-536); the 8-GPU suite measures xGMI's
-  t->ll128On = (int)paramInt("NCCL_AMD_LL128", 0);
-  if (const char* proto = paramStr("NCCL_PROTO")) {  // reference syntax: "LL,Simple" or "^LL128"
-    bool exclude = proto[0] == '^';
-    bool hasLL = false, hasSimple = false, hasLL128 = false;
-    std::string list(proto + (exclude ? 1 : 0));
-    size_t pos = 0;
-    while (true) {
-      size_t comma = list.find(',', pos);
-      std::string tok = list.substr(pos, comma == std::string::npos ? std::string::npos : comma - pos);
-      hasLL |= !strcasecmp(tok.c_str(), "LL");
-      hasSimple |= !strcasecmp(tok.c_str(), "Simple");
-      hasLL128 |= !strcasecmp(tok.c_str(), "LL128");
-      if (comma == std::string::npos) break;
-      pos = comma + 1;
-    }
-    t->llOn = exclude ? !hasLL : hasLL;
-    t->simpleOn = exclude ? !hasSimple : hasSimple;
-    t->ll128On = exclude ? (t->ll128On && !hasLL128) : hasLL128;
-    if (!t->llOn && !t->simpleOn && !t->ll128On) {
-      WARN("NCCL_PROTO=%s leaves no protocol enabled; using Simple", proto);
-      t->simpleOn = 1;
+  const char* protoStr = paramStr("NCCL_PROTO");
+  const char* algoStr = paramStr("NCCL_ALGO");
+  t->parseError = 0;
+  if (protoStr && parseEnableList("NCCL_PROTO", protoStr, kProtoName, kProtoNames, &protoOn[0][0]) != ncclSuccess)
+    t->parseError = ncclInvalidUsage;
+  if (algoStr && parseEnableList("NCCL_ALGO", algoStr, kAlgoName, kAlgoNames, &algoOn[0][0]) != ncclSuccess)
+    t->parseError = ncclInvalidUsage;
+  const int ll128Default = (int)paramInt("NCCL_AMD_LL128", 0);
+  for (int f = 0; f < FUNC_COUNT; f++) resolveFuncTuning(algoOn[kRefFuncOf[f]], protoOn[kRefFuncOf[f]], ll128Default, &t->fn[f]);
+  if (algoStr || protoStr) {
+    for (int f = 0; f < FUNC_COUNT; f++) {
+      const FuncTuning& ft = t->fn[f];
+      INFO("NCCL_ALGO / NCCL_PROTO: %s: %s%s, protocols LL %d LL128 %d Simple %d", kRefFuncName[kRefFuncOf[f]],
+           ft.noAlgo ? "no algorithm available" : ft.algo != FORCE_NONE ? "forced " : "size table over",
+           ft.noAlgo ? "" : ft.algo != FORCE_NONE ? kForceName[ft.algo]
+                          : ft.oneShotOk && ft.directOk ? " one-shot, direct" : ft.oneShotOk ? " one-shot" : " direct",
+           ft.llOn, ft.ll128On, ft.simpleOn);
     }
   }
   t->symDisable = (int)paramInt("NCCL_AMD_SYM_DISABLE", 0);
@@ -178,7 +273,8 @@ void loadTuning(CommTuning* t) {
   // grains, LL / 2 in 16-byte grains, LL128 x 15/16 in 1920-byte grains (enqueue.cc:2222-2227, 2321; buffers
   // init.cc:810-827: 4 MiB, 8 x 512 x 8 x 16 B, 120 x 640 x 8 x 8 B). A chunk below one grain (which never
   // advances in the reference) is raised to one grain.
-  t->refProto = t->llOn && !t->simpleOn && !t->ll128On ? 0 : t->ll128On && !t->llOn && !t->simpleOn ? 1 : 2;
+  const FuncTuning& ar = t->fn[FUNC_ALLREDUCE];
+  t->refProto = ar.llOn && !ar.simpleOn && !ar.ll128On ? 0 : ar.ll128On && !ar.llOn && !ar.simpleOn ? 1 : 2;
   if (t->refProto == 2) {
     t->refChunkBytes = t->ringChunkBytes;
   } else if (t->refProto == 0) {
@@ -289,6 +385,25 @@ int linkChannelBudget(int n) {
   int c = 32;
   while (c < need && c < NCCL_AMD_MAX_CHANNELS) c *= 2;
   return c;
+}
+
+// Channels per launch that stay co-resident when several ranks share a GPU (NCCL_MULTI_RANK_GPU_ENABLE, the one-GPU
+// rehearsals). A channel spins on the same channel of every peer, so a collective progresses only while, for some
+// channel, every rank's workgroup is resident. A GPU holds 2 of these workgroups per CU (512 threads, 4 waves per
+// SIMD, kernels.h kCoResident). One rank per GPU runs one collective at a time there (stream order), so every channel
+// fits: 2 x CUs. Ranks SHARING a GPU are not in step: a fast rank launches its next collective (or the next on another
+// communicator from the same stream) while slow ranks still finish this one, so two generations of collectives are in
+// flight on the GPU — never three: a rank starting generation k+2 had its k+1 complete, which needed every rank's k+1
+// started, so every rank's k had completed (one stream per rank). The round-5 cap, 2 x CUs / ranks per GPU, fitted ONE
+// generation exactly (8 ranks x 64 = 512 slots): the fast ranks' next-generation workgroups, spinning on the slow
+// ranks' next generation, held slots the slow ranks' current-generation workgroups still waited for, and every rank
+// stalled until the spin timeout (the n = 8 rehearsal stall of round 5). Both generations fit with
+// CUs / ranks per GPU.
+int coResidentChannelCap(int minCUs, int ranksPerGpu) {
+  if (minCUs < 1) minCUs = 256;
+  if (ranksPerGpu < 1) ranksPerGpu = 1;
+  const int cap = ranksPerGpu == 1 ? 2 * minCUs : minCUs / ranksPerGpu;
+  return cap < 1 ? 1 : cap;
 }
 
 void resolveLinkChannels(CommTuning* t, int nranks, bool userMaxCTAs) {
@@ -483,10 +598,11 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   const size_t npk = (bytes + 7) / 8;
   const size_t nLines = (bytes + kLL64Payload - 1) / kLL64Payload;  // LL64 lines
   const CommTuning& t = comm->tune;
+  const FuncTuning& ft = t.fn[info.func];
   const bool blocked = info.func == FUNC_REDUCESCATTER || info.func == FUNC_ALLGATHER;
   const bool shape = !blocked || (bytes & 7) == 0;
-  const bool fits = t.llOn && shape && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
-  const bool fits64 = t.ll128On && shape && nLines <= (size_t)comm->llChannels * (comm->llBytes / 64);
+  const bool fits = ft.llOn && shape && npk <= (size_t)comm->llChannels * (comm->llBytes / 16);
+  const bool fits64 = ft.ll128On && shape && nLines <= (size_t)comm->llChannels * (comm->llBytes / 64);
   // a forced NCCL_ALGO (ONESHOT / DIRECT / RING / TREE) selects the SIMPLE-protocol kernels unless
   // NCCL_PROTO leaves only LL-class protocols enabled.
   // LL lines carry 2x the payload to each of the n-1 peers: its range shrinks with n like the one-shot's
@@ -495,9 +611,9 @@ bool llPlan(const CollInfo& info, LLOp* op) {
   // it, so the LL128 class takes the next range (default up to 1 MiB / n) before one-shot / direct.
   const size_t llLim = t.llBytes > 0 ? (size_t)t.llBytes : (size_t)t.tableLL[n];
   const size_t ll64Lim = t.ll128Bytes > 0 ? (size_t)t.ll128Bytes : (size_t)t.tableLL128[n];
-  const bool sized = t.algo == FORCE_NONE;
+  const bool sized = ft.algo == FORCE_NONE;
   int proto = -1;
-  if (!t.simpleOn) {  // only LL-class protocols enabled: the range's protocol, else whichever fits
+  if (!ft.simpleOn) {  // only LL-class protocols enabled: the range's protocol, else whichever fits
     if (fits && (bytes <= llLim || !fits64)) proto = LLP_LL;
     else if (fits64) proto = LLP_LL64;
   } else if (fits && sized && bytes <= llLim) {
@@ -591,6 +707,13 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     return ncclSuccess;
   }
 
+  const FuncTuning& ft = comm->tune.fn[info.func];
+  if (ft.noAlgo) {  // reference enqueue.cc:2052-2065 (ncclInvalidUsage when NCCL_ALGO / NCCL_PROTO caused it)
+    WARN("No algorithm/protocol available for function %s with datatype %d. NCCL_ALGO was set to %s. NCCL_PROTO was "
+         "set to %s.", info.opName, (int)info.datatype, paramStr("NCCL_ALGO") ? paramStr("NCCL_ALGO") : "(unset)",
+         paramStr("NCCL_PROTO") ? paramStr("NCCL_PROTO") : "(unset)");
+    return ncclInvalidUsage;
+  }
   p.algo = ALGO_DIRECT;
   const uint64_t epp = 16 / ts;
   size_t count = info.count;
@@ -632,15 +755,16 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     // profiles/r02_scale_rehearsal_n2_onegpu.json)
     size_t bytes = count * (size_t)ts;
     size_t lim = comm->tune.oneShotBytes > 0 ? (size_t)comm->tune.oneShotBytes : (size_t)comm->tune.tableOneShot[n];
-    oneShot = comm->tune.algo == FORCE_ONESHOT || (comm->tune.algo == FORCE_NONE && bytes <= lim);
+    // several algorithms enabled: the size table, over the SIMPLE kernels they leave (resolveFuncTuning)
+    oneShot = ft.algo == FORCE_ONESHOT || (ft.algo == FORCE_NONE && ft.oneShotOk && (bytes <= lim || !ft.directOk));
   }
   // NCCL_AMD_REF_ORDER: AllReduce always on the direct kernel in the reference's partition (below)
-  const bool refOrder = comm->tune.refOrder && info.func == FUNC_ALLREDUCE && comm->tune.algo != FORCE_RING &&
-                        comm->tune.algo != FORCE_TREE;
+  const bool refOrder = comm->tune.refOrder && info.func == FUNC_ALLREDUCE && ft.algo != FORCE_RING &&
+                        ft.algo != FORCE_TREE;
   if (refOrder) oneShot = false;
   // NCCL_ALGO=RING with NCCL_PROTO naming LL or LL128 alone: the reference's RING/LL or RING/LL128 AllReduce, i.e.
   // the ring kernel on that protocol's partition (ringParts), not this engine's LL kernel (another fold order)
-  const bool ringProtoPart = info.func == FUNC_ALLREDUCE && comm->tune.algo == FORCE_RING && comm->tune.refProto != 2;
+  const bool ringProtoPart = info.func == FUNC_ALLREDUCE && ft.algo == FORCE_RING && comm->tune.refProto != 2;
   int tunedNch = 0;
   if (comm->tunerLoaded) {  // external tuner plugin: one-shot (TREE/SIMPLE) vs direct (RING/SIMPLE), channels
     int tuned = TUNE_DEFAULT;
@@ -667,8 +791,8 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
   // The reference's own algorithms, forced with NCCL_ALGO=RING / TREE (pipe.h): the ring for AllReduce,
   // ReduceScatter and AllGather, the chain (the intra-node tree) for AllReduce; Reduce's ring is the chain
   // to the root (reduce.h). Where the reference has no such algorithm the default plan runs, with a warning.
-  if (comm->tune.algo == FORCE_RING || comm->tune.algo == FORCE_TREE) {
-    const bool ring = comm->tune.algo == FORCE_RING;
+  if (ft.algo == FORCE_RING || ft.algo == FORCE_TREE) {
+    const bool ring = ft.algo == FORCE_RING;
     int kind = -1;
     if (info.func == FUNC_ALLREDUCE) kind = ring ? PIPE_RING_AR : PIPE_CHAIN_AR;
     else if (ring) kind = info.func == FUNC_REDUCESCATTER ? PIPE_RING_RS : info.func == FUNC_ALLGATHER ? PIPE_RING_AG

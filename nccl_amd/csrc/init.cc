@@ -139,8 +139,8 @@ static ncclResult_t fillPeerInfo(ncclComm* comm, PeerInfo* p) {
 
 // Channels of one launch must all be resident at once on every GPU (a channel spins on the same
 // channel of its peers). With several ranks on one GPU (NCCL_MULTI_RANK_GPU_ENABLE / test boxes) the
-// launches share the CUs, so cap channels at 2 workgroups per CU divided by the most ranks any device
-// hosts. Every rank computes this from the same peer table, so all agree.
+// launches share the CUs, and two generations of them can be in flight (enqueue.cc coResidentChannelCap).
+// Every rank computes this from the same peer table, so all agree.
 static void computeChannelCap(ncclComm* c) {
   int minCU = 1 << 30, maxPer = 1;
   for (size_t i = 0; i < c->peers.size(); i++) {
@@ -150,8 +150,7 @@ static void computeChannelCap(ncclComm* c) {
     if (c->peers[i].numCUs > 0 && c->peers[i].numCUs < minCU) minCU = c->peers[i].numCUs;
   }
   if (minCU == (1 << 30)) minCU = 256;
-  int cap = 2 * minCU / maxPer;
-  if (cap < 1) cap = 1;
+  const int cap = coResidentChannelCap(minCU, maxPer);
   c->chanCap = cap < c->maxChannels ? cap : c->maxChannels;
   bool oneDevice = true;
   for (size_t i = 1; i < c->peers.size(); i++) oneDevice = oneDevice && !strcmp(c->peers[i].busId, c->peers[0].busId);
@@ -201,6 +200,14 @@ static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id
     std::vector<ShapeInfo> shapes(nranks);
     shapes[rank] = {comm->maxChannels, comm->minCTAs, comm->nSlots, comm->slotBytes, comm->tune};
     if ((res = bootstrapAllGather(comm->bootstrap, shapes.data(), sizeof(ShapeInfo))) != ncclSuccess) goto fail;
+    // NCCL_ALGO / NCCL_PROTO that did not parse on ANY rank fail every rank's init (reference: parseList's
+    // ncclInvalidUsage out of ncclTopoTuneModel, src/graph/tuning.cc:456-461), so no rank is left waiting
+    for (int r = 0; r < nranks; r++)
+      if (shapes[r].tune.parseError) {
+        WARN("rank %d: NCCL_ALGO / NCCL_PROTO could not be parsed on rank %d", rank, r);
+        res = ncclInvalidUsage;
+        goto fail;
+      }
     comm->maxChannels = comm->maxCTAs = shapes[0].maxChannels;
     comm->nSlots = shapes[0].nSlots;
     comm->slotBytes = shapes[0].slotBytes;
@@ -397,6 +404,10 @@ NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
     int d = devlist ? devlist[i] : i;
     cs[i] = new ncclComm();
     commDefaults(cs[i], i, ndev, d, nullptr);
+    if (cs[i]->tune.parseError) {  // NCCL_ALGO / NCCL_PROTO (reference tuning.cc:456-461)
+      res = ncclInvalidUsage;
+      break;
+    }
     res = transportSetup(cs[i]);
     if (res == ncclSuccess) res = fillPeerInfo(cs[i], &infos[i]);
   }

@@ -749,10 +749,9 @@ struct Channel {
     off = g.off + (uint64_t)l * g.loop + bb + lo;
     len = hi - lo;
   }
-  // k-th peer (k = 1..n-1) this channel sends to. Staggered by channel: every channel starting with the
-  // same peer would put all of a rank's scatter traffic on ONE xGMI link at a time; rotating the start
-  // spreads the channels evenly over the n-1 links (data placement and fold order are unaffected).
-  __device__ int peerAt(int k) const { return (me + 1 + (k - 1 + c) % (n - 1)) % n; }
+  // k-th peer (k = 1..n-1) this channel sends to (scatter) or reads from (pull gather), staggered by channel
+  // (chanPeer, device_abi.h): all of a rank's channels on ONE xGMI link at a time otherwise.
+  __device__ int peerAt(int k) const { return chanPeer(me, n, c, k); }
   __device__ const uint64_t* myFlags(int kind) const { return dc.flags[me] + flagIndex(c, kind, 0); }
   __device__ bool pushesTo(int p) const {
     if (kAR || COLL == COLL_AG) return true;
@@ -959,8 +958,10 @@ struct Channel {
     if (tid < NCCL_AMD_MAX_RANKS) sh.want[tid] = (tid < n && tid != me) ? ctr(recvKind, tid) + 1 : 0;
     __syncthreads();
     if (!waitAll<PROBE_STAGED>(dc, sh.st, myFlags(agPull ? FLG_PULL_READY : FLG_AG_READY), sh.want, !noAcq, &sh.probe)) return false;
+    // peers in the channel-rotated order: copyRange is workgroup-wide, so one order on every
+    // channel would pull from one owner at a time — one incoming link of n-1 — while all channels move in step
     for (int k = 1; k < n; k++) {
-      int q = (me + n - k) % n;
+      const int q = peerAt(k);
       const int b = blockOf(q);  // the block rank q owns (its index shifts past the root when rootless)
       uint64_t off, len;
       blockSlice(step, b, off, len);
@@ -1685,7 +1686,7 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
   if (ok && (COLL == SYM_AR || COLL == SYM_AG)) {
     // pull every other rank's block part from its output (AR: its reduced block; AG: its input block)
     for (int k = 1; k < n; k++) {
-      const int q = (me + n - 1 - (k - 1 + c) % (n - 1)) % n;  // staggered by channel: all links busy
+      const int q = chanPeer(me, n, c, k);  // staggered by channel: all links busy
       uint64_t lo, hi;
       partOf(blockLen(q), lo, hi);
       const uint64_t off = ((uint64_t)q * a.chunk + lo) * ts;
@@ -1848,6 +1849,7 @@ inline ncclResult_t launchTyped(const LaunchPlan& p) {
       if (p.algo == ALGO_LL) launchLL<T, 0>(p);
       else launchColl<T, 0, COLL_AG>(p);
       break;
+    default: return ncclInternalError;
   }
   HIPCHECK(hipGetLastError());
   return ncclSuccess;

@@ -60,14 +60,15 @@ def _env_int(name: str, default: int) -> int:
 def ring_channels(n: int, ranks_per_gpu: int | None = None) -> int:
     """The channel count K a NCCL_ALGO=RING / NCCL_AMD_REF_ORDER AllReduce is planned on (enqueue.cc
     refChannelCount): NCCL_AMD_REF_NCHANNELS when set, else the communicator's co-resident channel cap —
-    NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS (default 256) capped at 2 workgroups per CU divided by the ranks per GPU
-    (init.cc computeChannelCap; every test rank shares the box's one GPU) — and at most the reference's
-    MAXCHANNELS = 64 (src/include/device.h:91) and the channel cap."""
+    NCCL_MAX_CTAS / NCCL_MAX_NCHANNELS (default 256) capped at 2 workgroups per CU for one rank per GPU, at CUs
+    divided by the ranks per GPU when they share one (enqueue.cc coResidentChannelCap; every test rank shares the box's
+    one GPU) — and at most the reference's MAXCHANNELS = 64 (src/include/device.h:91) and the channel cap."""
     import torch
     cap = _env_int("NCCL_MAX_CTAS", _env_int("NCCL_MAX_NCHANNELS", 256))
     cap = max(1, min(cap, 256))
     cus = torch.cuda.get_device_properties(0).multi_processor_count
-    cap = max(1, min(cap, 2 * cus // (ranks_per_gpu or n)))
+    rpg = ranks_per_gpu or n
+    cap = max(1, min(cap, 2 * cus if rpg == 1 else cus // rpg))
     k = _env_int("NCCL_AMD_REF_NCHANNELS", 0) or cap
     return max(1, min(k, 64, cap))  # every part needs a workgroup: never more parts than the channel cap
 
@@ -106,8 +107,8 @@ def ref_proto() -> tuple[int, int]:
         excl = proto.startswith("^")
         toks = {t.strip().lower() for t in proto.lstrip("^").split(",")}
         on = {k: ((k not in toks) and (on[k] if k == "ll128" else True)) if excl else (k in toks) for k in on}
-        if not any(on.values()):
-            on["simple"] = True
+        if excl and not on["ll"] and not on["simple"] and "ll128" not in toks:
+            on["ll128"] = True  # LL128 at its gate is on when it is the only protocol left (enqueue.cc resolveFuncTuning)
     if on["ll"] and not on["simple"] and not on["ll128"]:
         return oracle.PROTO_LL, _env_int("NCCL_LL_BUFFSIZE", 0)
     if on["ll128"] and not on["ll"] and not on["simple"]:

@@ -82,6 +82,35 @@ void ipcDrainReleases() {}
 using namespace ncclamd;
 
 int main(int argc, char** argv) {
+  if (argc == 4 && !strcmp(argv[1], "peers")) {
+    // the kernels' per-channel peer order (device_abi.h chanPeer): one line "me c p(1) ... p(n-1)" per (rank, channel)
+    const int n = atoi(argv[2]), K = atoi(argv[3]);
+    for (int me = 0; me < n; me++)
+      for (int c = 0; c < K; c++) {
+        printf("%d %d", me, c);
+        for (int k = 1; k < n; k++) printf(" %d", chanPeer(me, n, c, k));
+        printf("\n");
+      }
+    return 0;
+  }
+  if (argc == 4 && !strcmp(argv[1], "cap")) {  // the co-residency channel cap for (CUs, ranks per GPU)
+    printf("%d\n", coResidentChannelCap(atoi(argv[2]), atoi(argv[3])));
+    return 0;
+  }
+  if (argc == 2 && !strcmp(argv[1], "matrix")) {
+    // NCCL_ALGO / NCCL_PROTO as loadTuning resolves them: "parse=<ncclResult_t>", then one line per collective
+    CommTuning t;
+    loadTuning(&t);
+    printf("parse=%d\n", t.parseError);
+    const char* fn[] = {"allreduce", "reducescatter", "allgather", "reduce"};
+    const char* force[] = {"none", "oneshot", "direct", "ring", "tree"};
+    for (int f = 0; f < FUNC_COUNT; f++) {
+      const FuncTuning& ft = t.fn[f];
+      printf("func=%s algo=%s oneshot=%d direct=%d noalgo=%d ll=%d ll128=%d simple=%d\n", fn[f], force[ft.algo],
+             ft.oneShotOk, ft.directOk, ft.noAlgo, ft.llOn, ft.ll128On, ft.simpleOn);
+    }
+    return 0;
+  }
   if (argc < 5) {
     fprintf(stderr, "usage: plan_test NRANKS FUNC DTYPE COUNT [ALIGN_OFFSET] [CHANCAP]\n");
     return 2;
