@@ -23,7 +23,7 @@ DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
 all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test mapcheck-test xgmi-probe atomicity-probe \
-     fp8-probe
+     fp8-probe release-probe reuse-probe
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -170,3 +170,20 @@ tests/native/mapcheck_test: tests/native/mapcheck_test.cc $(SRCDIR)/mapcheck.cc 
 	  $(SRCDIR)/mapcheck.cc $(SRCDIR)/debug.cc -lpthread
 
 .PHONY: mapcheck-test
+
+# does unmapping an imported dma-buf mapping wait for the device? (decides where peers' mappings are released,
+# DESIGN.md §3.2)
+release-probe: tests/native/release_probe
+
+tests/native/release_probe: tests/native/release_probe.hip
+	$(HIPCC) -O2 --offload-arch=$(ARCH) -o $@ $<
+
+.PHONY: release-probe
+
+# the importer's unmap-then-allocate pattern of eager registration churn, without the library
+reuse-probe: tests/native/reuse_probe
+
+tests/native/reuse_probe: tests/native/reuse_probe.hip
+	$(HIPCC) -O2 --offload-arch=$(ARCH) -o $@ $<
+
+.PHONY: reuse-probe

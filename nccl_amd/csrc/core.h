@@ -125,8 +125,12 @@ struct FdServer;
 bool ipcLegacy();
 const char* ipcServerName(const ncclComm* comm);  // "" without an fd server
 // Release peers' mappings whose owner deregistered them (ipc.cc): called on the caller's thread at the blocking entry
-// points only (init, finalize, destroy, (de)registration), never in a collective; a no-op unless a RELEASE arrived.
+// points (init, finalize, destroy, (de)registration); a no-op unless a RELEASE arrived.
 void ipcDrainReleases();
+// The same on the collective path (ipc.cc): mappings whose owner released them, unmapped without waiting for the device
+void ipcProgressReleases();
+// after each kernel launch of a multi-process communicator (outside captures): the stream's tail event (ipc.cc)
+void ipcNoteLaunch(hipStream_t stream, int device);
 // Held around this library's device allocations, imports and releases (ipc.cc gMapMu): no allocation of ours can
 // interleave with a mapping being torn down on another thread (a non-blocking init runs on its own thread).
 std::mutex& ipcMapMutex();
@@ -141,6 +145,7 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested);
 ncclResult_t ipcServerStart(ncclComm* comm);
 void ipcServerStop(ncclComm* comm);
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d);
+hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd);  // under gMapMu, retried (ipc.cc)
 void ipcUnexport(ncclComm* comm, const IpcDesc& d);
 ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d);  // serve an fd (owned) under a new key
 ncclResult_t ipcFetchFd(const IpcDesc& d, int* fd);  // an exporter's fd for d, over its fd server (bounded)
@@ -151,6 +156,9 @@ void ipcRelease(IpcImport* m);
 // the caller keeps its copy) on its device on behalf of `rank`, remembered under `tag`; *addr = where it
 // landed in the peer's process. Release drops that mapping (best effort: a peer already gone released it).
 ncclResult_t ipcRemoteImport(const char* server, int rank, uint64_t tag, int fd, uint64_t size, uint64_t* addr);
+// the same with a hipIpc handle of the allocation instead of a dma-buf fd (the owner's export was refused)
+ncclResult_t ipcRemoteImportHandle(const char* server, int rank, uint64_t tag, const hipIpcMemHandle_t& h, uint64_t size,
+                                   uint64_t* addr);
 void ipcRemoteRelease(const char* server, int rank, uint64_t tag);
 uint64_t ipcNewTag();
 
@@ -201,6 +209,11 @@ struct RegAlloc {
   int localRefs, graphRefs;
   bool eagerRef;       // held by the eager registration cache (NCCL_AMD_EAGER_REGISTER=1, register.cc)
   uint64_t lastUse;    // the comm's registration clock at its last collective (eager cache eviction order)
+  // recorded after every zero-copy kernel launched on it (outside captures): once complete, no kernel of this rank
+  // hands the peers its addresses any more and no peer kernel reads it (each peer reads before its DONE signal,
+  // which this rank's kernel waits for), so its peers' mappings may go without waiting for the device (regProgress)
+  hipEvent_t lastEv;
+  bool evMissing;      // lastEv could not be created: released only at a blocking entry point (after a device wait)
 };
 enum RegRefKind { REF_LOCAL = 0, REF_GRAPH = 1, REF_EAGER = 2 };
 struct RegHandle {  // what ncclCommRegister returns
@@ -255,7 +268,8 @@ struct CommTuning {
   int refChannels;          // NCCL_AMD_REF_NCHANNELS: the reference run's channel count K (0: the channel cap), <= 64
   int eagerRegister;        // NCCL_AMD_EAGER_REGISTER: unregistered buffers are registered on first use (register.cc)
   int64_t eagerBytes;       // NCCL_AMD_EAGER_REGISTER_BYTES: ... for collectives of at least this many bytes
-  int eagerMax;             // NCCL_AMD_EAGER_REGISTER_MAX: eager registrations kept past a blocking entry point
+  int eagerMax;             // NCCL_AMD_EAGER_REGISTER_MAX: eager registrations kept (LRU beyond it retired)
+  int64_t eagerMaxBytes;    // NCCL_AMD_EAGER_REGISTER_MAX_BYTES: ... and their bytes
   // size table (NCCL_AMD_SIZE_TABLE, enqueue.cc sizeTable): per rank count, the upper ends of the LL, LL128-class
   // and one-shot ranges in bytes (0 = the built-in default); loaded once at init and agreed with rank 0's
   int64_t tableLL[NCCL_AMD_MAX_RANKS + 1], tableLL128[NCCL_AMD_MAX_RANKS + 1], tableOneShot[NCCL_AMD_MAX_RANKS + 1];
@@ -334,6 +348,8 @@ struct ncclComm {
   // peers' RELEASE requests go out at this rank's next blocking entry point, never inside a collective (register.cc)
   std::vector<ncclamd::RegAlloc*> regRetired;
   uint64_t regClock = 0;     // registration uses (RegAlloc::lastUse)
+  ncclamd::RegAlloc* regLastUse[2] = {};  // the registrations regLookup's last hit returned (send, recv)
+  size_t regScan = 0;        // regProgress: round-robin cursor of the freed-allocation check
   uint64_t regGen = 0;       // this comm's identity for graph-release tokens (0 until the first graph hold)
   bool warnedEagerCap = false;
   std::vector<std::pair<uint64_t, uint64_t>> eagerFailed;  // (base, buffer id) whose eager registration failed
@@ -355,6 +371,8 @@ struct ncclComm {
 namespace ncclamd {
 
 ncclResult_t commCheck(const ncclComm* comm, const char* opname, const char* what);
+// a device-side error recorded by a kernel (timeout, abort, kernel mismatch) becomes the comm's async error (init.cc)
+void commPollAsync(ncclComm* comm);
 ncclResult_t transportSetup(ncclComm* comm);     // allocate staging/flags + IPC export
 ncclResult_t transportConnect(ncclComm* comm);   // map peers after the PeerInfo exchange
 ncclResult_t transportFree(ncclComm* comm);
@@ -427,6 +445,7 @@ ncclResult_t enqueueCheck(CollInfo* info);
 // plan + launch (enqueue.cc); forkJoin=false: the caller (group end) forks/joins shared-GPU comms itself
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin = true);
 ncclResult_t collFork(const CollInfo& info);
+void collProgress(ncclComm* comm);  // enqueue.cc: registration / release upkeep on the collective path, never waiting
 bool llPlan(const CollInfo& info, LLOp* op);                  // LL eligibility + plan (enqueue.cc)
 
 // ---------------------------------------------------------------- tuner plugin (reference src/plugin/tuner.cc)
@@ -452,6 +471,7 @@ struct SymPlan {  // one symmetric (window) kernel launch
   int nChannels;
   hipStream_t stream;
   SymArgs args;
+  RegAlloc* regUse[2];  // registered mode: the send / recv registrations it runs on (their lastEv, register.cc)
 };
 ncclResult_t launchSymPlan(const SymPlan& plan);  // kernels.hip
 
@@ -480,10 +500,15 @@ void windowsFree(ncclComm* comm, bool notifyPeers);
 // A blocking entry point's registration upkeep (register.cc): graph-held references whose graphs are gone are
 // dropped, stale and surplus eager registrations released, and retired registrations' RELEASE requests sent.
 void regBlockingPoint(ncclComm* comm);
+// The same upkeep on the collective path, never waiting (register.cc): freed allocations found, the eager cache kept
+// within its count and byte bounds, and RELEASE sent for retired registrations whose last kernel completed.
+void regProgress(ncclComm* comm);
+// after a launched zero-copy plan: its registrations' lastEv recorded on its stream (outside captures)
+void regRecordUse(ncclComm* comm, const SymPlan& sp);
 // Set by ncclGroupSimulateEnd around its planning (group.cc): an eager lookup then registers nothing and reports the
 // zero-copy plan the real group end would take (register.cc regLookup).
 extern thread_local bool tPlanOnly;
-// [p, +bytes) lies in a usable registration held by an ncclCommRegister handle or the eager cache (no side effects)
+// [p, +bytes) lies in a usable registration held by an ncclCommRegister handle (no side effects)
 bool regCovers(ncclComm* comm, const void* p, size_t bytes);
 // all-gather over the comm's bootstrap (multi-process) or in-process clique (ncclCommInitAll)
 ncclResult_t commAllGather(ncclComm* comm, void* data, size_t bytesPerRank);

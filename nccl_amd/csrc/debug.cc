@@ -82,8 +82,15 @@ void logMessage(int level, const char* file, int line, const char* fmt, ...) {
   if (level == LOG_WARN)
     fprintf(gLogFile, "%s:%d:%ld [%s] %s:%d NCCL %s %s\n", host, getpid(), (long)syscall(SYS_gettid),
             "mi355x", file, line, levelName(level), buf);
-  else
+  else if (level == LOG_TRACE) {  // with a system-wide clock, so ranks' lines can be merged; flushed (a crash keeps them)
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    fprintf(gLogFile, "%s:%d:%ld %ld.%06ld NCCL %s %s\n", host, getpid(), (long)syscall(SYS_gettid), (long)ts.tv_sec,
+            ts.tv_nsec / 1000, levelName(level), buf);
+    fflush(gLogFile);
+  } else {
     fprintf(gLogFile, "%s:%d:%ld NCCL %s %s\n", host, getpid(), (long)syscall(SYS_gettid), levelName(level), buf);
+  }
 }
 
 void setLastError(const char* fmt, ...) {

@@ -11,6 +11,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cmath>
 
 #include "core.h"
 
@@ -241,6 +242,9 @@ void loadTuning(CommTuning* t) {
   t->eagerBytes = paramInt("NCCL_AMD_EAGER_REGISTER_BYTES", 1 << 20);
   t->eagerMax = (int)paramInt("NCCL_AMD_EAGER_REGISTER_MAX", 64);
   if (t->eagerMax < 1) t->eagerMax = 1;
+  // bytes of eager-only registrations kept (their peers map them; once the owner frees one, until the next
+  // collective's upkeep finds it, that HBM stays held): the least recently used beyond it are retired
+  t->eagerMaxBytes = paramInt("NCCL_AMD_EAGER_REGISTER_MAX_BYTES", (int64_t)32 << 30);
   // the size table's ranges (per rank count; NCCL_AMD_SIZE_TABLE overrides rows, the three knobs below all rows)
   (void)loadSizeTable(t, paramStr("NCCL_AMD_SIZE_TABLE"));
   t->oneShotBytes = paramInt("NCCL_AMD_ONESHOT_BYTES", 0);  // 0: size table default (2 MiB / nRanks; 2 MiB at 2 ranks)
@@ -302,7 +306,7 @@ static int64_t parseBytes(const char* tok, bool* ok) {
   if (!strcmp(tok, "-")) return -1;
   char* end = nullptr;
   const double v = strtod(tok, &end);
-  if (end == tok || v < 0) {
+  if (end == tok || !std::isfinite(v) || v < 0) {  // 'nan' / 'inf' are malformed sizes
     *ok = false;
     return 0;
   }
@@ -566,8 +570,11 @@ static uint32_t refSubCount(ncclComm* comm, const RingParts& r, uint64_t chunk, 
   return g < 1 ? 1 : (uint32_t)g;
 }
 
-// The plugin's regBuff (reference enqueue.cc:2141-2147): both buffers registered (ncclCommRegister, a window, or the
-// eager cache), or a capture with NCCL_GRAPH_REGISTER on. Asked only when a tuner plugin is loaded.
+// The plugin's regBuff (reference enqueue.cc:2141-2147): both buffers registered (an ncclCommRegister handle or a
+// window), or a capture with NCCL_GRAPH_REGISTER on. Asked only when a tuner plugin is loaded. The plan must be the
+// same on every rank, so regBuff rests only on what the user does on every rank alike: not on the eager cache, whose
+// contents follow each rank's own LRU clock. A plugin must still not key on regBuff where its user
+// registers buffers on some ranks only — the reference passes it the same way (enqueue.cc:2141-2148).
 static int tunerRegBuff(ncclComm* comm, const CollInfo& info) {
   const int n = comm->nRanks;
   const size_t ts = (size_t)typeSize(info.datatype);
@@ -895,6 +902,8 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       sp.args.redArg = p.args.redArg;
       sp.args.redArgPtr = p.args.redArgPtr;
       sp.args.regMode = regMode;
+      sp.regUse[0] = regMode == 1 ? comm->regLastUse[0] : nullptr;  // their lastEv follow this launch (regRecordUse)
+      sp.regUse[1] = regMode == 1 ? comm->regLastUse[1] : nullptr;
       uintptr_t al = 0;
       for (int r = 0; r < n; r++) {
         sp.args.send[r] = sendPtr[r];
@@ -978,12 +987,15 @@ static ncclResult_t checkGrid(const ncclComm* comm, int kind, const LaunchPlan& 
   return ncclInternalError;
 }
 
+static void noteLaunch(ncclComm* comm, hipStream_t stream);
+
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   ncclComm* comm = info.comm;
   HIPCHECK(hipSetDevice(comm->device));
   LaunchPlan p;
   SymPlan sp;
   int kind;
+  collProgress(comm);
   NCCLCHECK(planColl(info, p, sp, &kind));
   if (kind == PLAN_NONE) return ncclSuccess;
   NCCLCHECK(checkGrid(comm, kind, p, sp));
@@ -991,12 +1003,38 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   // and a join (see ncclComm::internalStream)
   const bool shared =
       comm->sharedDevInProcess && !(kind == PLAN_KERNEL && (p.algo == ALGO_COPY || p.algo == ALGO_ONERANK));
-  if (!shared) return kind == PLAN_SYM ? launchSymPlan(sp) : launchPlan(p);
-  if (forkJoin) NCCLCHECK(collFork(info));
-  p.stream = sp.stream = comm->internalStream;
-  NCCLCHECK(kind == PLAN_SYM ? launchSymPlan(sp) : launchPlan(p));
-  if (forkJoin) NCCLCHECK(collJoin(info));
+  if (shared) {
+    if (forkJoin) NCCLCHECK(collFork(info));
+    p.stream = sp.stream = comm->internalStream;
+  }
+  if (kind == PLAN_SYM) {
+    NCCLCHECK(launchSymPlan(sp));
+    regRecordUse(comm, sp);
+  } else {
+    NCCLCHECK(launchPlan(p));
+  }
+  noteLaunch(comm, kind == PLAN_SYM ? sp.stream : p.stream);
+  if (shared && forkJoin) NCCLCHECK(collJoin(info));
   return ncclSuccess;
+}
+
+// A multi-process communicator's launches leave their stream's tail event (ipc.cc ipcNoteLaunch): peers' released
+// mappings are unmapped on the collective path only while none of this library's kernels is in flight here.
+static void noteLaunch(ncclComm* comm, hipStream_t stream) {
+  if (!comm->fdServer) return;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return;  // a graph's kernels are launched by its replays, each complete on every rank independently
+  }
+  ipcNoteLaunch(stream, comm->device);
+}
+
+// Upkeep on the collective path, before anything of this collective is planned or launched, never waiting (VERDICT r5
+// item 4): this rank's registrations (register.cc regProgress) and the peers' mappings they released (ipc.cc).
+void collProgress(ncclComm* comm) {
+  regProgress(comm);
+  ipcProgressReleases();
 }
 
 // ---- group aggregation (reference: a group's ops aggregated into one kernel plan, enqueue.cc:405-470) ----
@@ -1042,7 +1080,17 @@ ncclResult_t launchBatch(std::vector<PlannedColl>& run) {
       comm->sharedDevInProcess && !(run[0].kind == PLAN_KERNEL && (p.algo == ALGO_COPY || p.algo == ALGO_ONERANK));
   if (shared) p.stream = run[0].sp.stream = comm->internalStream;
   for (const PlannedColl& x : run) NCCLCHECK(checkGrid(comm, x.kind, x.p, x.sp));
-  if (run.size() == 1) return run[0].kind == PLAN_SYM ? launchSymPlan(run[0].sp) : launchPlan(p);
+  if (run.size() == 1) {
+    if (run[0].kind != PLAN_SYM) {
+      NCCLCHECK(launchPlan(p));
+      noteLaunch(comm, p.stream);
+      return ncclSuccess;
+    }
+    NCCLCHECK(launchSymPlan(run[0].sp));
+    regRecordUse(comm, run[0].sp);
+    noteLaunch(comm, run[0].sp.stream);
+    return ncclSuccess;
+  }
   if (p.algo == ALGO_LL) {
     int off = p.ll.ops[0].nch % comm->llChannels, used = p.ll.ops[0].nch;
     for (size_t k = 1; k < run.size(); k++) {
@@ -1066,7 +1114,9 @@ ncclResult_t launchBatch(std::vector<PlannedColl>& run) {
     for (int k = 0; k < p.ll.nOps; k++)
       for (int j = 0; j < p.ll.ops[k].nch; j++) p.ll.chMask[(p.ll.ops[k].chOff + j) % comm->llChannels] |= 1u << k;
     TRACE("LL batch: %d ops (first %s), %d channels", p.ll.nOps, kFuncName[run[0].info.func], p.nChannels);
-    return launchPlan(p);
+    NCCLCHECK(launchPlan(p));
+    noteLaunch(comm, p.stream);
+    return ncclSuccess;
   }
   CollBatchArgs& b = p.batch;
   int off = 0, used = 0;
@@ -1081,7 +1131,9 @@ ncclResult_t launchBatch(std::vector<PlannedColl>& run) {
   p.nChannels = used < comm->chanCap ? used : comm->chanCap;
   TRACE("staged batch: %d %s ops (%s), %d channels", b.nOps, kFuncName[run[0].info.func],
         p.algo == ALGO_ONESHOT ? "one-shot" : "direct", p.nChannels);
-  return launchPlan(p);
+  NCCLCHECK(launchPlan(p));
+  noteLaunch(comm, p.stream);
+  return ncclSuccess;
 }
 
 // Fork / join of a shared-GPU comm's internal stream with the caller's stream. A group issues every
@@ -1117,8 +1169,14 @@ ncclResult_t enqueueCheck(CollInfo* info) {
     return ret;
   }
   // (no ipcDrainReleases here: unmapping a peer's deregistered buffer is a device-synchronising hipFree, and a
-  // collective must return once its work is enqueued, nccl.h.in:431-442; the blocking entry points drain, ipc.cc)
+  // collective must return once its work is enqueued, nccl.h.in:431-442; launchColl / the group end unmap only while
+  // none of the library's kernels is in flight, collProgress, and the blocking entry points drain, ipc.cc)
   ret = argsCheck(info);
+  // A kernel of this comm recorded a device error (spin timeout, abort, kernel mismatch): its peers' handshake state no
+  // longer matches this rank's, and a zero-copy kernel would read peer pointers of some earlier collective — launch
+  // nothing more (the reference's comm is equally unusable after an async error; its kernels, though, hang rather
+  // than touch stale mappings)
+  commPollAsync(info->comm);
   if (ret == ncclSuccess && info->comm->asyncResult.load() != ncclSuccess) {
     WARN("%s: communicator is in error state %d", info->opName, info->comm->asyncResult.load());
     ret = ncclInvalidUsage;

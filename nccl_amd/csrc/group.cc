@@ -155,6 +155,15 @@ ncclResult_t groupEndInternal(ncclSimInfo_t* simInfo) {
   }
   int dev = 0;
   (void)hipGetDevice(&dev);
+  // each communicator's upkeep first, before any of the group's kernels is launched (enqueue.cc collProgress)
+  for (size_t i = 0; i < colls.size(); i++) {
+    bool seen = false;
+    for (size_t j = 0; j < i && !seen; j++) seen = colls[j].comm == colls[i].comm;
+    if (!seen) {
+      (void)hipSetDevice(colls[i].comm->device);
+      collProgress(colls[i].comm);
+    }
+  }
   ncclResult_t r = ncclSuccess;
   for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = collFork(colls[i]);
   // launches in group order per comm; consecutive ops that planned onto the same kernel with the same stream,

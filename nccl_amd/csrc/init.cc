@@ -439,7 +439,7 @@ NCCL_EXPORT ncclResult_t ncclCommInitAll(ncclComm_t* comms, int ndev, const int*
 }
 NCCL_ALIAS(ncclResult_t, ncclCommInitAll, ncclComm_t*, int, const int*)
 
-static void pollAsync(ncclComm* comm) {
+void ncclamd::commPollAsync(ncclComm* comm) {
   if (comm->hostError && __atomic_load_n(comm->hostError, __ATOMIC_ACQUIRE) != DERR_NONE) {
     uint32_t e = __atomic_load_n(comm->hostError, __ATOMIC_ACQUIRE);
     int cur = ncclSuccess;
@@ -544,7 +544,7 @@ NCCL_EXPORT ncclResult_t ncclCommGetAsyncError(ncclComm_t comm, ncclResult_t* as
     WARN("ncclGetAsyncError : asyncError argument is NULL");
     return ncclInvalidArgument;
   }
-  pollAsync(comm);
+  commPollAsync(comm);
   *asyncError = (ncclResult_t)comm->asyncResult.load();
   return ncclSuccess;
 }

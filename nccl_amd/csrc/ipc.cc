@@ -67,16 +67,18 @@ struct FdServer {
 //
 // What the mechanism guarantees since round 4:
 //  * the fd server never touches the device for a RELEASE: it moves the mapping to gPending and answers;
-//  * gPending is drained only on the caller's thread at entry points that may block by contract — CommInitRank /
-//    InitAll, Finalize, Destroy, (Window)Register and (Window)Deregister — never inside a collective (a collective
-//    returns once its work is enqueued, reference nccl.h.in:431-442; the reference unmaps on its proxy thread for
-//    the same reason, src/transport/p2p.cc:762-780), and never concurrently with this library's allocations or
-//    imports (gMapMu);
+//  * gPending is drained on the caller's thread only: at entry points that may block by contract — CommInitRank /
+//    InitAll, Finalize, Destroy, (Window)Register and (Window)Deregister — and, since round 6, at a collective's
+//    enqueue once none of this library's kernels is in flight in this process (ipcProgressReleases: the unmap then
+//    waits for nothing of ours; a collective returns once its work is enqueued, reference nccl.h.in:431-442; the
+//    reference unmaps on its proxy thread, src/transport/p2p.cc:762-780), never concurrently with this library's
+//    allocations or imports (gMapMu);
 //  * a mapping stays valid until drained, so a kernel of this rank still reading the peer's buffer never faults:
 //    the dma-buf import keeps the peer's memory referenced even after the peer freed it.
-// The cost is memory: a peer's deregistered buffer stays mapped here until this rank's next such entry point.
+// The cost is memory: a peer's deregistered buffer stays mapped here until this rank's next such point.
 static std::mutex gMapMu;
 std::mutex& ipcMapMutex() { return gMapMu; }
+static void releaseLocked(IpcImport* m);
 struct PendingRelease {
   IpcImport map;
   int device;
@@ -85,9 +87,9 @@ static std::mutex gPendMu;
 static std::vector<PendingRelease> gPending;
 static std::atomic<bool> gHavePending{false};
 
-// Bytes of released peer mappings waiting for a blocking entry point. A rank that only issues collectives keeps them
-// (and so the peers' freed HBM) until its next blocking call; past NCCL_AMD_PENDING_RELEASE_WARN_BYTES (4 GiB) that
-// is said once per crossing, with the calls that would return the memory.
+// Bytes of released peer mappings waiting to be unmapped (ipcProgressReleases, ipcDrainReleases); past
+// NCCL_AMD_PENDING_RELEASE_WARN_BYTES (4 GiB) that is said once per crossing, with the calls that return the memory
+// (ADVICE r4).
 static uint64_t gPendingBytes = 0;
 static bool gPendingWarned = false;
 
@@ -100,8 +102,9 @@ static void releaseLater(int device, const IpcImport& m) {
   if (gPendingBytes >= warnAt && !gPendingWarned) {
     gPendingWarned = true;
     WARN("%.2f GiB of peers' deregistered buffers are still mapped in this process (device %d): they are unmapped at "
-         "this rank's next blocking call (ncclCommRegister / Deregister / Finalize / Destroy / Init), and until then "
-         "the peers' freed HBM stays allocated", gPendingBytes / (double)(1ull << 30), device);
+         "this rank's next collective issued while none of the library's kernels runs here, or its next blocking call "
+         "(ncclCommRegister / Deregister / Finalize / Destroy / Init); until then the peers' freed HBM stays allocated",
+         gPendingBytes / (double)(1ull << 30), device);
   }
 }
 
@@ -129,6 +132,92 @@ void ipcDrainReleases() {
   TRACE("ipc: released %zu peer mapping(s) of deregistered buffers", batch.size());
 }
 
+// Every stream this library launched a kernel on in this process, with an event recorded after its latest launch
+// (multi-process communicators, outside captures: ipcNoteLaunch). "Every one complete" means no kernel of this library
+// is in flight here — the condition for unmapping on the collective path below.
+struct StreamTail {
+  hipStream_t stream;
+  int device;
+  hipEvent_t ev;
+};
+static std::mutex gTailMu;
+static std::vector<StreamTail> gTails;
+static bool gTailsOverflow = false;  // more streams than tracked: the collective path never unmaps
+constexpr size_t kMaxTails = 64;
+
+void ipcNoteLaunch(hipStream_t stream, int device) {
+  std::lock_guard<std::mutex> g(gTailMu);
+  if (gTailsOverflow) return;
+  for (StreamTail& t : gTails)
+    if (t.stream == stream && t.device == device) {
+      if (hipEventRecord(t.ev, stream) != hipSuccess) (void)hipGetLastError(), gTailsOverflow = true;
+      return;
+    }
+  StreamTail t = {stream, device, nullptr};
+  if (gTails.size() >= kMaxTails || hipEventCreateWithFlags(&t.ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventRecord(t.ev, stream) != hipSuccess) {
+    (void)hipGetLastError();
+    gTailsOverflow = true;  // (an event created before a failed record stays unused)
+    return;
+  }
+  gTails.push_back(t);
+}
+
+static bool libraryIdle() {
+  std::lock_guard<std::mutex> g(gTailMu);
+  if (gTailsOverflow) return false;
+  for (const StreamTail& t : gTails)
+    if (hipEventQuery(t.ev) == hipErrorNotReady) return false;
+  (void)hipGetLastError();
+  return true;
+}
+
+// The collective path's share of the drain. A mapping whose owner sent RELEASE is read by no
+// kernel any more: the owner sends it only once its own last kernel on the buffer has completed (register.cc
+// regProgress, an event query), and every peer kernel reads the buffer before the DONE signal that kernel waits for.
+// What keeps it off the collective path is the unmap itself: hipFree of an imported mapping waits for every kernel
+// of this process on the device (tests/native/release_probe: 300.0 ms behind a 300 ms kernel; hipDestroyExternalMemory
+// 2 us; profiles/r06_release_probe.json). Waiting for one of this library's kernels there could deadlock: it may wait
+// on a peer that waits for this rank's next launch (a peer importing a registration from this process's fd server,
+// which needs gMapMu; ranks issuing collectives of two communicators in different orders). So the collective path
+// unmaps only once every kernel this library launched here has completed (libraryIdle: event queries, never a wait);
+// the hipFree then waits at most for the application's own kernels, as any hipFree of the application does. Bounded
+// work — two mappings per call — and never contending with this library's allocations and imports: when another thread
+// holds gMapMu (a non-blocking init, the fd server importing a peer's registration) they wait for a later call.
+// NCCL_AMD_RELEASE_ON_COLL=0 leaves them to the blocking entry points.
+void ipcProgressReleases() {
+  if (!gHavePending.load(std::memory_order_acquire)) return;
+  static const bool on = paramInt("NCCL_AMD_RELEASE_ON_COLL", 1) != 0;
+  if (!on || !libraryIdle()) return;
+  std::unique_lock<std::mutex> lk(gMapMu, std::try_to_lock);
+  if (!lk.owns_lock()) return;
+  std::vector<PendingRelease> batch;
+  {
+    std::lock_guard<std::mutex> g(gPendMu);
+    while (!gPending.empty() && batch.size() < 2) {
+      batch.push_back(gPending.back());
+      gPending.pop_back();
+      gPendingBytes -= std::min(gPendingBytes, batch.back().map.size);
+    }
+    if (gPending.empty()) {
+      gPendingWarned = false;
+      gHavePending.store(false, std::memory_order_release);
+    }
+  }
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;  // the caller's stream may be capturing
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  for (PendingRelease& r : batch) {
+    (void)hipSetDevice(r.device);
+    releaseLocked(&r.map);
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  (void)hipSetDevice(dev);
+  (void)hipGetLastError();
+  TRACE("ipc: released %zu peer mapping(s) on the collective path", batch.size());
+}
+
 // Requests on the fd server's socket (one per connection). FETCH: hand over the fd published under `key`.
 // IMPORT: map the dma-buf fd attached to the request (SCM_RIGHTS) on this comm's device on behalf of rank
 // `from`, remember it under (from, key) and answer the address it got here. RELEASE: drop that mapping.
@@ -138,6 +227,9 @@ struct IpcRequest {
   int32_t from;
   uint64_t key;
   uint64_t size;
+  uint32_t legacy;            // IMPORT: map `handle` (a hipIpc handle) instead of an attached dma-buf fd
+  uint32_t pad;
+  hipIpcMemHandle_t handle;
 };
 struct IpcReply {
   int32_t status;  // 0 = ok
@@ -182,6 +274,7 @@ static void setTimeouts(int fd) {
 }
 
 static ncclResult_t importFd(int fd, uint64_t size, IpcImport* out);
+static ncclResult_t importLegacy(const IpcDesc& d, IpcImport* out);
 
 static int recvWithFd(int c, void* buf, size_t len, int* fd) {
   struct msghdr m = {};
@@ -237,11 +330,44 @@ static void serveOne(FdServer* s, int c) {
       outFd = it->second;
       reply.status = 0;
     }
-  } else if (q.op == IPC_IMPORT && inFd >= 0) {
+  } else if (q.op == IPC_IMPORT && (inFd >= 0 || q.legacy)) {
     IpcImport m;
-    if (hipSetDevice(s->device) == hipSuccess && importFd(inFd, q.size, &m) == ncclSuccess) {
-      inFd = -1;  // owned by the mapping now
+    bool mapped = false;
+    if (hipSetDevice(s->device) == hipSuccess) {
+      if (q.legacy) {  // a registration whose dma-buf export the owner's runtime refused (ipcRemoteImportHandle)
+        IpcDesc d;
+        memset(&d, 0, sizeof(d));
+        d.legacy = 1;
+        d.size = q.size;
+        d.handle = q.handle;
+        memset(&m, 0, sizeof(m));
+        m.fd = -1;
+        mapped = importLegacy(d, &m) == ncclSuccess;
+        m.size = q.size;
+      } else {
+        mapped = importFd(inFd, q.size, &m) == ncclSuccess;
+        if (mapped) inFd = -1;  // owned by the mapping now
+      }
+    }
+    if (mapped) {
       auto key = std::make_pair((int)q.from, q.key);
+      // diagnostics: a mapping the runtime placed where an earlier one of ours still lives (live or pending release)
+      const uint64_t lo = (uint64_t)m.ptr, hi = lo + m.size;
+      auto overlaps = [&](const IpcImport& x) { return lo < (uint64_t)x.ptr + x.size && (uint64_t)x.ptr < hi; };
+      for (const auto& kv : s->imports)
+        if (overlaps(kv.second))
+          WARN("ipc: rank %d tag %lu mapped at %p over the live mapping of rank %d tag %lu (%p, ino %lu / %lu)", q.from,
+               (unsigned long)q.key, m.ptr, kv.first.first, (unsigned long)kv.first.second, kv.second.ptr,
+               (unsigned long)m.fdIno, (unsigned long)kv.second.fdIno);
+      {
+        std::lock_guard<std::mutex> g(gPendMu);
+        for (const PendingRelease& r : gPending)
+          if (overlaps(r.map))
+            WARN("ipc: rank %d tag %lu mapped at %p over a mapping pending release (%p, ino %lu / %lu)", q.from,
+                 (unsigned long)q.key, m.ptr, r.map.ptr, (unsigned long)m.fdIno, (unsigned long)r.map.fdIno);
+      }
+      TRACE("ipc: IMPORT rank %d tag %lu: %lu MiB at %p (%s %lu)", q.from, (unsigned long)q.key,
+            (unsigned long)(m.size >> 20), m.ptr, q.legacy ? "hipIpc handle" : "dma-buf ino", (unsigned long)m.fdIno);
       auto old = s->imports.find(key);
       if (old != s->imports.end()) releaseLater(s->device, old->second);  // a re-registration replaces its mapping
       s->imports[key] = m;
@@ -253,6 +379,8 @@ static void serveOne(FdServer* s, int c) {
   } else if (q.op == IPC_RELEASE) {
     auto it = s->imports.find(std::make_pair((int)q.from, q.key));
     if (it != s->imports.end()) {
+      TRACE("ipc: RELEASE rank %d tag %lu: %p (ino %lu) pending", q.from, (unsigned long)q.key, it->second.ptr,
+            (unsigned long)it->second.fdIno);
       releaseLater(s->device, it->second);  // never block the server on the device (gPending above)
       s->imports.erase(it);
     }
@@ -355,6 +483,27 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested) {
   return !requested && size < ((size_t)2 << 30);
 }
 
+// The dma-buf export of [base, +size) (hipMemGetHandleForAddressRange), under gMapMu like every import and release of
+// this library. Round 6's eager churn (tests/test_gpu_eager.py, gpurun_out TRACE logs): exports made
+// on the caller's thread while this process's fd server thread was importing a peer's registration failed with
+// "invalid argument" — 5 of 24 registrations in 8 iterations, always beside a concurrent import — and a plain
+// export / import / unmap cycle of the same buffers without that concurrency never failed (scripts/eager_churn_probe.py,
+// tests/native/reuse_probe.hip: 0 of 80). A failure is retried (1, 2, 4, 8 ms apart, the lock released meanwhile).
+hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd) {
+  hipError_t e = hipErrorInvalidValue;
+  for (int attempt = 0; attempt < 5; attempt++) {
+    if (attempt) std::this_thread::sleep_for(std::chrono::milliseconds(1 << (attempt - 1)));
+    std::lock_guard<std::mutex> g(gMapMu);
+    e = hipMemGetHandleForAddressRange(fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
+    if (e == hipSuccess) {
+      if (attempt) INFO("ipc: dma-buf export of %p (+%zu MiB) succeeded at attempt %d", base, size >> 20, attempt + 1);
+      return e;
+    }
+    (void)hipGetLastError();
+  }
+  return e;
+}
+
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
   memset(d, 0, sizeof(*d));
   d->size = size;
@@ -376,7 +525,7 @@ ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d) {
   int fd = -1;
   hipError_t e = paramInt("NCCL_AMD_IPC_FAIL_EXPORT", 0)  // tests: exercise the fallback below
                      ? hipErrorInvalidValue
-                     : hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
+                     : ipcExportDmaBuf(base, size, &fd);
   const int err = errno;
   if (e != hipSuccess) {
     // Seen on the one-GPU box after many communicators and registrations in one process (bench.py's N = 4
@@ -474,7 +623,11 @@ static ncclResult_t ipcCall(const char* server, const IpcRequest& q, int sendFd,
 }
 
 ncclResult_t ipcFetchFd(const IpcDesc& d, int* out) {
-  IpcRequest q = {IPC_FETCH, -1, d.key, 0};
+  IpcRequest q;
+  memset(&q, 0, sizeof(q));
+  q.op = IPC_FETCH;
+  q.from = -1;
+  q.key = d.key;
   IpcReply r;
   int fd = -1;
   ncclResult_t res = ipcCall(d.server, q, -1, &r, &fd, true);
@@ -489,8 +642,33 @@ ncclResult_t ipcFetchFd(const IpcDesc& d, int* out) {
   return ncclSuccess;
 }
 
+ncclResult_t ipcRemoteImportHandle(const char* server, int rank, uint64_t tag, const hipIpcMemHandle_t& h,
+                                   uint64_t size, uint64_t* addr) {
+  IpcRequest q;
+  memset(&q, 0, sizeof(q));
+  q.op = IPC_IMPORT;
+  q.from = rank;
+  q.key = tag;
+  q.size = size;
+  q.legacy = 1;
+  q.handle = h;
+  IpcReply r;
+  NCCLCHECK(ipcCall(server, q, -1, &r, nullptr, true));
+  if (r.status != 0) {
+    WARN("ipc: %s could not open the hipIpc handle of a registered buffer of %zu MiB", server, (size_t)(size >> 20));
+    return ncclRemoteError;
+  }
+  *addr = r.value;
+  return ncclSuccess;
+}
+
 ncclResult_t ipcRemoteImport(const char* server, int rank, uint64_t tag, int fd, uint64_t size, uint64_t* addr) {
-  IpcRequest q = {IPC_IMPORT, rank, tag, size};
+  IpcRequest q;
+  memset(&q, 0, sizeof(q));
+  q.op = IPC_IMPORT;
+  q.from = rank;
+  q.key = tag;
+  q.size = size;
   IpcReply r;
   NCCLCHECK(ipcCall(server, q, fd, &r, nullptr, true));
   if (r.status != 0) {
@@ -502,7 +680,11 @@ ncclResult_t ipcRemoteImport(const char* server, int rank, uint64_t tag, int fd,
 }
 
 void ipcRemoteRelease(const char* server, int rank, uint64_t tag) {
-  IpcRequest q = {IPC_RELEASE, rank, tag, 0};
+  IpcRequest q;
+  memset(&q, 0, sizeof(q));
+  q.op = IPC_RELEASE;
+  q.from = rank;
+  q.key = tag;
   IpcReply r;
   (void)ipcCall(server, q, -1, &r, nullptr, false);  // a peer already gone has released everything itself
 }
@@ -608,6 +790,12 @@ ncclResult_t ipcImportHandle(const IpcDesc& d, IpcImport* out) {
 void ipcRelease(IpcImport* m) {
   if (!m->ptr) return;
   std::lock_guard<std::mutex> g(gMapMu);
+  releaseLocked(m);
+}
+
+static void releaseLocked(IpcImport* m) {  // caller holds gMapMu
+  if (!m->ptr) return;
+  TRACE("ipc: unmapping %p (%lu MiB, ino %lu)", m->ptr, (unsigned long)(m->size >> 20), (unsigned long)m->fdIno);
   if (m->legacy) {
     (void)hipIpcCloseMemHandle(m->ptr);
   } else {

@@ -1590,6 +1590,11 @@ __global__ void __launch_bounds__(kThreads) kCoResident symKernel(SymArgs a) {
     __builtin_memcpy(&opArg, a.redArgPtr, sizeof(T));
   }
   const Red<T, OP> fn(opArg);
+  // Registered mode reads peers' buffers at the pointers they hand over at ENTER. After a device error of this comm (a
+  // kernel mismatch, a timeout) the ranks' epochs no longer match: an ENTER wait could pass on a peer's flag of an older
+  // collective and read pointers whose mappings are gone. The error word is only written by this comm's kernels, which
+  // precede this one in stream order, so every workgroup reads the same value and leaves at once.
+  if (a.regMode && __hip_atomic_load(dc.errorWord, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != DERR_NONE) return;
   if (tid < NCCL_AMD_MAX_RANKS) {
     sh.send[tid] = a.send[tid];
     sh.recv[tid] = a.recv[tid];

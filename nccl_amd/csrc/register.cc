@@ -179,14 +179,23 @@ static uint64_t bufferIdOf(const void* p) {
 
 // Drop the peers' mappings of an allocation (the caller made sure no kernel of this rank still uses it; a
 // peer's kernels stop reading it before this rank's kernel passes its DONE handshake).
-static void regRelease(ncclComm* comm, RegAlloc* ra) {
-  for (int r = 0; r < comm->nRanks; r++)
-    if (ra->imported[r]) ipcRemoteRelease(comm->peers[r].fdServer, comm->rank, ra->tag);
+static void regFree(RegAlloc* ra) {
+  if (ra->lastEv) (void)hipEventDestroy(ra->lastEv);
   delete ra;
 }
 
-// Map the allocation [base, +size) into every peer process (same process: its own pointer).
-static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint64_t id, RegAlloc** out) {
+static void regRelease(ncclComm* comm, RegAlloc* ra) {
+  TRACE("rank %d: RELEASE of allocation %lx (id %lu, tag %lu) to its peers", comm->rank, (unsigned long)ra->base,
+        (unsigned long)ra->bufferId, (unsigned long)ra->tag);
+  for (int r = 0; r < comm->nRanks; r++)
+    if (ra->imported[r]) ipcRemoteRelease(comm->peers[r].fdServer, comm->rank, ra->tag);
+  regFree(ra);
+}
+
+// Map the allocation [base, +size) into every peer process (same process: its own pointer). `deferRelease` (inside a
+// collective): a registration failing after some peers mapped it is retired, not released from here.
+static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint64_t id, RegAlloc** out,
+                              bool deferRelease) {
   RegAlloc* ra = new RegAlloc();
   memset(ra, 0, sizeof(*ra));
   ra->base = base;
@@ -196,6 +205,8 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
   ra->usable = true;
   const int me = comm->rank, pid = getpid();
   int fd = -1;
+  bool useHandle = false;  // the dma-buf export was refused: peers open a hipIpc handle instead (below)
+  hipIpcMemHandle_t handle;
   ncclResult_t res = ncclSuccess;
   for (int r = 0; r < comm->nRanks && res == ncclSuccess; r++) {
     if (r == me || comm->peers[r].pid == pid) {  // one address space (peer access enabled at init)
@@ -208,35 +219,56 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
       ra->usable = false;
       break;
     }
-    if (fd < 0) {
-      hipError_t e = paramInt("NCCL_AMD_REG_FAIL_EXPORT", 0)  // tests: a registration that fails on one rank only
+    if (fd < 0 && !useHandle) {
+      const bool failAll = paramInt("NCCL_AMD_REG_FAIL_EXPORT", 0) != 0;  // tests: a registration failing on one rank
+      hipError_t e = failAll || paramInt("NCCL_AMD_REG_FAIL_DMABUF", 0)  // tests: the hipIpc fallback below
                          ? hipErrorInvalidValue
-                         : hipMemGetHandleForAddressRange(&fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
+                         : ipcExportDmaBuf((void*)base, size, &fd);
       if (e != hipSuccess) {
         (void)hipGetLastError();
-        WARN("ncclCommRegister: allocation %lx (+%zu) cannot be exported: %s", (unsigned long)base, (size_t)size,
-             hipGetErrorString(e));
-        res = ncclUnhandledCudaError;
-        break;
+        // The runtime sometimes refuses the dma-buf export of a fresh allocation ("invalid argument"; round 6's eager
+        // churn: an allocation over the range of one just freed and released), as it once refused a
+        // fresh slab's (ipc.cc ipcExport). A registration failing on one rank only makes the ranks run different
+        // kernels, so — as for the slab — its peers open a hipIpc handle instead where the runtime can (below 2 GiB,
+        // or a 7.2+ runtime).
+        {
+          std::lock_guard<std::mutex> g(ipcMapMutex());
+          useHandle = !failAll && ipcLegacyAllowed(hipRuntimeInfo().version, size, false) &&
+                      hipIpcGetMemHandle(&handle, (void*)base) == hipSuccess;
+        }
+        (void)hipGetLastError();
+        if (useHandle) {
+          INFO("rank %d: allocation %lx (+%zu MiB): dma-buf export refused (%s); its peers open a hipIpc handle", me,
+               (unsigned long)base, (size_t)(size >> 20), hipGetErrorString(e));
+        } else {
+          WARN("ncclCommRegister: allocation %lx (+%zu) cannot be exported: %s", (unsigned long)base, (size_t)size,
+               hipGetErrorString(e));
+          res = ncclUnhandledCudaError;
+          break;
+        }
       }
     }
-    res = ipcRemoteImport(comm->peers[r].fdServer, me, ra->tag, fd, size, &ra->rmt[r]);
+    res = useHandle ? ipcRemoteImportHandle(comm->peers[r].fdServer, me, ra->tag, handle, size, &ra->rmt[r])
+                    : ipcRemoteImport(comm->peers[r].fdServer, me, ra->tag, fd, size, &ra->rmt[r]);
     if (res == ncclSuccess) ra->imported[r] = true;
   }
   if (fd >= 0) close(fd);
   if (res != ncclSuccess) {
-    regRelease(comm, ra);
+    if (deferRelease) comm->regRetired.push_back(ra);  // never used by a kernel: released at the next progress call
+    else regRelease(comm, ra);
     return res;
   }
-  TRACE("rank %d: registered allocation %lx +%zu MiB (tag %lu, %s)", me, (unsigned long)base, (size_t)(size >> 20),
-        (unsigned long)ra->tag, ra->usable ? "mapped by every peer" : "local only");
+  TRACE("rank %d: registered allocation %lx +%zu MiB (id %lu, tag %lu, %s; in rank %d at %lx)", me, (unsigned long)base,
+        (size_t)(size >> 20), (unsigned long)id, (unsigned long)ra->tag, ra->usable ? "mapped by every peer" : "local only",
+        (me + 1) % comm->nRanks, (unsigned long)ra->rmt[(me + 1) % comm->nRanks]);
   *out = ra;
   return ncclSuccess;
 }
 
 // Find or create the registration of the allocation holding [buff, +size) and take a reference of `kind` on it
 // (an eager reference is one flag: the cache holds an allocation at most once).
-static ncclResult_t regAcquire(ncclComm* comm, const void* buff, size_t size, int kind, RegAlloc** out) {
+static ncclResult_t regAcquire(ncclComm* comm, const void* buff, size_t size, int kind, RegAlloc** out,
+                               bool deferRelease = false) {
   hipDeviceptr_t base = nullptr;
   size_t allocSize = 0;
   HIPCHECK(hipMemGetAddressRange(&base, &allocSize, (hipDeviceptr_t)buff));
@@ -249,7 +281,7 @@ static ncclResult_t regAcquire(ncclComm* comm, const void* buff, size_t size, in
   for (RegAlloc* x : comm->regs)
     if (x->base == (uint64_t)base && x->size == allocSize && x->bufferId == id) ra = x;
   if (!ra) {
-    NCCLCHECK(regCreate(comm, (uint64_t)base, allocSize, id, &ra));
+    NCCLCHECK(regCreate(comm, (uint64_t)base, allocSize, id, &ra, deferRelease));
     comm->regs.push_back(ra);
   }
   if (kind == REF_GRAPH) ra->graphRefs++;
@@ -454,20 +486,133 @@ void regBlockingPoint(ncclComm* comm) {
   }
   std::vector<RegAlloc*> retired;
   retired.swap(comm->regRetired);
-  for (RegAlloc* ra : retired) regRelease(comm, ra);
+  bool synced = false;
+  for (RegAlloc* ra : retired) {
+    if (ra->lastEv) (void)hipEventSynchronize(ra->lastEv);  // a blocking call: its last kernel may still run
+    if (ra->evMissing && !synced) {
+      DeviceRestore restore;
+      (void)hipSetDevice(comm->device);
+      (void)hipDeviceSynchronize();
+      synced = true;
+    }
+    regRelease(comm, ra);
+  }
+}
+
+// The upkeep above on the collective path, without waiting for anything: a loop that
+// frees and re-allocates buffers and only issues collectives must neither grow the retired list nor keep its peers
+// holding freed HBM until some blocking call. Per call, bounded work:
+//  * freed allocations: the buffer id of two eager registrations (round robin) is checked; one whose allocation is
+//    gone is retired (the lookup of a collective on a re-allocated range retires it too, regFind);
+//  * the eager cache's bounds: beyond NCCL_AMD_EAGER_REGISTER_MAX registrations or NCCL_AMD_EAGER_REGISTER_MAX_BYTES,
+//    the least recently used eager-only ones are retired (retiring is local: the kernel choice of later collectives,
+//    which every rank must share, never depends on it — an evicted allocation is registered again on its next use);
+//  * retired registrations whose last zero-copy kernel has completed (hipEventQuery, never a wait) get their peers'
+//    RELEASE now, at most four per call (one socket round trip per importing peer each); the peers unmap at their own
+//    next collective (ipcProgressReleases). A retired registration still in flight waits for a later call.
+void regProgress(ncclComm* comm) {
+  if (tPlanOnly || (comm->regs.empty() && comm->regRetired.empty())) return;
+  hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;  // event queries are not capture-safe in global mode
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+  uint64_t eagerBytes = 0;
+  int eagerCount = 0;
+  for (RegAlloc* ra : comm->regs)
+    if (ra->eagerRef && ra->localRefs == 0 && ra->graphRefs == 0) eagerBytes += ra->size, eagerCount++;
+  for (int k = 0; k < 2 && !comm->regs.empty(); k++) {
+    const size_t i = comm->regScan++ % comm->regs.size();
+    RegAlloc* ra = comm->regs[i];
+    if (!ra->eagerRef || bufferIdOf((const void*)ra->base) == ra->bufferId) continue;
+    INFO("rank %d: eager registration of allocation %lx retired (the allocation is gone)", comm->rank,
+         (unsigned long)ra->base);
+    if (ra->localRefs == 0 && ra->graphRefs == 0) eagerBytes -= ra->size, eagerCount--;
+    regPut(comm, ra, REF_EAGER, /*defer=*/true);
+  }
+  if (eagerCount > comm->tune.eagerMax || eagerBytes > (uint64_t)comm->tune.eagerMaxBytes) {
+    std::vector<RegAlloc*> lru;
+    for (RegAlloc* ra : comm->regs)
+      if (ra->eagerRef && ra->localRefs == 0 && ra->graphRefs == 0) lru.push_back(ra);
+    std::sort(lru.begin(), lru.end(), [](const RegAlloc* a, const RegAlloc* b) { return a->lastUse < b->lastUse; });
+    size_t dropped = 0;
+    // the most recent registration stays whatever its size (the collective that made it is in flight)
+    for (size_t i = 0; i + 1 < lru.size() &&
+                       (eagerCount > comm->tune.eagerMax || eagerBytes > (uint64_t)comm->tune.eagerMaxBytes); i++) {
+      eagerBytes -= lru[i]->size;
+      eagerCount--;
+      regPut(comm, lru[i], REF_EAGER, /*defer=*/true);
+      dropped++;
+    }
+    if (dropped)
+      INFO("rank %d: %zu eager registrations retired (cache bounds %d / %.1f GiB)", comm->rank, dropped,
+           comm->tune.eagerMax, comm->tune.eagerMaxBytes / (double)(1ull << 30));
+  }
+  int sent = 0;
+  for (size_t i = 0; i < comm->regRetired.size() && sent < 4;) {
+    RegAlloc* ra = comm->regRetired[i];
+    const hipError_t q = ra->evMissing ? hipErrorNotReady : ra->lastEv ? hipEventQuery(ra->lastEv) : hipSuccess;
+    if (q == hipErrorNotReady) {
+      i++;
+      continue;
+    }
+    (void)hipGetLastError();
+    comm->regRetired.erase(comm->regRetired.begin() + i);
+    regRelease(comm, ra);
+    sent++;
+  }
+  (void)hipThreadExchangeStreamCaptureMode(&mode);
+}
+
+void regRecordUse(ncclComm* comm, const SymPlan& sp) {
+  if (!sp.args.regMode) return;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(sp.stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return;  // a capture holds its registrations through the graph's lifetime instead (graphHold)
+  }
+  for (RegAlloc* ra : sp.regUse) {
+    if (!ra) continue;
+    if (!ra->lastEv && hipEventCreateWithFlags(&ra->lastEv, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      ra->lastEv = nullptr;
+      ra->evMissing = true;
+      continue;
+    }
+    if (hipEventRecord(ra->lastEv, sp.stream) != hipSuccess) (void)hipGetLastError();
+  }
+  (void)comm;
 }
 
 thread_local bool tPlanOnly = false;
 
+// The eager cache's failure memory (ncclComm::eagerFailed): the allocation holding p by (base, buffer id); a pointer
+// the runtime knows no allocation of (hipMemGetAddressRange fails: host or managed memory) by (p, its buffer id).
+static std::pair<uint64_t, uint64_t> eagerKey(const void* p) {
+  hipDeviceptr_t base = nullptr;
+  size_t allocSize = 0;
+  if (hipMemGetAddressRange(&base, &allocSize, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    base = (hipDeviceptr_t)p;
+  }
+  return {(uint64_t)base, bufferIdOf(p)};
+}
+static bool eagerFailedBefore(ncclComm* comm, const void* p) {
+  if (comm->eagerFailed.empty()) return false;
+  const auto key = eagerKey(p);
+  return std::find(comm->eagerFailed.begin(), comm->eagerFailed.end(), key) != comm->eagerFailed.end();
+}
+
+// Covered by an ncclCommRegister handle (the user registers the same buffers on every rank, bufferreg.rst:55-56). The
+// eager cache does not count: its contents follow this rank's own LRU clock, and the tuner's regBuff must not differ
+// between ranks, or a plugin keying on it would pick different kernels on different ranks.
 bool regCovers(ncclComm* comm, const void* p, size_t bytes) {
   const uint64_t a = (uint64_t)p;
   for (const RegAlloc* ra : comm->regs)
-    if (ra->usable && (ra->localRefs > 0 || ra->eagerRef) && a >= ra->base && a + bytes <= ra->base + ra->size) return true;
+    if (ra->usable && ra->localRefs > 0 && a >= ra->base && a + bytes <= ra->base + ra->size) return true;
   return false;
 }
 
 bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
                size_t recvBytes, const char** rmtSend, char** rmtRecv, bool eager) {
+  comm->regLastUse[0] = comm->regLastUse[1] = nullptr;
   if (comm->nRanks == 1) return false;
   bool capturing = false;
   if (comm->tune.graphRegister || eager) {
@@ -518,6 +663,8 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     // what is missing and run zero-copy, so the plan says so (the pointers are never used: nothing launches)
     if (!rr || (send && !rs)) {
       if (!comm->regIpcAll) return false;  // registrations would stay local (regCreate): the staged plan
+      // an allocation whose eager registration already failed runs staged at the real group end too
+      if ((send && !rs && eagerFailedBefore(comm, send)) || (!rr && eagerFailedBefore(comm, recv))) return false;
       for (int r = 0; r < comm->nRanks; r++) rmtSend[r] = nullptr, rmtRecv[r] = nullptr;
       return true;
     }
@@ -527,21 +674,19 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     // allocation and said once; this rank then runs the staged kernel, and if its peers registered theirs every rank
     // stops with the kernel-mismatch error (kernels.h WaitProbe) instead of waiting for the spin timeout.
     auto acquire = [&](const void* b, size_t bytes) -> RegAlloc* {
-      hipDeviceptr_t base = nullptr;
-      size_t allocSize = 0;
-      if (hipMemGetAddressRange(&base, &allocSize, (hipDeviceptr_t)b) != hipSuccess) {
-        (void)hipGetLastError();
-        return nullptr;
-      }
-      const std::pair<uint64_t, uint64_t> key((uint64_t)base, bufferIdOf(b));
-      if (std::find(comm->eagerFailed.begin(), comm->eagerFailed.end(), key) != comm->eagerFailed.end()) return nullptr;
+      if (eagerFailedBefore(comm, b)) return nullptr;
       RegAlloc* y = nullptr;
-      ncclResult_t res = regAcquire(comm, b, bytes, REF_EAGER, &y);
+      // a registration failing half way is retired, its peers' RELEASE sent by regProgress, not from here
+      ncclResult_t res = regAcquire(comm, b, bytes, REF_EAGER, &y, /*deferRelease=*/true);
       if (res != ncclSuccess) {
+        // not a plain device allocation (host-pinned, managed: hipMemGetAddressRange fails) or the export / an import
+        // failed: remembered, said once. Every rank must pass buffers of the same kind.
+        const std::pair<uint64_t, uint64_t> key = eagerKey(b);
         comm->eagerFailed.push_back(key);
-        WARN("rank %d: eager registration of allocation %lx failed (%d): this rank runs its collectives on it staged; "
-             "if its peers registered theirs, they stop with a kernel-mismatch error (NCCL_AMD_EAGER_REGISTER=0 on "
-             "every rank avoids it)", comm->rank, (unsigned long)key.first, (int)res);
+        WARN("rank %d: eager registration of the allocation holding %p failed (%d): this rank runs its collectives on "
+             "it staged; if its peers registered theirs, they stop with a kernel-mismatch error (pass device "
+             "allocations of the same kind on every rank, or NCCL_AMD_EAGER_REGISTER=0 on every rank)", comm->rank, b,
+             (int)res);
         return nullptr;
       }
       if ((int)comm->regs.size() > comm->tune.eagerMax && !comm->warnedEagerCap) {
@@ -561,6 +706,12 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
   const uint64_t use = ++comm->regClock;
   rr->lastUse = use;
   if (rs) rs->lastUse = use;
+  comm->regLastUse[0] = rs;
+  comm->regLastUse[1] = rr;
+  TRACE("rank %d: zero-copy on send %p (tag %lu) recv %p (tag %lu); in rank %d at %lx / %lx", comm->rank, send,
+        rs ? (unsigned long)rs->tag : 0ul, recv, (unsigned long)rr->tag, (comm->rank + 1) % comm->nRanks,
+        rs ? (unsigned long)(rs->rmt[(comm->rank + 1) % comm->nRanks] + ((uint64_t)send - rs->base)) : 0ul,
+        (unsigned long)(rr->rmt[(comm->rank + 1) % comm->nRanks] + ((uint64_t)recv - rr->base)));
   for (int r = 0; r < comm->nRanks; r++) {
     rmtSend[r] = send ? (const char*)(rs->rmt[r] + ((uint64_t)send - rs->base)) : nullptr;
     rmtRecv[r] = (char*)(rr->rmt[r] + ((uint64_t)recv - rr->base));
@@ -592,9 +743,10 @@ void windowsFree(ncclComm* comm, bool notifyPeers) {
   comm->regRetired.clear();
   for (RegAlloc* ra : comm->regs) {
     if (notifyPeers) regRelease(comm, ra);
-    else delete ra;
+    else regFree(ra);
   }
   comm->regs.clear();
+  comm->regLastUse[0] = comm->regLastUse[1] = nullptr;
 }
 
 }  // namespace ncclamd

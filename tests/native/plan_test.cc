@@ -76,7 +76,12 @@ void groupRecordError(ncclResult_t) {}
 void tunerPick(ncclComm*, CollFunc, size_t, int, int, int, int*, int* nch) { *nch = 0; }
 bool regCovers(ncclComm*, const void*, size_t) { return false; }
 ncclResult_t commCheck(const ncclComm*, const char*, const char*) { return ncclSuccess; }
+void commPollAsync(ncclComm*) {}
 void ipcDrainReleases() {}
+void ipcProgressReleases() {}
+void regProgress(ncclComm*) {}
+void regRecordUse(ncclComm*, const SymPlan&) {}
+void ipcNoteLaunch(hipStream_t, int) {}
 }  // namespace ncclamd
 
 using namespace ncclamd;

@@ -3,7 +3,8 @@ collectives are registered on first use — the allocation holding them is mappe
 (reference: IPC registration of a collective's buffers, src/register/coll_reg.cc:326-395; the read-mode P2P transport,
 src/transport/p2p.cc:326-343) — and the collective runs the zero-copy kernel that reads the peers' HBM. Results must be
 bit-identical to the oracle, also across free → re-allocate at the same address; the memory a peer's mapping keeps
-alive after the owner frees it is measured and must come back at the next blocking calls. Also the
+alive after the owner frees it is measured and must come back at the next collectives, with no blocking call
+(DESIGN.md §10.3), also in a loop that allocates, runs collectives and frees. Also the
 graph-registration retain failure path. Every rank is a process on the box's one GPU (dma-buf IPC)."""
 import os
 import re
@@ -19,9 +20,11 @@ pytestmark = pytest.mark.gpu
 MIB = 1 << 20
 
 
-def _eager_worker(rank, nranks, uid, q):
+def _eager_worker(rank, nranks, uid, q, fail_dmabuf_rank=-1):
     try:
         os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
+        if rank == fail_dmabuf_rank:  # this rank's dma-buf exports are refused: its peers open hipIpc handles
+            os.environ["NCCL_AMD_REG_FAIL_DMABUF"] = "1"
         logf = _trace_env(f"eager{nranks}")
         import torch
         import nccl_amd
@@ -87,7 +90,9 @@ def _eager_worker(rank, nranks, uid, q):
         s.synchronize()
         check("after re-allocation", y, oracle.all_reduce(ins, 7, 0))
         text2 = open(logf).read()[pos:]
-        restaged = "freed and re-allocated" in text2 and text2.count("registered allocation") == 1
+        # the stale registration is found by the lookup (regFind) or, first, by the collective path's upkeep (regProgress)
+        restaged = ("freed and re-allocated" in text2 or "retired (the allocation is gone)" in text2) and \
+            text2.count("registered allocation") == 1
         # small ops stay on their kernels: the one-shot / LL ranges are not registered
         pos = os.path.getsize(logf)
         comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), 1024, 7, 0, sp)
@@ -100,12 +105,14 @@ def _eager_worker(rank, nranks, uid, q):
         q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0, False, False, 0)))
 
 
-@pytest.mark.parametrize("nranks", [2, 3])
-def test_eager_zero_copy_multi_process(built, nranks):
+@pytest.mark.parametrize("nranks,fail_dmabuf_rank", [(2, -1), (3, -1), (2, 1), (3, 0)])
+def test_eager_zero_copy_multi_process(built, nranks, fail_dmabuf_rank):
     """Every AllReduce / ReduceScatter / AllGather of 12 MiB on plain torch allocations runs zero-copy, bit-exact vs
     the oracle; the allocations are registered once (four: x, y, the ReduceScatter and AllGather outputs), and a
-    freed and re-allocated buffer is registered again and stays bit-exact."""
-    res = _spawn(_eager_worker, nranks)
+    freed and re-allocated buffer is registered again and stays bit-exact. fail_dmabuf_rank: that rank's runtime
+    refuses every dma-buf export (NCCL_AMD_REG_FAIL_DMABUF=1, as seen in round 6's churn): its peers open hipIpc
+    handles of its allocations instead, and every rank still runs zero-copy (register.cc regCreate)."""
+    res = _spawn(_eager_worker, nranks, args=(fail_dmabuf_rank,))
     bad = [e for r in sorted(res) for e in res[r][0]]
     assert not bad, "\n".join(bad[:20])
     for r, (_, zc, regs, same_addr, restaged, small_zc) in res.items():
@@ -116,14 +123,17 @@ def test_eager_zero_copy_multi_process(built, nranks):
         assert small_zc == 0, f"rank {r}: a one-shot / LL-range op ran zero-copy"
 
 
-def _pinning_worker(rank, nranks, uid, q):
+def _pinning_worker(rank, nranks, uid, q, on_coll=True):
     """What a peer's mapping costs: rank r's 1 GiB pair is freed by its owner while the peers still map it, so the
-    device's free memory stays down until the owner's next blocking call (RELEASE to the peers) and the peers' next
-    blocking call (unmap). All ranks share the one GPU, so hipMemGetInfo sees every rank's memory."""
+    device's free memory stays down until the owner's next collective finds the freed allocation and sends RELEASE
+    (register.cc regProgress: its last kernel has completed) and the peers' next collective unmaps it (ipc.cc
+    ipcProgressReleases: none of the library's kernels in flight there). No blocking call is made.
+    All ranks share the one GPU, so hipMemGetInfo sees every rank's memory."""
     try:
         os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
-        # ADVICE r4: released peer mappings past this many bytes are reported once (ipc.cc releaseLater)
-        os.environ["NCCL_AMD_PENDING_RELEASE_WARN_BYTES"] = str(256 * MIB)
+        if not on_coll:  # the unmaps wait for a blocking call (ipc.cc); past this many bytes that is said once
+            os.environ["NCCL_AMD_RELEASE_ON_COLL"] = "0"
+            os.environ["NCCL_AMD_PENDING_RELEASE_WARN_BYTES"] = str(256 * MIB)
         logf = f"/tmp/nccl_amd_pinning_{os.getpid()}.log"
         os.environ["NCCL_DEBUG"] = "WARN"
         os.environ["NCCL_DEBUG_FILE"] = logf
@@ -135,13 +145,9 @@ def _pinning_worker(rank, nranks, uid, q):
         sp = s.cuda_stream
         tiny = torch.zeros(256, dtype=torch.float32, device="cuda")
 
-        def sync():  # a small (LL) AllReduce as a barrier across the processes
+        def sync():  # a small (LL) AllReduce as a barrier across the processes: a collective, not a blocking call
             comm.all_reduce_raw(tiny.data_ptr(), tiny.data_ptr(), 256, 7, 0, sp)
             s.synchronize()
-
-        def blocking_call():
-            h = comm.register_buffer(tiny.data_ptr(), tiny.numel() * 4)
-            comm.deregister_buffer(h)
 
         count = (512 * MIB) // 4
         torch.cuda.synchronize()
@@ -157,38 +163,110 @@ def _pinning_worker(rank, nranks, uid, q):
         del x, y
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        sync()
         time.sleep(0.2)
-        free1 = torch.cuda.mem_get_info()[0]
-        sync()
-        blocking_call()  # this rank's eager registrations of freed allocations: RELEASE to the peers
-        sync()
-        blocking_call()  # what the peers released: unmapped here
-        sync()
-        time.sleep(0.2)
-        free2 = torch.cuda.mem_get_info()[0]
-        sync()
+        free1 = torch.cuda.mem_get_info()[0]  # freed by both owners, still mapped by the peers
+        back = []
+        for _ in range(3):  # collectives only: each rank's releases go out, then the peers' mappings go
+            sync()
+            sync()
+            time.sleep(0.1)
+            back.append(torch.cuda.mem_get_info()[0])
+        if not on_coll:
+            h = comm.register_buffer(tiny.data_ptr(), tiny.numel() * 4)  # a blocking call: the unmaps
+            comm.deregister_buffer(h)
+            sync()
+            time.sleep(0.1)
+            back.append(torch.cuda.mem_get_info()[0])
         comm.destroy()
         warned = "still mapped in this process" in (open(logf).read() if os.path.exists(logf) else "")
-        q.put((rank, (ok, free0, free1, free2, warned)))
+        q.put((rank, (ok, free0, free1, back, warned)))
     except Exception as e:
-        q.put((rank, (False, repr(e), 0, 0, False)))
+        q.put((rank, (False, repr(e), 0, [], False)))
 
 
 def test_eager_registration_memory_pinning(built):
     """DESIGN.md §10.3's measured cost: with 2 ranks each freeing a 512 MiB send / receive pair (1 GiB per rank) that
-    the other maps, how much device memory stays held after the free, and that it all comes back after one blocking
-    call on each side."""
+    the other maps, how much device memory stays held after the free — and that it all comes back after the next
+    collectives on each side, with no blocking call."""
     res = _spawn(_pinning_worker, 2)
-    for r, (ok, free0, free1, free2, warned) in res.items():
+    for r, (ok, free0, free1, back, _) in res.items():
+        assert ok is True, f"rank {r}: {free0}"
+    free0, free1, back = res[0][1], res[0][2], res[0][3]
+    held = (free0 - free1) / (1 << 30)
+    print(f"eager pinning: {held:.3f} GiB held after both ranks freed 1 GiB each; free after each pair of collectives "
+          f"{[round(b / (1 << 30), 3) for b in back]} GiB (start {free0 / (1 << 30):.3f})")
+    assert held > 1.5, f"only {held:.3f} GiB held: the peers' mappings did not keep the freed pairs (test premise)"
+    assert back[-1] >= free0 - 256 * MIB, (free0, free1, back)
+
+
+def test_eager_release_left_to_blocking_calls(built):
+    """NCCL_AMD_RELEASE_ON_COLL=0: the peers' unmaps wait for a blocking call (the round-5 behaviour): the memory stays
+    held through collectives, the pending-release warning fires (ipc.cc releaseLater), and one blocking
+    call on each side returns it."""
+    res = _spawn(_pinning_worker, 2, args=(False,))
+    for r, (ok, free0, free1, back, warned) in res.items():
         assert ok is True, f"rank {r}: {free0}"
         assert warned, f"rank {r}: 1 GiB of released peer mappings pending without the warning"
-    free0, free1, free2 = res[0][1], res[0][2], res[0][3]
-    held = (free0 - free1) / (1 << 30)
-    back = (free2 - free1) / (1 << 30)
-    print(f"eager pinning: {held:.3f} GiB held after both ranks freed 1 GiB each; {back:.3f} GiB back after the "
-          f"blocking calls (free {free0 / (1 << 30):.2f} -> {free1 / (1 << 30):.2f} -> {free2 / (1 << 30):.2f} GiB)")
-    assert free2 >= free0 - 256 * MIB, (free0, free1, free2)
+    free0, free1, back = res[0][1], res[0][2], res[0][3]
+    assert back[-2] < free0 - (1 << 30), ("released on the collective path although NCCL_AMD_RELEASE_ON_COLL=0", back)
+    assert back[-1] >= free0 - 256 * MIB, (free0, free1, back)
+
+
+def _churn_worker(rank, nranks, uid, q):
+    """a loop that allocates, runs an eager collective and frees, issuing collectives only. Freed
+    registrations must be found and released on the collective path (regProgress), so memory held by the peers'
+    mappings stays bounded instead of growing with every iteration."""
+    try:
+        os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
+        import torch
+        import nccl_amd
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.Stream()
+        sp = s.cuda_stream
+        tiny = torch.zeros(256, dtype=torch.float32, device="cuda")
+
+        def sync():
+            comm.all_reduce_raw(tiny.data_ptr(), tiny.data_ptr(), 256, 7, 0, sp)
+            s.synchronize()
+
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        sync()
+        free0 = torch.cuda.mem_get_info()[0]
+        lows, ok = [], True
+        for it in range(8):  # 8 x 2 x 256 MiB per rank: 8 GiB over both ranks if nothing were released
+            count = (256 * MIB) // 4 + it * 1024  # a new allocation every time
+            x = torch.full((count,), float(it + 1), dtype=torch.float32, device="cuda")
+            y = torch.empty_like(x)
+            comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, sp)
+            s.synchronize()
+            ok = ok and bool((y == float(nranks * (it + 1))).all())
+            del x, y
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            sync()
+            lows.append(torch.cuda.mem_get_info()[0])
+        for _ in range(3):
+            sync()
+        time.sleep(0.1)
+        free1 = torch.cuda.mem_get_info()[0]
+        comm.destroy()
+        q.put((rank, (ok, free0, lows, free1)))
+    except Exception as e:
+        q.put((rank, (False, repr(e), [], 0)))
+
+
+def test_eager_registration_collective_only_churn(built):
+    res = _spawn(_churn_worker, 2)
+    for r, (ok, free0, lows, free1) in res.items():
+        assert ok is True, f"rank {r}: {free0}"
+    free0, lows, free1 = res[0][1], res[0][2], res[0][3]
+    held = [(free0 - lo) / (1 << 30) for lo in lows]
+    print(f"eager churn: GiB held after each iteration {[round(h, 3) for h in held]}; after 3 more collectives "
+          f"{(free0 - free1) / (1 << 30):.3f}")
+    assert max(held) < 2.5, held            # bounded: never more than the last couple of iterations' pairs
+    assert free1 >= free0 - 256 * MIB, (free0, free1)
 
 
 def _retain_fail_worker(rank, nranks, uid, q):

@@ -466,7 +466,8 @@ def _async_after_dereg_worker(rank, nranks, uid, q, tag):
     peer. Rank 0 issues AllReduce #1 (its kernel waits: rank 1 is deliberately late), rank 1 deregisters (its
     RELEASE request reaches rank 0's fd server), then rank 0 issues AllReduce #2. Round 3 unmapped the peer's
     buffer inside that call with a device-synchronising hipFree, so the call blocked until rank 1 arrived (the
-    late rank's delay); the unmapping now waits for rank 0's next blocking entry point (ipc.cc ipcDrainReleases)."""
+    late rank's delay); the unmapping now waits until none of the library's kernels is in flight when a collective is
+    issued (round 6, ipc.cc ipcProgressReleases: AllReduce #1 still is, so #2 leaves it) or for a blocking entry point."""
     try:
         os.environ["NCCL_AMD_SPIN_TIMEOUT_MS"] = "60000"
         os.environ["NCCL_PROTO"] = "^LL"

@@ -1,6 +1,6 @@
 """Build-time resource check of the channel kernels (no GPU): every collKernel / llKernel / symKernel
 instantiation must fit two 512-thread workgroups per CU (>= 4 waves per SIMD, <= 128 VGPRs) without
-spilling VGPRs to scratch. Several ranks on one GPU rely on it: the host plans up to 2 x CUs / ranksPerGPU channels
+spilling VGPRs to scratch. Several ranks on one GPU rely on it: the host plans up to CUs / ranksPerGPU channels
 per launch and every channel of every rank must be resident at once, or the ranks wait on each other
 forever (a 1-byte kernel at 256 VGPRs did exactly that before the kCoResident budget). The report comes
 from the compiler (-Rpass-analysis=kernel-resource-usage, written to build/<name>.usage by `make`)."""

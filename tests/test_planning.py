@@ -537,12 +537,14 @@ def test_size_table_bad_lines_are_ignored(exe, tmp_path):
                  "x 1K 1K 1K\n"         # not a rank count
                  "99 1K 1K 1K\n"        # out of range
                  "8 1Q 1K 1K\n"         # bad size
+                 "8 nan 1K 1K\n"        # not finite (strtod accepts it)
+                 "8 1K inf -\n"
                  "8 - - 512K\n")        # the one good row
     e = dict(NCCL_AMD_SIZE_TABLE=str(t), NCCL_DEBUG="WARN")
     assert plan(exe, 8, "ar", 7, (512 << 10) // 4, **e)["algo"] == "oneshot"
     assert plan(exe, 8, "ar", 7, (32 << 10) // 4, **e)["algo"] == "ll"          # built-in LL row kept
     out = subprocess.run([exe, "8", "ar", "7", "1000"], env=dict(os.environ, **e), capture_output=True, text=True)
-    assert out.stderr.count("line ignored") + out.stdout.count("line ignored") == 4, out.stdout + out.stderr
+    assert out.stderr.count("line ignored") + out.stdout.count("line ignored") == 6, out.stdout + out.stderr
     # an unreadable file: the built-in table, with a warning
     assert plan(exe, 8, "ar", 7, (256 << 10) // 4, NCCL_AMD_SIZE_TABLE=str(tmp_path / "none"))["algo"] == "oneshot"
 
