@@ -131,6 +131,8 @@ void ipcDrainReleases();
 void ipcProgressReleases();
 // after each kernel launch of a multi-process communicator (outside captures): the stream's tail event (ipc.cc)
 void ipcNoteLaunch(hipStream_t stream, int device);
+// none of this library's kernels in flight in this process (the streams ipcNoteLaunch tracks are idle)
+bool ipcLibraryIdle();
 // Held around this library's device allocations, imports and releases (ipc.cc gMapMu): no allocation of ours can
 // interleave with a mapping being torn down on another thread (a non-blocking init runs on its own thread).
 std::mutex& ipcMapMutex();
@@ -214,8 +216,19 @@ struct RegAlloc {
   // which this rank's kernel waits for), so its peers' mappings may go without waiting for the device (regProgress)
   hipEvent_t lastEv;
   bool evMissing;      // lastEv could not be created: released only at a blocking entry point (after a device wait)
+  int bouncePlans;     // a bounce allocation: planned collectives on it not launched yet (register.cc bounceFor)
 };
 enum RegRefKind { REF_LOCAL = 0, REF_GRAPH = 1, REF_EAGER = 2 };
+// An eager collective whose buffers this rank could not register runs on the communicator's bounce allocation
+// instead (register.cc bounceFor): its input copied in before the zero-copy kernel, its output copied out after.
+struct BounceCopy {
+  RegAlloc* ra;          // the bounce allocation's registration
+  const void* userSend;  // nullptr: nothing to copy in (AllGather reads its own input in place)
+  void* userRecv;
+  char* send;            // in the bounce allocation (this process's address)
+  char* recv;
+  size_t sendBytes, recvBytes;
+};
 struct RegHandle {  // what ncclCommRegister returns
   void* buff;
   size_t size;
@@ -353,6 +366,15 @@ struct ncclComm {
   uint64_t regGen = 0;       // this comm's identity for graph-release tokens (0 until the first graph hold)
   bool warnedEagerCap = false;
   std::vector<std::pair<uint64_t, uint64_t>> eagerFailed;  // (base, buffer id) whose eager registration failed
+  // the bounce allocation (register.cc bounceFor): registered with every peer once, grown on demand; grown-out ones
+  // are freed at the next blocking entry point. bounceEv follows its last copy-out (uses on different streams wait).
+  ncclamd::RegAlloc* bounce = nullptr;
+  void* bounceMem = nullptr;
+  hipEvent_t bounceEv = nullptr;
+  std::vector<std::pair<ncclamd::RegAlloc*, void*>> bounceOld;
+  bool bounceFailed = false;
+  ncclamd::BounceCopy bounceNext = {};  // regLookup's last result when it bounced (bounceUsed)
+  bool bounceUsed = false;
 
   std::vector<ncclamd::UserRedOp> userOps;
   std::atomic<int> asyncResult{ncclSuccess};
@@ -472,6 +494,8 @@ struct SymPlan {  // one symmetric (window) kernel launch
   hipStream_t stream;
   SymArgs args;
   RegAlloc* regUse[2];  // registered mode: the send / recv registrations it runs on (their lastEv, register.cc)
+  bool bounced;         // runs on the bounce allocation: `bounce` copies around the launch (bounceLaunch)
+  BounceCopy bounce;
 };
 ncclResult_t launchSymPlan(const SymPlan& plan);  // kernels.hip
 
@@ -505,6 +529,8 @@ void regBlockingPoint(ncclComm* comm);
 void regProgress(ncclComm* comm);
 // after a launched zero-copy plan: its registrations' lastEv recorded on its stream (outside captures)
 void regRecordUse(ncclComm* comm, const SymPlan& sp);
+// a zero-copy plan on the bounce allocation (sp.bounced): launched between its copy-in and copy-out (register.cc)
+ncclResult_t bounceLaunch(ncclComm* comm, const SymPlan& sp);
 // Set by ncclGroupSimulateEnd around its planning (group.cc): an eager lookup then registers nothing and reports the
 // zero-copy plan the real group end would take (register.cc regLookup).
 extern thread_local bool tPlanOnly;

@@ -904,6 +904,8 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
       sp.args.regMode = regMode;
       sp.regUse[0] = regMode == 1 ? comm->regLastUse[0] : nullptr;  // their lastEv follow this launch (regRecordUse)
       sp.regUse[1] = regMode == 1 ? comm->regLastUse[1] : nullptr;
+      sp.bounced = regMode == 1 && comm->bounceUsed;  // this rank's buffers go through the bounce allocation
+      if (sp.bounced) sp.bounce = comm->bounceNext;
       uintptr_t al = 0;
       for (int r = 0; r < n; r++) {
         sp.args.send[r] = sendPtr[r];
@@ -1008,7 +1010,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
     p.stream = sp.stream = comm->internalStream;
   }
   if (kind == PLAN_SYM) {
-    NCCLCHECK(launchSymPlan(sp));
+    NCCLCHECK(sp.bounced ? bounceLaunch(comm, sp) : launchSymPlan(sp));
     regRecordUse(comm, sp);
   } else {
     NCCLCHECK(launchPlan(p));
@@ -1086,7 +1088,7 @@ ncclResult_t launchBatch(std::vector<PlannedColl>& run) {
       noteLaunch(comm, p.stream);
       return ncclSuccess;
     }
-    NCCLCHECK(launchSymPlan(run[0].sp));
+    NCCLCHECK(run[0].sp.bounced ? bounceLaunch(comm, run[0].sp) : launchSymPlan(run[0].sp));
     regRecordUse(comm, run[0].sp);
     noteLaunch(comm, run[0].sp.stream);
     return ncclSuccess;

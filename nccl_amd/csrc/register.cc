@@ -192,6 +192,8 @@ static void regRelease(ncclComm* comm, RegAlloc* ra) {
   regFree(ra);
 }
 
+static thread_local bool tBounceCreate = false;  // regCreate of the bounce allocation (bounceFor)
+
 // Map the allocation [base, +size) into every peer process (same process: its own pointer). `deferRelease` (inside a
 // collective): a registration failing after some peers mapped it is retired, not released from here.
 static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint64_t id, RegAlloc** out,
@@ -220,7 +222,8 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
       break;
     }
     if (fd < 0 && !useHandle) {
-      const bool failAll = paramInt("NCCL_AMD_REG_FAIL_EXPORT", 0) != 0;  // tests: a registration failing on one rank
+      // tests: a registration failing on one rank (not the bounce allocation's: bounceFor)
+      const bool failAll = !tBounceCreate && paramInt("NCCL_AMD_REG_FAIL_EXPORT", 0) != 0;
       hipError_t e = failAll || paramInt("NCCL_AMD_REG_FAIL_DMABUF", 0)  // tests: the hipIpc fallback below
                          ? hipErrorInvalidValue
                          : ipcExportDmaBuf((void*)base, size, &fd);
@@ -458,6 +461,8 @@ static void regDrainGraphReleases(ncclComm* comm, bool defer) {
 // Eager registration (NCCL_AMD_EAGER_REGISTER=1; reference: IPC registration of a collective's buffers,
 // src/register/coll_reg.cc:326-395, which NCCL does on request or under capture): planColl decides which ops qualify
 // from what every rank shares (bytes, the size table), so every rank takes the same kernel. At blocking entry points:
+static void bounceFree(ncclComm* comm, bool all, bool notifyPeers);
+
 void regBlockingPoint(ncclComm* comm) {
   regDrainGraphReleases(comm, false);
   // eager cache upkeep: registrations whose allocation is gone go first (nothing of ours can use them: the range was
@@ -484,6 +489,7 @@ void regBlockingPoint(ncclComm* comm) {
     for (size_t i = 0; i < drop; i++) regPut(comm, eager[i], REF_EAGER, true);
     INFO("rank %d: %zu eager registrations released (cache bound %d)", comm->rank, drop, comm->tune.eagerMax);
   }
+  bounceFree(comm, /*all=*/false, /*notifyPeers=*/true);
   std::vector<RegAlloc*> retired;
   retired.swap(comm->regRetired);
   bool synced = false;
@@ -511,7 +517,7 @@ void regBlockingPoint(ncclComm* comm) {
 //    RELEASE now, at most four per call (one socket round trip per importing peer each); the peers unmap at their own
 //    next collective (ipcProgressReleases). A retired registration still in flight waits for a later call.
 void regProgress(ncclComm* comm) {
-  if (tPlanOnly || (comm->regs.empty() && comm->regRetired.empty())) return;
+  if (tPlanOnly || (comm->regs.empty() && comm->regRetired.empty() && comm->bounceOld.empty())) return;
   hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;  // event queries are not capture-safe in global mode
   (void)hipThreadExchangeStreamCaptureMode(&mode);
   uint64_t eagerBytes = 0;
@@ -544,6 +550,22 @@ void regProgress(ncclComm* comm) {
     if (dropped)
       INFO("rank %d: %zu eager registrations retired (cache bounds %d / %.1f GiB)", comm->rank, dropped,
            comm->tune.eagerMax, comm->tune.eagerMaxBytes / (double)(1ull << 30));
+  }
+  // grown-out bounce allocations (bounceFor): once no planned collective still names one, its last copy-out has
+  // completed and none of the library's kernels runs here (hipFree would wait for the device otherwise)
+  for (size_t i = 0; i < comm->bounceOld.size();) {
+    auto& x = comm->bounceOld[i];
+    if (x.first->bouncePlans > 0 || hipEventQuery(comm->bounceEv) != hipSuccess || !ipcLibraryIdle()) {
+      (void)hipGetLastError();
+      break;
+    }
+    TRACE("rank %d: grown-out bounce allocation %lx freed", comm->rank, (unsigned long)x.first->base);
+    regRelease(comm, x.first);
+    {
+      std::lock_guard<std::mutex> g(ipcMapMutex());
+      (void)hipFree(x.second);
+    }
+    comm->bounceOld.erase(comm->bounceOld.begin() + i);
   }
   int sent = 0;
   for (size_t i = 0; i < comm->regRetired.size() && sent < 4;) {
@@ -610,9 +632,122 @@ bool regCovers(ncclComm* comm, const void* p, size_t bytes) {
   return false;
 }
 
+// ---- the bounce allocation ----
+// An eager collective whose buffers this rank cannot register (the runtime refused the export — measured in round 6's
+// collective-only churn, DESIGN.md §10.3 — or host memory) would leave this rank on the staged kernel while its peers
+// run zero-copy: a kernel-mismatch error on every rank. It runs zero-copy on the bounce allocation instead: one
+// allocation of the library per communicator, registered with every peer once, the input copied in before the kernel
+// and the output copied out after, on the collective's stream (the kernel's DONE handshake: no peer reads it once this
+// rank's kernel has ended). The peers cannot tell. Grown on demand up to NCCL_AMD_EAGER_BOUNCE_MAX_BYTES (4 GiB);
+// beyond that, or when the bounce itself cannot be registered, the collective runs staged as before (said once).
+static bool bounceFor(ncclComm* comm, const void* send, size_t sendBytes, const void* recv, size_t recvBytes,
+                      const char** rmtSend, char** rmtRecv) {
+  static const uint64_t maxBytes = (uint64_t)paramInt("NCCL_AMD_EAGER_BOUNCE_MAX_BYTES", (int64_t)4 << 30);
+  const uint64_t sendLen = send ? (sendBytes + 4095) / 4096 * 4096 : 0;
+  const uint64_t need = sendLen + recvBytes;
+  if (comm->bounceFailed) return false;
+  if (need > maxBytes) {
+    WARN("rank %d: a collective of %zu + %zu bytes needs more than NCCL_AMD_EAGER_BOUNCE_MAX_BYTES=%lu of bounce "
+         "allocation: it runs staged on this rank", comm->rank, sendBytes, recvBytes, (unsigned long)maxBytes);
+    return false;
+  }
+  if (!comm->bounceEv && hipEventCreateWithFlags(&comm->bounceEv, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    comm->bounceEv = nullptr;
+    comm->bounceFailed = true;
+    WARN("rank %d: no event for the bounce allocation: eager collectives this rank cannot register run staged",
+         comm->rank);
+    return false;
+  }
+  if (!comm->bounce || comm->bounce->size < need) {
+    const uint64_t mib64 = (uint64_t)64 << 20;  // 64 MiB steps, at least doubling: few re-registrations
+    const uint64_t sz = std::min(std::max((need + mib64 - 1) / mib64 * mib64, comm->bounce ? 2 * comm->bounce->size : 0),
+                                 maxBytes);
+    if (comm->bounce) comm->bounceOld.push_back({comm->bounce, comm->bounceMem});  // planned ops may still use it
+    comm->bounce = nullptr;
+    comm->bounceMem = nullptr;
+    void* mem = nullptr;
+    RegAlloc* ra = nullptr;
+    hipError_t e;
+    {
+      std::lock_guard<std::mutex> g(ipcMapMutex());  // the library's allocations, imports and releases: one at a time
+      e = hipMalloc(&mem, sz);
+    }
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      comm->bounceFailed = true;
+      WARN("rank %d: bounce allocation of %lu MiB failed: eager collectives this rank cannot register run staged",
+           comm->rank, (unsigned long)(sz >> 20));
+      return false;
+    }
+    tBounceCreate = true;
+    const ncclResult_t res = regCreate(comm, (uint64_t)mem, sz, bufferIdOf(mem), &ra, /*deferRelease=*/true);
+    tBounceCreate = false;
+    if (res != ncclSuccess || !ra->usable) {
+      if (res == ncclSuccess) regFree(ra);
+      std::lock_guard<std::mutex> g(ipcMapMutex());
+      (void)hipFree(mem);  // a peer that mapped it before the failure keeps the memory until its RELEASE
+      comm->bounceFailed = true;
+      WARN("rank %d: the bounce allocation (%lu MiB) could not be registered (%d): eager collectives this rank cannot "
+           "register run staged", comm->rank, (unsigned long)(sz >> 20), (int)res);
+      return false;
+    }
+    comm->bounce = ra;
+    comm->bounceMem = mem;
+    INFO("rank %d: bounce allocation of %lu MiB registered with every peer (eager collectives on buffers this rank "
+         "cannot register)", comm->rank, (unsigned long)(sz >> 20));
+  }
+  RegAlloc* b = comm->bounce;
+  b->bouncePlans++;
+  BounceCopy& bc = comm->bounceNext;
+  bc.ra = b;
+  bc.userSend = send;
+  bc.userRecv = const_cast<void*>(recv);
+  bc.send = send ? (char*)b->base : nullptr;
+  bc.recv = (char*)(b->base + sendLen);
+  bc.sendBytes = send ? sendBytes : 0;
+  bc.recvBytes = recvBytes;
+  comm->bounceUsed = true;
+  for (int r = 0; r < comm->nRanks; r++) {
+    rmtSend[r] = send ? (const char*)b->rmt[r] : nullptr;
+    rmtRecv[r] = (char*)(b->rmt[r] + sendLen);
+  }
+  TRACE("rank %d: bounced zero-copy: send %p recv %p through %lx (+%lu)", comm->rank, send, recv,
+        (unsigned long)b->base, (unsigned long)sendLen);
+  return true;
+}
+
+ncclResult_t bounceLaunch(ncclComm* comm, const SymPlan& sp) {
+  const BounceCopy& b = sp.bounce;
+  b.ra->bouncePlans--;
+  HIPCHECK(hipStreamWaitEvent(sp.stream, comm->bounceEv, 0));  // a use on another stream is done with it
+  if (b.userSend) HIPCHECK(hipMemcpyAsync(b.send, b.userSend, b.sendBytes, hipMemcpyDefault, sp.stream));
+  NCCLCHECK(launchSymPlan(sp));
+  HIPCHECK(hipMemcpyAsync(b.userRecv, b.recv, b.recvBytes, hipMemcpyDefault, sp.stream));
+  HIPCHECK(hipEventRecord(comm->bounceEv, sp.stream));
+  return ncclSuccess;
+}
+
+// Grown-out bounce allocations (their last use done: a blocking point) and, at teardown, the current one.
+static void bounceFree(ncclComm* comm, bool all, bool notifyPeers) {
+  if (comm->bounceOld.empty() && !(all && comm->bounce)) return;
+  if (comm->bounceEv && notifyPeers) (void)hipEventSynchronize(comm->bounceEv);  // (abort: nothing waits)
+  if (all && comm->bounce) comm->bounceOld.push_back({comm->bounce, comm->bounceMem});
+  if (all) comm->bounce = nullptr, comm->bounceMem = nullptr;
+  for (auto& x : comm->bounceOld) {
+    if (notifyPeers) regRelease(comm, x.first);
+    else regFree(x.first);
+    std::lock_guard<std::mutex> g(ipcMapMutex());
+    (void)hipFree(x.second);
+  }
+  comm->bounceOld.clear();
+  if (all && comm->bounceEv) (void)hipEventDestroy(comm->bounceEv), comm->bounceEv = nullptr;
+}
+
 bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t sendBytes, const void* recv,
                size_t recvBytes, const char** rmtSend, char** rmtRecv, bool eager) {
   comm->regLastUse[0] = comm->regLastUse[1] = nullptr;
+  comm->bounceUsed = false;
   if (comm->nRanks == 1) return false;
   bool capturing = false;
   if (comm->tune.graphRegister || eager) {
@@ -664,7 +799,10 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     if (!rr || (send && !rs)) {
       if (!comm->regIpcAll) return false;  // registrations would stay local (regCreate): the staged plan
       // an allocation whose eager registration already failed runs staged at the real group end too
-      if ((send && !rs && eagerFailedBefore(comm, send)) || (!rr && eagerFailedBefore(comm, recv))) return false;
+      // (unless the bounce allocation takes it, as it does at the real group end: bounceFor)
+      if (comm->bounceFailed &&
+          ((send && !rs && eagerFailedBefore(comm, send)) || (!rr && eagerFailedBefore(comm, recv))))
+        return false;
       for (int r = 0; r < comm->nRanks; r++) rmtSend[r] = nullptr, rmtRecv[r] = nullptr;
       return true;
     }
@@ -701,6 +839,8 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
     else if (rs && !rs->eagerRef && rs->localRefs == 0) rs->eagerRef = true;  // a graph's registration, now cached
     if (!rr) rr = acquire(recv, recvBytes);
     else if (!rr->eagerRef && rr->localRefs == 0) rr->eagerRef = true;
+    // this rank could not register them: its peers run zero-copy all the same, so this rank does too, on the bounce
+    if ((!rr || (send && !rs)) && comm->regIpcAll) return bounceFor(comm, send, sendBytes, recv, recvBytes, rmtSend, rmtRecv);
   }
   if (!rr || (send && !rs)) return false;
   const uint64_t use = ++comm->regClock;
@@ -739,6 +879,7 @@ void windowsFree(ncclComm* comm, bool notifyPeers) {
   // left, and its ipcServerStop drops every mapping it held for us anyway), so a peer whose communicator lives on
   // does not keep this rank's registered allocations — graph auto-registrations included — mapped until then
   // (the reference drops them with the registration, src/register/register.cc). Abort sends nothing.
+  bounceFree(comm, /*all=*/true, notifyPeers);
   for (RegAlloc* ra : comm->regRetired) comm->regs.push_back(ra);
   comm->regRetired.clear();
   for (RegAlloc* ra : comm->regs) {

@@ -81,7 +81,9 @@ void ipcDrainReleases() {}
 void ipcProgressReleases() {}
 void regProgress(ncclComm*) {}
 void regRecordUse(ncclComm*, const SymPlan&) {}
+ncclResult_t bounceLaunch(ncclComm*, const SymPlan& sp) { return launchSymPlan(sp); }
 void ipcNoteLaunch(hipStream_t, int) {}
+bool ipcLibraryIdle() { return true; }
 }  // namespace ncclamd
 
 using namespace ncclamd;

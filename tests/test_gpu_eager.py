@@ -20,11 +20,13 @@ pytestmark = pytest.mark.gpu
 MIB = 1 << 20
 
 
-def _eager_worker(rank, nranks, uid, q, fail_dmabuf_rank=-1):
+def _eager_worker(rank, nranks, uid, q, fail_dmabuf_rank=-1, fail_export_rank=-1):
     try:
         os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
         if rank == fail_dmabuf_rank:  # this rank's dma-buf exports are refused: its peers open hipIpc handles
             os.environ["NCCL_AMD_REG_FAIL_DMABUF"] = "1"
+        if rank == fail_export_rank:  # no allocation of this rank can be registered: it runs on its bounce allocation
+            os.environ["NCCL_AMD_REG_FAIL_EXPORT"] = "1"
         logf = _trace_env(f"eager{nranks}")
         import torch
         import nccl_amd
@@ -74,6 +76,7 @@ def _eager_worker(rank, nranks, uid, q, fail_dmabuf_rank=-1):
         text = open(logf).read()[pos:]
         zc = len(_zero_copy_lines(logf, pos))
         regs = text.count("registered allocation")
+        bounced = text.count("bounced zero-copy")
         # free x and allocate the same size again: the caching allocator's segment goes back to the runtime and the
         # new one (usually at the same address) has another buffer id, so the stale registration is never used
         old_ptr = x.data_ptr()
@@ -93,6 +96,8 @@ def _eager_worker(rank, nranks, uid, q, fail_dmabuf_rank=-1):
         # the stale registration is found by the lookup (regFind) or, first, by the collective path's upkeep (regProgress)
         restaged = ("freed and re-allocated" in text2 or "retired (the allocation is gone)" in text2) and \
             text2.count("registered allocation") == 1
+        if rank == fail_export_rank:  # nothing of this rank's is registered: the new buffer goes through the bounce too
+            restaged = text2.count("bounced zero-copy") == 1 and "registered allocation" not in text2
         # small ops stay on their kernels: the one-shot / LL ranges are not registered
         pos = os.path.getsize(logf)
         comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), 1024, 7, 0, sp)
@@ -100,24 +105,32 @@ def _eager_worker(rank, nranks, uid, q, fail_dmabuf_rank=-1):
         s.synchronize()
         small_zc = len(_zero_copy_lines(logf, pos))
         comm.destroy()
-        q.put((rank, (errs, zc, regs, same_addr, restaged, small_zc)))
+        q.put((rank, (errs, zc, regs, same_addr, restaged, small_zc, bounced)))
     except Exception as e:
-        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0, False, False, 0)))
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, 0, False, False, 0, 0)))
 
 
-@pytest.mark.parametrize("nranks,fail_dmabuf_rank", [(2, -1), (3, -1), (2, 1), (3, 0)])
-def test_eager_zero_copy_multi_process(built, nranks, fail_dmabuf_rank):
+@pytest.mark.parametrize("nranks,fail_dmabuf_rank,fail_export_rank",
+                         [(2, -1, -1), (3, -1, -1), (2, 1, -1), (3, 0, -1), (2, 1, 1), (3, -1, 2)])
+def test_eager_zero_copy_multi_process(built, nranks, fail_dmabuf_rank, fail_export_rank):
     """Every AllReduce / ReduceScatter / AllGather of 12 MiB on plain torch allocations runs zero-copy, bit-exact vs
     the oracle; the allocations are registered once (four: x, y, the ReduceScatter and AllGather outputs), and a
     freed and re-allocated buffer is registered again and stays bit-exact. fail_dmabuf_rank: that rank's runtime
     refuses every dma-buf export (NCCL_AMD_REG_FAIL_DMABUF=1, as seen in round 6's churn): its peers open hipIpc
-    handles of its allocations instead, and every rank still runs zero-copy (register.cc regCreate)."""
-    res = _spawn(_eager_worker, nranks, args=(fail_dmabuf_rank,))
+    handles of its allocations instead, and every rank still runs zero-copy (register.cc regCreate).
+    fail_export_rank: no allocation of that rank can be registered at all (NCCL_AMD_REG_FAIL_EXPORT=1): it runs every
+    one of these collectives zero-copy on its bounce allocation (one registration, register.cc bounceFor) while its
+    peers run on their own buffers, still bit-exact — no kernel mismatch."""
+    res = _spawn(_eager_worker, nranks, args=(fail_dmabuf_rank, fail_export_rank))
     bad = [e for r in sorted(res) for e in res[r][0]]
     assert not bad, "\n".join(bad[:20])
-    for r, (_, zc, regs, same_addr, restaged, small_zc) in res.items():
+    for r, (_, zc, regs, same_addr, restaged, small_zc, bounced) in res.items():
         assert zc == 12, f"rank {r}: {zc} zero-copy plans for 12 eligible collectives"
-        assert regs == 4, f"rank {r}: {regs} registrations (want 4: one per allocation, once)"
+        if r == fail_export_rank:
+            assert regs == 1 and bounced == 12, f"rank {r}: {regs} registrations, {bounced} bounced (want 1, 12)"
+            assert restaged, f"rank {r}: the re-allocated buffer did not go through the bounce allocation"
+            continue
+        assert regs == 4 and bounced == 0, f"rank {r}: {regs} registrations (want 4: one per allocation, once)"
         if same_addr:
             assert restaged, f"rank {r}: the re-allocated buffer at the same address was not registered anew"
         assert small_zc == 0, f"rank {r}: a one-shot / LL-range op ran zero-copy"
@@ -215,9 +228,14 @@ def test_eager_release_left_to_blocking_calls(built):
 def _churn_worker(rank, nranks, uid, q):
     """a loop that allocates, runs an eager collective and frees, issuing collectives only. Freed
     registrations must be found and released on the collective path (regProgress), so memory held by the peers'
-    mappings stays bounded instead of growing with every iteration."""
+    mappings stays bounded instead of growing with every iteration. An allocation the runtime refuses to export
+    (measured in this very loop) goes through the rank's bounce allocation, so every iteration stays
+    zero-copy on every rank and correct; the bounce allocation itself stays (the library's cached memory)."""
     try:
         os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
+        logf = f"/tmp/nccl_amd_churn_{os.getpid()}.log"
+        os.environ["NCCL_DEBUG"] = "INFO"
+        os.environ["NCCL_DEBUG_FILE"] = logf
         import torch
         import nccl_amd
         torch.cuda.set_device(0)
@@ -252,21 +270,29 @@ def _churn_worker(rank, nranks, uid, q):
         time.sleep(0.1)
         free1 = torch.cuda.mem_get_info()[0]
         comm.destroy()
-        q.put((rank, (ok, free0, lows, free1)))
+        text = open(logf).read() if os.path.exists(logf) else ""
+        sizes = re.findall(r"bounce allocation of (\d+) MiB registered", text)
+        bounce = int(sizes[-1]) * MIB if sizes else 0
+        mismatch = "kernel mismatch" in text
+        q.put((rank, (ok and not mismatch, free0, lows, free1, bounce, text.count("eager registration of the allocation holding"))))
     except Exception as e:
-        q.put((rank, (False, repr(e), [], 0)))
+        q.put((rank, (False, repr(e), [], 0, 0, 0)))
 
 
 def test_eager_registration_collective_only_churn(built):
     res = _spawn(_churn_worker, 2)
-    for r, (ok, free0, lows, free1) in res.items():
+    for r, (ok, free0, *_rest) in res.items():
         assert ok is True, f"rank {r}: {free0}"
     free0, lows, free1 = res[0][1], res[0][2], res[0][3]
+    bounce = sum(v[4] for v in res.values())  # both ranks' bounce allocations (one GPU: mem_get_info sees both)
     held = [(free0 - lo) / (1 << 30) for lo in lows]
     print(f"eager churn: GiB held after each iteration {[round(h, 3) for h in held]}; after 3 more collectives "
-          f"{(free0 - free1) / (1 << 30):.3f}")
-    assert max(held) < 2.5, held            # bounded: never more than the last couple of iterations' pairs
-    assert free1 >= free0 - 256 * MIB, (free0, free1)
+          f"{(free0 - free1) / (1 << 30):.3f}; bounce allocations {bounce / (1 << 30):.3f} GiB, refused registrations "
+          f"{[v[5] for v in res.values()]}")
+    # bounded: never more than the last couple of iterations' pairs, plus the bounce allocations (and one grown-out
+    # bounce awaiting its free)
+    assert max(held) < 2.5 + 2 * bounce / (1 << 30), held
+    assert free1 >= free0 - 256 * MIB - bounce, (free0, free1, bounce)
 
 
 def _retain_fail_worker(rank, nranks, uid, q):
