@@ -55,6 +55,11 @@ def hbm_bytes_per_rank(coll: str, n: int, S: int, pull_gather: bool = True) -> i
         return 2 * S
     if coll == "allreduce":
         return int(3 * S + 2 * (n - 1) * S / n) if pull_gather else int(2 * S + 4 * (n - 1) * S / n)
+    if coll == "allreduce_zero_copy":
+        # symKernel on the ranks' own buffers (eager / registered): my input's S/n read for my block, its (n-1)/n S read
+        # by the peers, my block written (S/n) and read by the n-1 peers, the other parts written ((n-1)/n S):
+        # S + (2n-1)/n S = 3S - S/n (PMC at n = 2: 2.502 S, profiles/pmc_traffic.json)
+        return int(3 * S - S / n)
     raise ValueError(coll)
 
 
@@ -406,7 +411,9 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         for env in envs:
             for k in knobs:
                 os.environ.pop(k, None)
-            os.environ.update(env)
+            # every column but the eager one tunes the staged kernel: eager zero-copy (the multi-process default since
+            # round 6) would otherwise take these collectives and no staged knob would matter
+            os.environ.update({"NCCL_AMD_EAGER_REGISTER": "0", **env})
             comms.append(nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank)))
         for k, v in saved.items():
             os.environ.pop(k, None)
@@ -447,14 +454,17 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
             cm.destroy()
         out["staged_tuning"] = {"config": f"ncclAllReduce sum fp32, {S // MIB} MiB per rank, n={n}",
                                 "method": f"{reps} interleaved rounds (column order rotated per round), 10 AllReduces "
-                                          "per column per round, max over ranks; ms = median over rounds",
+                                          "per column per round, max over ranks; ms = median over rounds; every "
+                                          "column but NCCL_AMD_EAGER_REGISTER=1 runs the staged kernel "
+                                          "(NCCL_AMD_EAGER_REGISTER=0 added), 'default' = the staged defaults",
                                 "runs": tuning}
         dflt = tuning[0] if not envs[0] else None
         eager = next((r for r in tuning if r["env"] == {"NCCL_AMD_EAGER_REGISTER": "1"}), None)
         if eager is not None:  # the unregistered buffers of the headline, registered on first use
-            out["eager_zero_copy"] = {"env": "NCCL_AMD_EAGER_REGISTER=1", "ms": eager["ms"], "ms_min": eager["ms_min"],
-                                      "ms_max": eager["ms_max"], "busbw_GBps": eager["busbw_GBps"],
-                                      "default_ms": dflt["ms"] if dflt else None, "check": eager["check"]}
+            out["eager_zero_copy"] = {"env": "NCCL_AMD_EAGER_REGISTER=1 (the multi-process default)", "ms": eager["ms"],
+                                      "ms_min": eager["ms_min"], "ms_max": eager["ms_max"],
+                                      "busbw_GBps": eager["busbw_GBps"],
+                                      "staged_default_ms": dflt["ms"] if dflt else None, "check": eager["check"]}
         del xs, ys, ref
 
     if selected("xgmi_probe"):
@@ -835,16 +845,21 @@ def main(argv=None):
 
     ms_per_step = wall / args.steps * 1e3
     value, algbw, busbw = rates(n, S, ms_per_step)
-    hbm_bytes = hbm_bytes_per_rank("allreduce", n, S, pull_gather=os.environ.get("NCCL_AMD_AG_PULL", "1") != "0")
     probe_links = n > 1 and torch.cuda.device_count() >= n  # ranks on separate GPUs: links exist to measure
     # the dominant (only) kernel of a step: the first one this process launched (warm-up of the same call)
     kernels = launched_kernels(klog)
     kname = kernels[0] if kernels else None
+    zero_copy = bool(kname and "symKernel" in kname)  # eager zero-copy (the multi-process default) or staged
+    if n > 1 and zero_copy:
+        workload = (f"ncclAllReduce sum fp32, {size_mib} MiB per rank, {n}xMI355X zero-copy (the ranks' buffers "
+                    "registered on first use, DESIGN.md §10.3)")
+    hbm_bytes = hbm_bytes_per_rank("allreduce_zero_copy" if zero_copy else "allreduce", n, S,
+                                   pull_gather=os.environ.get("NCCL_AMD_AG_PULL", "1") != "0")
     # launch_avg_ms: HIP events on the launch stream around the K back-to-back launches of the timed loop / K
     # (one launch per step; the rocprofv3 kernel average in profiles/ is the cross-check)
     launch_ms = gpu_ms
     hbm_rate = hbm_bytes / (launch_ms * 1e-3) / 1e9
-    wkey = f"allreduce_f32_{size_mib}MiB_n{n}"
+    wkey = f"allreduce_f32_{size_mib}MiB_n{n}" + ("_eager" if zero_copy else "")
     traffic = load_pmc(wkey)
     traffic_src = "profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, bytes/launch)" if traffic else None
     if n == 1:

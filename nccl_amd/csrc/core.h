@@ -387,6 +387,7 @@ struct ncclComm {
   // every rank can map every other-process peer's registered buffers (each such peer runs an fd server): derived
   // from the shared peer table at init, so every rank takes the same registered / staged decision (register.cc)
   bool regIpcAll = false;
+  bool multiProcess = false;  // some peer lives in another process (shared peer table: the same on every rank)
   uint64_t endMagic;
 };
 

@@ -236,9 +236,13 @@ void loadTuning(CommTuning* t) {
   t->graphRegister = (int)paramInt("NCCL_GRAPH_REGISTER", 1);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
   // Eager registration (register.cc regLookup): collectives of at least eagerBytes whose staged plan would be direct
-  // register their unregistered allocations on first use and run the zero-copy kernel. Opt-in: a
-  // peer's mapping keeps a freed allocation's memory until this rank's next blocking call releases it.
-  t->eagerRegister = (int)paramInt("NCCL_AMD_EAGER_REGISTER", 0);
+  // register their unregistered allocations on first use and run the zero-copy kernel. Default
+  // (-1): on for communicators spanning processes whose peers all serve registrations (eagerOn) — one-GPU rehearsal
+  // 0.209 / 1.014 / 1.143 ms vs 0.302 / 1.579 / 1.514 ms staged at n = 2 / 4 / 8 (2.50 S vs 4.0 S of HBM per rank at n = 2
+  // by PMC). Since round 6 its costs are bounded without a blocking call: freed allocations are found and released on
+  // the collective path, and an allocation this rank cannot register runs through the bounce allocation. 0: staged;
+  // 1: on for every communicator (one process too).
+  t->eagerRegister = (int)paramInt("NCCL_AMD_EAGER_REGISTER", -1);
   t->eagerBytes = paramInt("NCCL_AMD_EAGER_REGISTER_BYTES", 1 << 20);
   t->eagerMax = (int)paramInt("NCCL_AMD_EAGER_REGISTER_MAX", 64);
   if (t->eagerMax < 1) t->eagerMax = 1;
@@ -673,6 +677,12 @@ bool llPlan(const CollInfo& info, LLOp* op) {
 
 // Plan one op: the kernel launch (PLAN_KERNEL, in p), the symmetric-window launch (PLAN_SYM, in sp) or
 // nothing (PLAN_NONE). Every rank derives the same plan from what all ranks share.
+// Eager zero-copy for this communicator (NCCL_AMD_EAGER_REGISTER: 1 always, 0 never, default when it spans processes
+// whose every peer serves registrations). Every rank computes the same answer from the shared peer table.
+static bool eagerOn(const ncclComm* comm) {
+  return comm->tune.eagerRegister > 0 || (comm->tune.eagerRegister < 0 && comm->multiProcess && comm->regIpcAll);
+}
+
 ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kind) {
   ncclComm* comm = info.comm;
   const int ts = typeSize(info.datatype);
@@ -886,7 +896,7 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
                          info.recvbuff, rb, sendPtr, recvPtr,
                          // eager registration (NCCL_AMD_EAGER_REGISTER=1): ops of at least eagerBytes whose staged
                          // plan would be the direct kernel, decided from what every rank shares (bytes, the table)
-                         comm->tune.eagerRegister && !oneShotAR && std::max(sb, rb) >= (size_t)comm->tune.eagerBytes)) {
+                         eagerOn(comm) && !oneShotAR && std::max(sb, rb) >= (size_t)comm->tune.eagerBytes)) {
       regMode = 1;  // my buffers as mapped in each peer; the kernel exchanges them at entry
       if (info.func == FUNC_ALLGATHER) sendPtr[comm->rank] = (const char*)info.sendbuff;
     }

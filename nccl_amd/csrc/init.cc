@@ -161,6 +161,8 @@ static void computeChannelCap(ncclComm* c) {
   for (size_t i = 0; i < c->peers.size(); i++)
     for (size_t j = 0; j < c->peers.size(); j++)
       if (c->peers[i].pid != c->peers[j].pid && c->peers[j].fdServer[0] == 0) c->regIpcAll = false;
+  c->multiProcess = false;
+  for (size_t i = 1; i < c->peers.size(); i++) c->multiProcess = c->multiProcess || c->peers[i].pid != c->peers[0].pid;
 }
 
 // Which HIP runtime this process bound (reference: init-time INFO lines, src/init.cc:1831-1968): in a torch

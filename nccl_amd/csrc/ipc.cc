@@ -702,33 +702,6 @@ static bool closeIfMine(int fd, uint64_t dev, uint64_t ino) {
   return mine;
 }
 
-// The virtual range an unmapped dma-buf import occupied, reserved (no memory behind it) for the life of the process
-// so that no later allocation of this process lands on it (NCCL_AMD_HOLD_UNMAPPED_VA, default 1). Measured round 6
-// (tests/test_gpu_eager.py churn test, TRACE logs): with peers' mappings unmapped promptly, PyTorch's allocator handed
-// out ranges overlapping a just-unmapped import, and the runtime then refused to export that allocation (dma-buf and
-// hipIpc handle alike, "invalid argument"), while allocations elsewhere exported fine. Only address space is held;
-// the HBM is returned by the unmap.
-static size_t gHeldVa = 0, gHeldVaBytes = 0;
-static void holdVa(void* ptr, size_t size) {  // caller holds gMapMu
-  static const bool on = paramInt("NCCL_AMD_HOLD_UNMAPPED_VA", 1) != 0;
-  if (!on || !ptr || !size) return;
-  const size_t gran = (size_t)2 << 20;
-  const size_t len = (size + gran - 1) / gran * gran;
-  void* r = nullptr;
-  hipError_t e = hipMemAddressReserve(&r, len, 0, ptr, 0);
-  if (e != hipSuccess || r != ptr) {
-    if (e == hipSuccess) (void)hipMemAddressFree(r, len);
-    (void)hipGetLastError();
-    TRACE("ipc: could not hold the unmapped range %p (+%zu MiB): %s", ptr, len >> 20,
-          e != hipSuccess ? hipGetErrorString(e) : "reserved elsewhere");
-    return;
-  }
-  ++gHeldVa;
-  gHeldVaBytes += len;
-  TRACE("ipc: holding the unmapped range %p (+%zu MiB), %zu ranges / %zu GiB of address space held", ptr, len >> 20,
-        gHeldVa, gHeldVaBytes >> 30);
-}
-
 static ncclResult_t importLegacy(const IpcDesc& d, IpcImport* out) {
   std::lock_guard<std::mutex> g(gMapMu);
   HIPCHECK(hipIpcOpenMemHandle(&out->ptr, d.handle, hipIpcMemLazyEnablePeerAccess));
@@ -832,7 +805,6 @@ static void releaseLocked(IpcImport* m) {  // caller holds gMapMu
     (void)hipDestroyExternalMemory((hipExternalMemory_t)m->ext);
     const bool closed = closeIfMine(m->fd, m->fdDev, m->fdIno);
     TRACE("ipc: released mapping (fd %d %s)", m->fd, closed ? "still open: closed it" : "closed by the runtime");
-    holdVa(m->ptr, m->size);
   }
   memset(m, 0, sizeof(*m));
 }

@@ -230,10 +230,10 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
       if (e != hipSuccess) {
         (void)hipGetLastError();
         // The runtime sometimes refuses the dma-buf export of a fresh allocation ("invalid argument"; round 6's eager
-        // churn: an allocation over the range of one just freed and released), as it once refused a
-        // fresh slab's (ipc.cc ipcExport). A registration failing on one rank only makes the ranks run different
-        // kernels, so — as for the slab — its peers open a hipIpc handle instead where the runtime can (below 2 GiB,
-        // or a 7.2+ runtime).
+        // churn, DESIGN.md §10.3: a re-allocation at the address of a just-freed registered allocation whose peers were
+        // unmapping the old one), as it once refused a fresh slab's (ipc.cc ipcExport). Its peers then open a hipIpc
+        // handle instead where the runtime gives one (below 2 GiB, or a 7.2+ runtime); where it refuses that too, the
+        // eager path runs the collective on the bounce allocation (bounceFor).
         {
           std::lock_guard<std::mutex> g(ipcMapMutex());
           useHandle = !failAll && ipcLegacyAllowed(hipRuntimeInfo().version, size, false) &&

@@ -36,8 +36,8 @@ def main():
         os.environ.update(NCCL_ALGO="RING", NCCL_AMD_REF_NCHANNELS="32")
     if mode == "reforder":
         os.environ.update(NCCL_AMD_REF_ORDER="1", NCCL_AMD_REF_NCHANNELS="32")
-    if mode == "eager":
-        os.environ.update(NCCL_AMD_EAGER_REGISTER="1")
+    # the staged kernel unless the mode says otherwise (eager zero-copy is the multi-process default since round 6)
+    os.environ.update(NCCL_AMD_EAGER_REGISTER="1" if mode == "eager" else "0")
     if mode == "push":
         os.environ.update(NCCL_AMD_AG_PULL="0")
     n = int(os.environ.get("NRANKS", "2"))

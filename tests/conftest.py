@@ -8,6 +8,12 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# The GPU tests of the staged kernels spawn multi-process communicators, where eager zero-copy is the default since
+# round 6: they keep testing what they name. The eager tests set it on explicitly, and the default
+# itself is tested with the variable removed (tests/test_gpu_eager.py, tests/test_gpu_bench.py).
+os.environ.setdefault("NCCL_AMD_EAGER_REGISTER", "0")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu on the GPU box)")
 

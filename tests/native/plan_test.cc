@@ -142,6 +142,8 @@ int main(int argc, char** argv) {
   if (comm.slotBytes < ((size_t)16 << 10)) comm.slotBytes = (size_t)16 << 10;
   comm.chanCap = !batch && argc > 6 ? atoi(argv[6]) : 256;
   comm.devComm = (DevComm*)0x1000;
+  // PLAN_MULTIPROCESS=1: the peers live in other processes, every one serving registrations (init.cc)
+  comm.multiProcess = comm.regIpcAll = getenv("PLAN_MULTIPROCESS") && atoi(getenv("PLAN_MULTIPROCESS"));
   loadTuning(&comm.tune);
   resolveLinkChannels(&comm.tune, n, getenv("NCCL_MAX_CTAS") != nullptr);
   if (batch) {

@@ -24,6 +24,7 @@ def _free_port():
 
 def test_bench_two_ranks_quick(built):
     env = dict(os.environ, NCCL_AMD_SPIN_TIMEOUT_MS="20000")
+    env.pop("NCCL_AMD_EAGER_REGISTER", None)  # the library's defaults, as the driver runs it
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--quick-suite", "--cpu-seconds", "1"]
@@ -42,7 +43,10 @@ def test_bench_two_ranks_quick(built):
     assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
     assert 0.5 < roof["achieved"] / d["busbw_GBps"] < 2.0   # per-launch event time vs the whole step's wall time
     assert "hbm" in roof and roof["hbm"]["peak"] == 8000.0
-    assert roof["kernel"] and "ncclamd::collKernel<float, 0, 0>" in roof["kernel"], roof["kernel"]
+    # two processes: eager zero-copy by default (round 6), its HBM model and PMC entry
+    assert roof["kernel"] and "ncclamd::symKernel" in roof["kernel"], roof["kernel"]
+    assert "zero-copy" in d["config"]["workload"], d["config"]
+    assert roof["hbm"]["algorithmic_bytes_per_launch"] == int(2.5 * 256 * 2**20), roof["hbm"]
     # every N line carries the host-core baseline (rank 0, same run) and the PMC traffic
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1, d["cpu_baseline"]
     assert roof["traffic"] and roof["traffic"] > 0, roof

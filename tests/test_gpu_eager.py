@@ -136,6 +136,47 @@ def test_eager_zero_copy_multi_process(built, nranks, fail_dmabuf_rank, fail_exp
         assert small_zc == 0, f"rank {r}: a one-shot / LL-range op ran zero-copy"
 
 
+def _default_worker(rank, nranks, uid, q):
+    """The library's default (NCCL_AMD_EAGER_REGISTER unset): a communicator spanning processes runs an eligible
+    collective on the ranks' own buffers (round 6)."""
+    try:
+        os.environ.pop("NCCL_AMD_EAGER_REGISTER", None)
+        logf = _trace_env(f"eagerdefault{nranks}")
+        import torch
+        import nccl_amd
+        import oracle
+        from tests import gpu_cases as G
+        torch.cuda.set_device(0)
+        comm = nccl_amd.Communicator.init(nranks, rank, uid)
+        s = torch.cuda.Stream()
+        count = 3 << 20
+        x = torch.empty(count, dtype=torch.float32, device="cuda")
+        y = torch.empty(count, dtype=torch.float32, device="cuda")
+        pos = os.path.getsize(logf) if os.path.exists(logf) else 0
+        errs = []
+        for it in range(2):
+            ins = G.make_inputs(nranks, 7, count, seed=930 + it)
+            x.copy_(torch.from_numpy(ins[rank]))
+            torch.cuda.synchronize()
+            comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+            s.synchronize()
+            if comm.async_error() or not G.same_bits(y.cpu().numpy(), oracle.all_reduce(ins, 7, 0), 7):
+                errs.append(f"rank {rank} round {it}: differs (async {comm.async_error()})")
+        zc = len(_zero_copy_lines(logf, pos))
+        comm.destroy()
+        q.put((rank, (errs, zc)))
+    except Exception as e:
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0)))
+
+
+def test_eager_zero_copy_is_the_multi_process_default(built):
+    res = _spawn(_default_worker, 2)
+    bad = [e for r in sorted(res) for e in res[r][0]]
+    assert not bad, "\n".join(bad)
+    for r, (_, zc) in res.items():
+        assert zc == 2, f"rank {r}: {zc} zero-copy plans of 2 (default: eager zero-copy across processes)"
+
+
 def _pinning_worker(rank, nranks, uid, q, on_coll=True):
     """What a peer's mapping costs: rank r's 1 GiB pair is freed by its owner while the peers still map it, so the
     device's free memory stays down until the owner's next collective finds the freed allocation and sends RELEASE
