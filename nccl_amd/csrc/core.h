@@ -468,7 +468,7 @@ ncclResult_t enqueueCheck(CollInfo* info);
 // plan + launch (enqueue.cc); forkJoin=false: the caller (group end) forks/joins shared-GPU comms itself
 ncclResult_t launchColl(const CollInfo& info, bool forkJoin = true);
 ncclResult_t collFork(const CollInfo& info);
-void collProgress(ncclComm* comm);  // enqueue.cc: registration / release upkeep on the collective path, never waiting
+void collProgress(ncclComm* comm, hipStream_t stream);  // enqueue.cc: registration / release upkeep on the collective path, never waiting
 bool llPlan(const CollInfo& info, LLOp* op);                  // LL eligibility + plan (enqueue.cc)
 
 // ---------------------------------------------------------------- tuner plugin (reference src/plugin/tuner.cc)

@@ -1007,7 +1007,7 @@ ncclResult_t launchColl(const CollInfo& info, bool forkJoin) {
   LaunchPlan p;
   SymPlan sp;
   int kind;
-  collProgress(comm);
+  collProgress(comm, info.stream);
   NCCLCHECK(planColl(info, p, sp, &kind));
   if (kind == PLAN_NONE) return ncclSuccess;
   NCCLCHECK(checkGrid(comm, kind, p, sp));
@@ -1044,7 +1044,15 @@ static void noteLaunch(ncclComm* comm, hipStream_t stream) {
 
 // Upkeep on the collective path, before anything of this collective is planned or launched, never waiting (VERDICT r5
 // item 4): this rank's registrations (register.cc regProgress) and the peers' mappings they released (ipc.cc).
-void collProgress(ncclComm* comm) {
+// Never while `stream` is being captured: an unmap or free there would invalidate the capture (measured round 6,
+// test_graph_registrations_released_with_their_graph: hipErrorStreamCaptureInvalidated); the next collective outside
+// a capture, or a blocking call, does it instead.
+void collProgress(ncclComm* comm, hipStream_t stream) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone) {
+    (void)hipGetLastError();
+    return;
+  }
   regProgress(comm);
   ipcProgressReleases();
 }

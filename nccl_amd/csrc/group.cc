@@ -155,14 +155,22 @@ ncclResult_t groupEndInternal(ncclSimInfo_t* simInfo) {
   }
   int dev = 0;
   (void)hipGetDevice(&dev);
-  // each communicator's upkeep first, before any of the group's kernels is launched (enqueue.cc collProgress)
+  // each communicator's upkeep first, before any of the group's kernels is launched (enqueue.cc collProgress; not
+  // while any of its streams in this group is being captured)
   for (size_t i = 0; i < colls.size(); i++) {
     bool seen = false;
     for (size_t j = 0; j < i && !seen; j++) seen = colls[j].comm == colls[i].comm;
-    if (!seen) {
-      (void)hipSetDevice(colls[i].comm->device);
-      collProgress(colls[i].comm);
+    if (seen) continue;
+    bool capturing = false;
+    for (size_t j = i; j < colls.size() && !capturing; j++) {
+      if (colls[j].comm != colls[i].comm) continue;
+      hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+      capturing = hipStreamIsCapturing(colls[j].stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone;
+      (void)hipGetLastError();
     }
+    if (capturing) continue;
+    (void)hipSetDevice(colls[i].comm->device);
+    collProgress(colls[i].comm, colls[i].stream);
   }
   ncclResult_t r = ncclSuccess;
   for (size_t i = 0; i < colls.size() && r == ncclSuccess; i++) r = collFork(colls[i]);

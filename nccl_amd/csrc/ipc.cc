@@ -491,6 +491,25 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested) {
 // "invalid argument" — 5 of 24 registrations in 8 iterations, always beside a concurrent import — and a plain
 // export / import / unmap cycle of the same buffers without that concurrency never failed (scripts/eager_churn_probe.py,
 // tests/native/reuse_probe.hip: 0 of 80). A failure is retried (1, 2, 4, 8 ms apart, the lock released meanwhile).
+//
+// Every dma-buf this process exported is remembered by its inode (the dma-buf file's identity; the kernel numbers them
+// in increasing order, one per dma-buf created). Measured in round 6 (the eager churn inside the full GPU suite,
+// gpurun_out TRACE logs): a rank exported its send and then its receive allocation, and the peer received the SAME
+// dma-buf for both (one inode, two registrations) — the receive allocation's export had handed back an existing
+// dma-buf, and the peer's zero-copy kernel read the send buffer as the receive one: silently wrong results. An export
+// whose dma-buf was exported before is therefore refused here (the caller falls back as for any refused export).
+// (A dma-buf handed back again for the same allocation — same base, same buffer id — is fine.)
+static std::map<std::pair<uint64_t, uint64_t>, std::pair<uint64_t, uint64_t>> gExported;  // (dev, ino) -> (base, id)
+
+static uint64_t allocationId(void* p) {
+  unsigned long long id = 0;
+  if (hipPointerGetAttribute(&id, HIP_POINTER_ATTRIBUTE_BUFFER_ID, (hipDeviceptr_t)p) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (uint64_t)id;
+}
+
 hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd) {
   hipError_t e = hipErrorInvalidValue;
   for (int attempt = 0; attempt < 5; attempt++) {
@@ -498,6 +517,26 @@ hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd) {
     std::lock_guard<std::mutex> g(gMapMu);
     e = hipMemGetHandleForAddressRange(fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
     if (e == hipSuccess) {
+      struct stat st;
+      if (fstat(*fd, &st) != 0) {
+        WARN("ipc: dma-buf export of %p (+%zu MiB) returned fd %d, which fstat refuses: %s", base, size >> 20, *fd,
+             strerror(errno));
+        *fd = -1;
+        return hipErrorInvalidValue;
+      }
+      const std::pair<uint64_t, uint64_t> key((uint64_t)st.st_dev, (uint64_t)st.st_ino);
+      const std::pair<uint64_t, uint64_t> who((uint64_t)base, allocationId(base));
+      auto it = gExported.find(key);
+      if (it != gExported.end() && it->second != who) {
+        // not ours to close: the number may be the runtime's, or another export's still in flight
+        WARN("ipc: dma-buf export of %p (+%zu MiB) handed back fd %d = dma-buf ino %lu, exported before for %lx: "
+             "refused (it would map the other allocation)", base, size >> 20, *fd, (unsigned long)st.st_ino,
+             (unsigned long)it->second.first);
+        *fd = -1;
+        return hipErrorInvalidValue;
+      }
+      gExported[key] = who;
+      TRACE("ipc: exported %p (+%zu MiB) as fd %d, dma-buf ino %lu", base, size >> 20, *fd, (unsigned long)st.st_ino);
       if (attempt) INFO("ipc: dma-buf export of %p (+%zu MiB) succeeded at attempt %d", base, size >> 20, attempt + 1);
       return e;
     }

@@ -231,12 +231,17 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
         (void)hipGetLastError();
         // The runtime sometimes refuses the dma-buf export of a fresh allocation ("invalid argument"; round 6's eager
         // churn, DESIGN.md §10.3: a re-allocation at the address of a just-freed registered allocation whose peers were
-        // unmapping the old one), as it once refused a fresh slab's (ipc.cc ipcExport). Its peers then open a hipIpc
-        // handle instead where the runtime gives one (below 2 GiB, or a 7.2+ runtime); where it refuses that too, the
-        // eager path runs the collective on the bounce allocation (bounceFor).
+        // unmapping the old one), or hands back a dma-buf it exported before (refused by ipcExportDmaBuf), as it once
+        // refused a fresh slab's (ipc.cc ipcExport). An explicit registration's peers then open a hipIpc handle instead
+        // where the runtime gives one (below 2 GiB, or a 7.2+ runtime); the eager path runs the collective on the
+        // bounce allocation (bounceFor).
         {
           std::lock_guard<std::mutex> g(ipcMapMutex());
-          useHandle = !failAll && ipcLegacyAllowed(hipRuntimeInfo().version, size, false) &&
+          // not for the eager path's user allocations (deferRelease): those run on the bounce allocation instead,
+          // which needs no handle of a range the runtime just refused (§10.3: its exports are not to be trusted); the
+          // bounce allocation itself (the library's own) may go by handle
+          useHandle = !failAll && (!deferRelease || tBounceCreate) &&
+                      ipcLegacyAllowed(hipRuntimeInfo().version, size, false) &&
                       hipIpcGetMemHandle(&handle, (void*)base) == hipSuccess;
         }
         (void)hipGetLastError();

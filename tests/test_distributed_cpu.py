@@ -71,6 +71,9 @@ def test_rates():
     for n in (2, 4, 8):
         got = pmc[f"allreduce_f32_256MiB_n{n}"]["bytes_per_launch"]
         assert abs(got / bench.hbm_bytes_per_rank("allreduce", n, S) - 1) < 0.01, (n, got)
+        # eager zero-copy (the multi-process default since round 6): 3S - S/n
+        got = pmc[f"allreduce_f32_256MiB_n{n}_eager"]["bytes_per_launch"]
+        assert abs(got / bench.hbm_bytes_per_rank("allreduce_zero_copy", n, S) - 1) < 0.01, (n, got)
     assert bench.bus_factor("reducescatter", 4) == 0.75 and bench.bus_factor("reduce", 4) == 1.0
 
 

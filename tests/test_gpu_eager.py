@@ -96,7 +96,7 @@ def _eager_worker(rank, nranks, uid, q, fail_dmabuf_rank=-1, fail_export_rank=-1
         # the stale registration is found by the lookup (regFind) or, first, by the collective path's upkeep (regProgress)
         restaged = ("freed and re-allocated" in text2 or "retired (the allocation is gone)" in text2) and \
             text2.count("registered allocation") == 1
-        if rank == fail_export_rank:  # nothing of this rank's is registered: the new buffer goes through the bounce too
+        if rank in (fail_export_rank, fail_dmabuf_rank):  # nothing of this rank's registered: the bounce again
             restaged = text2.count("bounced zero-copy") == 1 and "registered allocation" not in text2
         # small ops stay on their kernels: the one-shot / LL ranges are not registered
         pos = os.path.getsize(logf)
@@ -116,17 +116,17 @@ def test_eager_zero_copy_multi_process(built, nranks, fail_dmabuf_rank, fail_exp
     """Every AllReduce / ReduceScatter / AllGather of 12 MiB on plain torch allocations runs zero-copy, bit-exact vs
     the oracle; the allocations are registered once (four: x, y, the ReduceScatter and AllGather outputs), and a
     freed and re-allocated buffer is registered again and stays bit-exact. fail_dmabuf_rank: that rank's runtime
-    refuses every dma-buf export (NCCL_AMD_REG_FAIL_DMABUF=1, as seen in round 6's churn): its peers open hipIpc
-    handles of its allocations instead, and every rank still runs zero-copy (register.cc regCreate).
-    fail_export_rank: no allocation of that rank can be registered at all (NCCL_AMD_REG_FAIL_EXPORT=1): it runs every
-    one of these collectives zero-copy on its bounce allocation (one registration, register.cc bounceFor) while its
-    peers run on their own buffers, still bit-exact — no kernel mismatch."""
+    refuses every dma-buf export (NCCL_AMD_REG_FAIL_DMABUF=1, as seen in round 6's churn) and fail_export_rank: no
+    allocation of that rank can be registered at all (NCCL_AMD_REG_FAIL_EXPORT=1). Either way that rank runs every one
+    of these collectives zero-copy on its bounce allocation (one registration, register.cc bounceFor; the eager path
+    takes no hipIpc handle of a range whose export was refused) while its peers run on their own buffers, still
+    bit-exact — no kernel mismatch."""
     res = _spawn(_eager_worker, nranks, args=(fail_dmabuf_rank, fail_export_rank))
     bad = [e for r in sorted(res) for e in res[r][0]]
     assert not bad, "\n".join(bad[:20])
     for r, (_, zc, regs, same_addr, restaged, small_zc, bounced) in res.items():
         assert zc == 12, f"rank {r}: {zc} zero-copy plans for 12 eligible collectives"
-        if r == fail_export_rank:
+        if r in (fail_export_rank, fail_dmabuf_rank):
             assert regs == 1 and bounced == 12, f"rank {r}: {regs} registrations, {bounced} bounced (want 1, 12)"
             assert restaged, f"rank {r}: the re-allocated buffer did not go through the bounce allocation"
             continue
@@ -274,8 +274,8 @@ def _churn_worker(rank, nranks, uid, q):
     zero-copy on every rank and correct; the bounce allocation itself stays (the library's cached memory)."""
     try:
         os.environ["NCCL_AMD_EAGER_REGISTER"] = "1"
-        logf = f"/tmp/nccl_amd_churn_{os.getpid()}.log"
-        os.environ["NCCL_DEBUG"] = "INFO"
+        logf = os.path.join(os.environ.get("CHURN_LOG_DIR", "/tmp"), f"nccl_amd_churn_{os.getpid()}.log")
+        os.environ["NCCL_DEBUG"] = "TRACE" if os.environ.get("CHURN_LOG_DIR") else "INFO"  # diagnostics: TRACE
         os.environ["NCCL_DEBUG_FILE"] = logf
         import torch
         import nccl_amd
@@ -300,7 +300,15 @@ def _churn_worker(rank, nranks, uid, q):
             y = torch.empty_like(x)
             comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, sp)
             s.synchronize()
-            ok = ok and bool((y == float(nranks * (it + 1))).all())
+            want = float(nranks * (it + 1))
+            good = bool((y == want).all())
+            if not good:
+                bad = (y != want).nonzero().flatten()
+                vals = torch.unique(y[bad[:1 << 20]]).tolist()[:8]
+                print(f"rank {rank}: iteration {it} differs (async error {comm.async_error()}): {bad.numel()} of {count} "
+                      f"elements, indices {bad[0].item()}..{bad[-1].item()}, values {vals} (want {want}); x {x.data_ptr():x}"
+                      f" y {y.data_ptr():x}", flush=True)
+            ok = ok and good
             del x, y
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
@@ -315,7 +323,11 @@ def _churn_worker(rank, nranks, uid, q):
         sizes = re.findall(r"bounce allocation of (\d+) MiB registered", text)
         bounce = int(sizes[-1]) * MIB if sizes else 0
         mismatch = "kernel mismatch" in text
-        q.put((rank, (ok and not mismatch, free0, lows, free1, bounce, text.count("eager registration of the allocation holding"))))
+        if not ok or mismatch:  # the reason, for the assertion message
+            free0 = f"results ok {ok}, mismatch {mismatch}; " + " | ".join(
+                l[l.find("NCCL WARN"):][:300] for l in text.splitlines() if "NCCL WARN" in l)[:3000]
+        q.put((rank, (ok and not mismatch, free0, lows, free1, bounce,
+                      text.count("eager registration of the allocation holding"))))
     except Exception as e:
         q.put((rank, (False, repr(e), [], 0, 0, 0)))
 
