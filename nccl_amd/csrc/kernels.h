@@ -269,6 +269,11 @@ constexpr int kFoldUnroll1B = NCCL_AMD_FOLD_UNROLL_1B;
 #ifndef NCCL_AMD_FOLD_REPACK
 #define NCCL_AMD_FOLD_REPACK 1
 #endif
+// foldRange: the next batch's first source loaded while the current batch's last source folds (1), or after the
+// batch's stores (0, round 5's order)
+#ifndef NCCL_AMD_FOLD_PREFETCH
+#define NCCL_AMD_FOLD_PREFETCH 1
+#endif
 
 // Copy [0,nbytes) from src to dst. Both 16-byte aligned when `aligned`; nbytes multiple of sizeof(T).
 template <typename T, bool REMOTE>
@@ -543,19 +548,36 @@ __device__ __forceinline__ void foldRange(const Red<T, OP>& fn, int n, const cha
   }
   if (aligned) {
     const uint64_t npk = nelem / EPP;
-    for (uint64_t base = threadIdx.x; base < npk; base += (uint64_t)U * kThreads) {
-      PackU<T> acc[U], cur[U], nxt[U];
+    const uint64_t step = (uint64_t)U * kThreads;
+    // (not for 1-byte types: their unpacked folds sit at the 128-VGPR cap, and the early loads spill there)
+    constexpr bool kPrefetch = NCCL_AMD_FOLD_PREFETCH && sizeof(T) > 1;
+    PackU<T> acc[U], cur[U], nxt[U];
+    if constexpr (kPrefetch) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        uint64_t i = base + (uint64_t)u * kThreads;
+        uint64_t i = threadIdx.x + (uint64_t)u * kThreads;
         if (i < npk) cur[u].v = __builtin_nontemporal_load((const u32x4*)src[0] + i);
       }
+    }
+    for (uint64_t base = threadIdx.x; base < npk; base += step) {
+      if constexpr (!kPrefetch) {  // round 5's order: each batch starts by loading its first source
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+          uint64_t i = base + (uint64_t)u * kThreads;
+          if (i < npk) cur[u].v = __builtin_nontemporal_load((const u32x4*)src[0] + i);
+        }
+      }
       for (int k = 0; k < n; k++) {
-        if (k + 1 < n) {
-          const u32x4* s = (const u32x4*)src[k + 1];
+        // the next source's packs in flight while this one folds; after the last source, the NEXT batch's first
+        // source (NCCL_AMD_FOLD_PREFETCH): the loads never drain between batches, which matters most at n = 2
+        // (half of each batch had nothing in flight) and for remote sources (zero-copy kernels reading peers)
+        const bool last = k + 1 == n;
+        if (!last || (kPrefetch && base + step < npk)) {
+          const u32x4* s = (const u32x4*)src[last ? 0 : k + 1];
+          const uint64_t b = last ? base + step : base;
 #pragma unroll
           for (int u = 0; u < U; u++) {
-            uint64_t i = base + (uint64_t)u * kThreads;
+            uint64_t i = b + (uint64_t)u * kThreads;
             if (i < npk) nxt[u].v = __builtin_nontemporal_load(s + i);
           }
         }

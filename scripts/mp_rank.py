@@ -59,14 +59,24 @@ def main():
     if mode == "ag":
         y = torch.empty(S // 4, dtype=torch.float32, device="cuda")
     blk = S // 4 // n  # elements of one rank block
-    for _ in range(2 + iters):
+
+    def one():
         if mode == "rs":
             comm.reduce_scatter_raw(x.data_ptr(), y.data_ptr(), blk, 7, 0, s.cuda_stream)
         elif mode == "ag":
             comm.all_gather_raw(x.data_ptr(), y.data_ptr(), blk, 7, s.cuda_stream)
         else:
             comm.all_reduce_raw(x.data_ptr(), y.data_ptr(), S // 4, 7, 0, s.cuda_stream)
+    for _ in range(2):
+        one()
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(iters):
+        one()
+    e1.record(s)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / max(iters, 1)
     total = float(n * (n + 1) // 2)
     if mode == "rs":
         ok = bool((y[:blk] == total).all())
@@ -74,7 +84,7 @@ def main():
         ok = all(bool((y[r * blk:(r + 1) * blk] == float(r + 1)).all()) for r in range(n))
     else:
         ok = bool((y == total).all())
-    print(f"rank {rank}: ok={ok} async={comm.async_error()}", flush=True)
+    print(f"rank {rank}: ok={ok} async={comm.async_error()} ms={ms:.4f}", flush=True)
     if mode == "sym":
         comm.deregister_window(win)
     if mode == "reg":

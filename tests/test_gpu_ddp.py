@@ -1,7 +1,9 @@
 """End to end on the north star's path: a torch DistributedDataParallel training step whose gradient
 buckets are all-reduced by this engine through a DDP comm hook (nccl_amd.ddp_comm_hook), 2 processes on the
 one GPU. After identical steps from identical weights on different data, both ranks must hold identical
-parameters, equal to a single-process reference step on the averaged gradient."""
+parameters, equal to a single-process reference step on the averaged gradient. `default`: a wider model with
+buckets of several MiB and the library's defaults, so the buckets run eager zero-copy (the multi-process default
+since round 6); `staged`: small buckets on the staged / LL kernels."""
 import multiprocessing as mp
 import os
 import socket
@@ -19,9 +21,18 @@ def _port():
     return p
 
 
-def _worker(rank, world, port, uid, q):
+def _model(torch, wide):
+    h = 1024 if wide else 256
+    return torch.nn.Sequential(torch.nn.Linear(64, h), torch.nn.ReLU(), torch.nn.Linear(h, h), torch.nn.ReLU(),
+                               torch.nn.Linear(h, 32)).cuda()
+
+
+def _worker(rank, world, port, uid, q, wide):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NCCL_AMD_SPIN_TIMEOUT_MS="30000")
+        if wide:
+            os.environ.pop("NCCL_AMD_EAGER_REGISTER", None)  # the library's default
+            os.environ.update(NCCL_DEBUG="TRACE", NCCL_DEBUG_FILE=f"/tmp/nccl_amd_ddp_{os.getpid()}.log")
         import torch
         import torch.distributed as dist
         import nccl_amd
@@ -29,8 +40,9 @@ def _worker(rank, world, port, uid, q):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         comm = nccl_amd.Communicator.init(world, rank, uid)
         torch.manual_seed(0)
-        model = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 32)).cuda()
-        ddp = torch.nn.parallel.DistributedDataParallel(model, bucket_cap_mb=0.01)  # several buckets
+        model = _model(torch, wide)
+        # several buckets: 4 MiB ones for the wide model (above the 2 MiB one-shot range at n = 2: eager zero-copy), 10 KB ones otherwise
+        ddp = torch.nn.parallel.DistributedDataParallel(model, bucket_cap_mb=4 if wide else 0.01)
         ddp.register_comm_hook(None, nccl_amd.ddp_comm_hook(comm))
         opt = torch.optim.SGD(ddp.parameters(), lr=0.1)
         g = torch.Generator(device="cuda").manual_seed(100 + rank)
@@ -42,14 +54,20 @@ def _worker(rank, world, port, uid, q):
             opt.step()
         torch.cuda.synchronize()
         flat = torch.cat([p.detach().flatten() for p in model.parameters()]).cpu()
-        q.put((rank, flat.numpy(), comm.async_error()))
+        err = comm.async_error()
         comm.destroy()
+        zc = 0
+        if wide:
+            zc = open(os.environ["NCCL_DEBUG_FILE"]).read().count("AllReduce: registered zero-copy")
+        q.put((rank, flat.numpy(), err, zc))
         dist.destroy_process_group()
     except Exception as e:
-        q.put((rank, repr(e), -1))
+        q.put((rank, repr(e), -1, 0))
 
 
-def test_ddp_step_through_engine(built):
+@pytest.mark.parametrize("mode", ["staged", "default"])
+def test_ddp_step_through_engine(built, mode):
+    wide = mode == "default"
     import numpy as np
     import torch
     import nccl_amd
@@ -57,23 +75,25 @@ def test_ddp_step_through_engine(built):
     q = ctx.Queue()
     uid = nccl_amd.get_unique_id()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, uid, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, uid, q, wide)) for r in range(2)]
     for p in ps:
         p.start()
     res = {}
     for _ in range(2):
-        r, flat, err = q.get(timeout=240)
-        res[r] = (flat, err)
+        r, flat, err, zc = q.get(timeout=240)
+        res[r] = (flat, err, zc)
     for p in ps:
         p.join(timeout=60)
     for r in range(2):
         assert not isinstance(res[r][0], str), res[r][0]
         assert res[r][1] == 0
+        if wide:  # every step's large buckets ran zero-copy on the ranks' own bucket tensors
+            assert res[r][2] >= 3, f"rank {r}: {res[r][2]} zero-copy AllReduces"
     a, b = res[0][0], res[1][0]
     assert np.array_equal(a, b), "ranks diverged"
     # single-process reference: same init, gradient = mean of the two ranks' gradients, same 3 steps
     torch.manual_seed(0)
-    model = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 32)).cuda()
+    model = _model(torch, wide)
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
     gens = [torch.Generator(device="cuda").manual_seed(100 + r) for r in range(2)]
     for _ in range(3):
