@@ -69,8 +69,14 @@ def settings(rng):
         env["NCCL_LL_BUFFSIZE"] = str(rng.choice([4096, 65536, 524288]))
     if rng.random() < 0.15:
         env["NCCL_LL128_BUFFSIZE"] = str(rng.choice([32768, 262144]))
-    if rng.random() < 0.25:  # eager zero-copy on the cases' plain torch buffers (register.cc), small thresholds too
+    # eager zero-copy on the cases' plain torch buffers (register.cc), small thresholds too; unset = the library's
+    # default (on across processes since round 6, so scripts/fuzz_mp.py runs it), "0" = the staged kernels
+    r = rng.random()
+    if r < 0.25:
+        env["NCCL_AMD_EAGER_REGISTER"] = "0"
+    elif r < 0.5:
         env["NCCL_AMD_EAGER_REGISTER"] = "1"
+    if r < 0.5 or rng.random() < 0.5:
         if rng.random() < 0.6:
             env["NCCL_AMD_EAGER_REGISTER_BYTES"] = str(rng.choice([16, 4096, 65536]))
         if rng.random() < 0.3:
