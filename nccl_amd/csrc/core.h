@@ -373,6 +373,7 @@ struct ncclComm {
   hipEvent_t bounceEv = nullptr;
   std::vector<std::pair<ncclamd::RegAlloc*, void*>> bounceOld;
   bool bounceFailed = false;
+  bool warnedEagerRefusal = false, warnedBounceMax = false;
   ncclamd::BounceCopy bounceNext = {};  // regLookup's last result when it bounced (bounceUsed)
   bool bounceUsed = false;
 

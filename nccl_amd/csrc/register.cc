@@ -652,8 +652,12 @@ static bool bounceFor(ncclComm* comm, const void* send, size_t sendBytes, const 
   const uint64_t need = sendLen + recvBytes;
   if (comm->bounceFailed) return false;
   if (need > maxBytes) {
-    WARN("rank %d: a collective of %zu + %zu bytes needs more than NCCL_AMD_EAGER_BOUNCE_MAX_BYTES=%lu of bounce "
-         "allocation: it runs staged on this rank", comm->rank, sendBytes, recvBytes, (unsigned long)maxBytes);
+    if (!comm->warnedBounceMax) {
+      comm->warnedBounceMax = true;
+      WARN("rank %d: a collective of %zu + %zu bytes needs more than NCCL_AMD_EAGER_BOUNCE_MAX_BYTES=%lu of bounce "
+           "allocation: it runs staged on this rank (a kernel-mismatch error if its peers run zero-copy)", comm->rank,
+           sendBytes, recvBytes, (unsigned long)maxBytes);
+    }
     return false;
   }
   if (!comm->bounceEv && hipEventCreateWithFlags(&comm->bounceEv, hipEventDisableTiming) != hipSuccess) {
@@ -814,8 +818,8 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
   } else if (eager) {
     // first use of an unregistered allocation: map it into every peer now (one dma-buf export + one IMPORT request per
     // peer process, once per allocation); later collectives find it in comm->regs. A failure is remembered per
-    // allocation and said once; this rank then runs the staged kernel, and if its peers registered theirs every rank
-    // stops with the kernel-mismatch error (kernels.h WaitProbe) instead of waiting for the spin timeout.
+    // allocation (not retried) and the collective runs on the bounce allocation (bounceFor), so the peers, which run
+    // zero-copy either way, see no difference.
     auto acquire = [&](const void* b, size_t bytes) -> RegAlloc* {
       if (eagerFailedBefore(comm, b)) return nullptr;
       RegAlloc* y = nullptr;
@@ -825,18 +829,26 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
         // not a plain device allocation (host-pinned, managed: hipMemGetAddressRange fails) or the export / an import
         // failed: remembered, said once. Every rank must pass buffers of the same kind.
         const std::pair<uint64_t, uint64_t> key = eagerKey(b);
+        // bounded: a loop of fresh allocations the runtime keeps refusing must not grow it for ever (the oldest
+        // keys name allocations long gone; forgetting one costs at most a repeated export attempt)
+        if (comm->eagerFailed.size() >= 256) comm->eagerFailed.erase(comm->eagerFailed.begin());
         comm->eagerFailed.push_back(key);
-        WARN("rank %d: eager registration of the allocation holding %p failed (%d): this rank runs its collectives on "
-             "it staged; if its peers registered theirs, they stop with a kernel-mismatch error (pass device "
-             "allocations of the same kind on every rank, or NCCL_AMD_EAGER_REGISTER=0 on every rank)", comm->rank, b,
-             (int)res);
+        // a WARN the first time on this communicator, INFO after (a churning allocator may see one per iteration)
+        if (!comm->warnedEagerRefusal) {
+          comm->warnedEagerRefusal = true;
+          WARN("rank %d: eager registration of the allocation holding %p failed (%d): its collectives run through "
+               "this rank's bounce allocation (copied in and out); later refusals are reported at INFO level",
+               comm->rank, b, (int)res);
+        } else {
+          INFO("rank %d: eager registration of the allocation holding %p failed (%d): bounce allocation", comm->rank,
+               b, (int)res);
+        }
         return nullptr;
       }
       if ((int)comm->regs.size() > comm->tune.eagerMax && !comm->warnedEagerCap) {
         comm->warnedEagerCap = true;
-        INFO("rank %d: %zu registrations exceed NCCL_AMD_EAGER_REGISTER_MAX=%d; the least recently used are released at "
-             "the next blocking call (ncclCommRegister / Deregister / Finalize / Destroy)", comm->rank,
-             comm->regs.size(), comm->tune.eagerMax);
+        INFO("rank %d: %zu registrations exceed NCCL_AMD_EAGER_REGISTER_MAX=%d; the least recently used are retired "
+             "at the next collectives (regProgress)", comm->rank, comm->regs.size(), comm->tune.eagerMax);
       }
       return y->usable ? y : nullptr;
     };
