@@ -147,7 +147,7 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested);
 ncclResult_t ipcServerStart(ncclComm* comm);
 void ipcServerStop(ncclComm* comm);
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d);
-hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd);  // under gMapMu, retried (ipc.cc)
+hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd, int attempts = 5);  // under gMapMu (ipc.cc)
 void ipcUnexport(ncclComm* comm, const IpcDesc& d);
 ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d);  // serve an fd (owned) under a new key
 ncclResult_t ipcFetchFd(const IpcDesc& d, int* fd);  // an exporter's fd for d, over its fd server (bounded)

@@ -486,11 +486,13 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested) {
 }
 
 // The dma-buf export of [base, +size) (hipMemGetHandleForAddressRange), under gMapMu like every import and release of
-// this library. Round 6's eager churn (tests/test_gpu_eager.py, gpurun_out TRACE logs): exports made
-// on the caller's thread while this process's fd server thread was importing a peer's registration failed with
-// "invalid argument" — 5 of 24 registrations in 8 iterations, always beside a concurrent import — and a plain
-// export / import / unmap cycle of the same buffers without that concurrency never failed (scripts/eager_churn_probe.py,
-// tests/native/reuse_probe.hip: 0 of 80). A failure is retried (1, 2, 4, 8 ms apart, the lock released meanwhile).
+// this library. Round 6's eager churn (tests/test_gpu_eager.py, gpurun_out TRACE logs): 2-5 of 16
+// exports per rank were refused with "invalid argument", each a re-allocation at the address of a just-freed
+// registered allocation whose peers were unmapping the old one; a plain export / import / unmap cycle of the same
+// buffers without the library's kernels never failed (scripts/eager_churn_probe.py, tests/native/reuse_probe.hip: 0 of
+// 80). `attempts` > 1 retries a refusal 1, 2, 4, 8 ms apart (the lock released meanwhile): kept for the init-time
+// exports, whose only alternative is failing the communicator; no retry was ever seen to succeed in the churn, where
+// the eager path has the bounce allocation instead and asks for one attempt.
 //
 // Every dma-buf this process exported is remembered by its inode (the dma-buf file's identity; the kernel numbers them
 // in increasing order, one per dma-buf created). Measured in round 6 (the eager churn inside the full GPU suite,
@@ -510,9 +512,9 @@ static uint64_t allocationId(void* p) {
   return (uint64_t)id;
 }
 
-hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd) {
+hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd, int attempts) {
   hipError_t e = hipErrorInvalidValue;
-  for (int attempt = 0; attempt < 5; attempt++) {
+  for (int attempt = 0; attempt < attempts; attempt++) {
     if (attempt) std::this_thread::sleep_for(std::chrono::milliseconds(1 << (attempt - 1)));
     std::lock_guard<std::mutex> g(gMapMu);
     e = hipMemGetHandleForAddressRange(fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);

@@ -226,7 +226,7 @@ static ncclResult_t regCreate(ncclComm* comm, uint64_t base, uint64_t size, uint
       const bool failAll = !tBounceCreate && paramInt("NCCL_AMD_REG_FAIL_EXPORT", 0) != 0;
       hipError_t e = failAll || paramInt("NCCL_AMD_REG_FAIL_DMABUF", 0)  // tests: the hipIpc fallback below
                          ? hipErrorInvalidValue
-                         : ipcExportDmaBuf((void*)base, size, &fd);
+                         : ipcExportDmaBuf((void*)base, size, &fd, deferRelease && !tBounceCreate ? 1 : 5);
       if (e != hipSuccess) {
         (void)hipGetLastError();
         // The runtime sometimes refuses the dma-buf export of a fresh allocation ("invalid argument"; round 6's eager
