@@ -523,6 +523,9 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
                size_t recvBytes, const char** rmtSend, char** rmtRecv, bool eager = false);
 // release every window and IPC mapping (destroy: also asks peers to unmap this rank's registrations; abort: not)
 void windowsFree(ncclComm* comm, bool notifyPeers);
+// at init: one plain allocation per rank registered with and read back by every peer; any failure turns the eager
+// zero-copy default off on every rank (register.cc)
+ncclResult_t eagerProbe(ncclComm* comm);
 // A blocking entry point's registration upkeep (register.cc): graph-held references whose graphs are gone are
 // dropped, stale and surplus eager registrations released, and retired registrations' RELEASE requests sent.
 void regBlockingPoint(ncclComm* comm);

@@ -233,6 +233,8 @@ static ncclResult_t commInitRankInto(ncclComm* comm, int nranks, ncclUniqueId id
   TRACE("rank %d: device state ready", rank);
   // every peer mapping carries bytes both ways before the first collective (mapcheck.cc; all ranks fail together)
   if ((res = mapCheck({comm})) != ncclSuccess) goto fail;
+  // ... and so does a plain device allocation, or eager zero-copy stays off on every rank (register.cc)
+  if ((res = eagerProbe(comm)) != ncclSuccess) goto fail;
   if ((res = tunerLoad(comm)) != ncclSuccess) goto fail;
   if ((res = bootstrapBarrier(comm->bootstrap)) != ncclSuccess) goto fail;
   unexportHandles(comm);  // every peer has mapped our slab and flags

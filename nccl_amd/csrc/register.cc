@@ -876,6 +876,93 @@ bool regLookup(ncclComm* comm, hipStream_t stream, const void* send, size_t send
   return true;
 }
 
+// Eager zero-copy is the default for a communicator spanning processes (enqueue.cc eagerOn), and it maps ordinary
+// device allocations — what PyTorch's allocator hands out — into the peers, which the init-time mapping check
+// (mapcheck.cc) does not cover: it checks the staging slab and flag block. So at init each rank registers one plain
+// hipMalloc allocation with every peer (the eager path: dma-buf export, IMPORT by each peer's fd server) and reads
+// every peer's through its own mapping, comparing the bytes. The outcome is all-gathered: if any rank failed any
+// part, every rank turns eager zero-copy off for this communicator (the kernel choice stays the same on every rank)
+// and the ranks that saw the failure say what failed. A few milliseconds per init; NCCL_AMD_EAGER_PROBE=0 skips it.
+static uint64_t probeWord(int rank, size_t i) {
+  uint64_t x = 0x9e3779b97f4a7c15ull * (uint64_t)(rank + 1) + 0xd1b54a32d192ed03ull * (uint64_t)(i + 1);
+  x ^= x >> 31;
+  return x * 0xbf58476d1ce4e5b9ull;
+}
+
+ncclResult_t eagerProbe(ncclComm* comm) {
+  if (!(comm->tune.eagerRegister < 0 && comm->multiProcess && comm->regIpcAll)) return ncclSuccess;
+  if (!paramInt("NCCL_AMD_EAGER_PROBE", 1)) return ncclSuccess;
+  const int n = comm->nRanks, me = comm->rank, pid = getpid();
+  const size_t bytes = (size_t)2 << 20, words = bytes / sizeof(uint64_t), checkWords = 512;
+  char why[160] = "";
+  void* mem = nullptr;
+  RegAlloc* ra = nullptr;
+  hipError_t e;
+  {
+    std::lock_guard<std::mutex> g(ipcMapMutex());
+    e = hipMalloc(&mem, bytes);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    mem = nullptr;
+    snprintf(why, sizeof(why), "hipMalloc of the probe: %s", hipGetErrorString(e));
+  } else {
+    std::vector<uint64_t> pat(words);
+    for (size_t i = 0; i < words; i++) pat[i] = probeWord(me, i);
+    if ((e = hipMemcpy(mem, pat.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) {
+      (void)hipGetLastError();
+      snprintf(why, sizeof(why), "filling the probe: %s", hipGetErrorString(e));
+    } else if (regCreate(comm, (uint64_t)mem, bytes, bufferIdOf(mem), &ra, /*deferRelease=*/false) != ncclSuccess) {
+      ra = nullptr;  // released by regCreate
+      snprintf(why, sizeof(why), "registering the probe with every peer (export or a peer's import)");
+    }
+  }
+  // where each peer mapped my probe: table[q * n + r] = rank q's probe as mapped in rank r's process
+  std::vector<uint64_t> table((size_t)n * n, 0);
+  if (ra)
+    for (int r = 0; r < n; r++) table[(size_t)me * n + r] = ra->rmt[r];
+  ncclResult_t res = commAllGather(comm, table.data(), (size_t)n * sizeof(uint64_t));
+  if (res == ncclSuccess && !why[0]) {
+    std::vector<uint64_t> got(checkWords);
+    for (int q = 0; q < n && !why[0]; q++) {
+      if (q == me || comm->peers[q].pid == pid) continue;
+      const uint64_t addr = table[(size_t)q * n + me];
+      if (!addr) continue;  // rank q could not register its probe: it reports that itself
+      for (size_t at : {(size_t)0, words - checkWords}) {  // the first and the last 4 KiB
+        if ((e = hipMemcpy(got.data(), (const void*)(addr + at * sizeof(uint64_t)), checkWords * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost)) != hipSuccess) {
+          (void)hipGetLastError();
+          snprintf(why, sizeof(why), "reading rank %d's probe through its mapping: %s", q, hipGetErrorString(e));
+          break;
+        }
+        for (size_t i = 0; i < checkWords && !why[0]; i++)
+          if (got[i] != probeWord(q, at + i))
+            snprintf(why, sizeof(why), "rank %d's probe reads back wrong through its mapping (word %zu)", q, at + i);
+      }
+    }
+  }
+  std::vector<int> ok(n, 0);
+  ok[me] = res == ncclSuccess && !why[0] ? 1 : 0;
+  if (res == ncclSuccess) res = commAllGather(comm, ok.data(), sizeof(int));
+  if (ra) regRelease(comm, ra);  // RELEASE to the peers (unmapped at their next blocking call or collective)
+  if (mem) {
+    std::lock_guard<std::mutex> g(ipcMapMutex());
+    (void)hipFree(mem);
+  }
+  if (res != ncclSuccess) return res;  // the bootstrap itself failed: the init fails
+  int bad = -1;
+  for (int r = 0; r < n && bad < 0; r++)
+    if (!ok[r]) bad = r;
+  if (bad >= 0) {
+    comm->tune.eagerRegister = 0;  // the same decision on every rank (the all-gathered outcomes)
+    if (why[0]) WARN("rank %d: eager zero-copy probe failed: %s; eager zero-copy is off for this communicator", me, why);
+    else INFO("rank %d: eager zero-copy is off for this communicator (rank %d's probe failed)", me, bad);
+  } else {
+    TRACE("rank %d: eager zero-copy probe passed (every peer's plain allocation read back through its mapping)", me);
+  }
+  return ncclSuccess;
+}
+
 void windowsFree(ncclComm* comm, bool notifyPeers) {
   (void)hipSetDevice(comm->device);
   {  // graph releases still queued for this communicator: every registration goes below anyway; tokens of its graphs

@@ -136,11 +136,15 @@ def test_eager_zero_copy_multi_process(built, nranks, fail_dmabuf_rank, fail_exp
         assert small_zc == 0, f"rank {r}: a one-shot / LL-range op ran zero-copy"
 
 
-def _default_worker(rank, nranks, uid, q):
+def _default_worker(rank, nranks, uid, q, fail_rank=-1):
     """The library's default (NCCL_AMD_EAGER_REGISTER unset): a communicator spanning processes runs an eligible
-    collective on the ranks' own buffers (round 6)."""
+    collective on the ranks' own buffers (round 6). fail_rank: that rank cannot register anything
+    (NCCL_AMD_REG_FAIL_EXPORT=1), so the init-time probe (register.cc eagerProbe) fails there and every rank runs
+    the staged kernel instead."""
     try:
         os.environ.pop("NCCL_AMD_EAGER_REGISTER", None)
+        if rank == fail_rank:
+            os.environ["NCCL_AMD_REG_FAIL_EXPORT"] = "1"
         logf = _trace_env(f"eagerdefault{nranks}")
         import torch
         import nccl_amd
@@ -163,18 +167,27 @@ def _default_worker(rank, nranks, uid, q):
             if comm.async_error() or not G.same_bits(y.cpu().numpy(), oracle.all_reduce(ins, 7, 0), 7):
                 errs.append(f"rank {rank} round {it}: differs (async {comm.async_error()})")
         zc = len(_zero_copy_lines(logf, pos))
+        text = open(logf).read()
+        probe = ("passed" if "eager zero-copy probe passed" in text else
+                 "failed here" if "eager zero-copy probe failed" in text else
+                 "off" if "eager zero-copy is off" in text else "none")
         comm.destroy()
-        q.put((rank, (errs, zc)))
+        q.put((rank, (errs, zc, probe)))
     except Exception as e:
-        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0)))
+        q.put((rank, ([f"rank {rank} exception: {e!r}"], 0, "")))
 
 
-def test_eager_zero_copy_is_the_multi_process_default(built):
-    res = _spawn(_default_worker, 2)
+@pytest.mark.parametrize("fail_rank", [-1, 1])
+def test_eager_zero_copy_is_the_multi_process_default(built, fail_rank):
+    res = _spawn(_default_worker, 2, args=(fail_rank,))
     bad = [e for r in sorted(res) for e in res[r][0]]
     assert not bad, "\n".join(bad)
-    for r, (_, zc) in res.items():
-        assert zc == 2, f"rank {r}: {zc} zero-copy plans of 2 (default: eager zero-copy across processes)"
+    for r, (_, zc, probe) in res.items():
+        if fail_rank < 0:
+            assert zc == 2 and probe == "passed", f"rank {r}: {zc} zero-copy plans of 2, probe {probe}"
+        else:  # one rank's probe failed: every rank runs staged, bit-exact
+            assert zc == 0, f"rank {r}: {zc} zero-copy plans after a failed probe"
+            assert probe == ("failed here" if r == fail_rank else "off"), f"rank {r}: probe {probe}"
 
 
 def _pinning_worker(rank, nranks, uid, q, on_coll=True):
