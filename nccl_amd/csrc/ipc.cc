@@ -190,9 +190,17 @@ bool ipcLibraryIdle() { return libraryIdle(); }
 void ipcProgressReleases() {
   if (!gHavePending.load(std::memory_order_acquire)) return;
   static const bool on = paramInt("NCCL_AMD_RELEASE_ON_COLL", 1) != 0;
-  if (!on || !libraryIdle()) return;
+  static std::atomic<int> said{0};  // why a pending release waits (INFO, the first 16 times in the process)
+  if (!on) return;
+  if (!libraryIdle()) {
+    if (said.fetch_add(1) < 16) INFO("ipc: peers' released mappings wait: a kernel of this library is in flight");
+    return;
+  }
   std::unique_lock<std::mutex> lk(gMapMu, std::try_to_lock);
-  if (!lk.owns_lock()) return;
+  if (!lk.owns_lock()) {
+    if (said.fetch_add(1) < 16) INFO("ipc: peers' released mappings wait: the mapping lock is busy");
+    return;
+  }
   std::vector<PendingRelease> batch;
   {
     std::lock_guard<std::mutex> g(gPendMu);
@@ -217,7 +225,8 @@ void ipcProgressReleases() {
   (void)hipThreadExchangeStreamCaptureMode(&mode);
   (void)hipSetDevice(dev);
   (void)hipGetLastError();
-  TRACE("ipc: released %zu peer mapping(s) on the collective path", batch.size());
+  INFO("ipc: released %zu peer mapping(s) on the collective path (%zu MiB still pending)", batch.size(),
+       (size_t)(gPendingBytes >> 20));
 }
 
 // Requests on the fd server's socket (one per connection). FETCH: hand over the fd published under `key`.

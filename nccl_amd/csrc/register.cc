@@ -577,6 +577,10 @@ void regProgress(ncclComm* comm) {
     RegAlloc* ra = comm->regRetired[i];
     const hipError_t q = ra->evMissing ? hipErrorNotReady : ra->lastEv ? hipEventQuery(ra->lastEv) : hipSuccess;
     if (q == hipErrorNotReady) {
+      static std::atomic<int> said{0};
+      if (said.fetch_add(1) < 16)
+        INFO("rank %d: retired registration %lx waits for its last kernel (%s)", comm->rank, (unsigned long)ra->base,
+             ra->evMissing ? "no event" : "event not complete");
       i++;
       continue;
     }
