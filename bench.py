@@ -411,8 +411,8 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         for env in envs:
             for k in knobs:
                 os.environ.pop(k, None)
-            # every column but the eager one tunes the staged kernel: eager zero-copy (the multi-process default since
-            # round 6) would otherwise take these collectives and no staged knob would matter
+            # every column but the eager one tunes the staged kernel, whatever the caller's NCCL_AMD_EAGER_REGISTER
+            # (eager zero-copy would otherwise take these collectives and no staged knob would matter)
             os.environ.update({"NCCL_AMD_EAGER_REGISTER": "0", **env})
             comms.append(nccl_amd.Communicator.init(n, rank, exchange_unique_id(dist, rank)))
         for k, v in saved.items():
@@ -461,7 +461,7 @@ def run_suite(comm, n: int, rank: int, dist, stream, quick: bool = False, out: d
         dflt = tuning[0] if not envs[0] else None
         eager = next((r for r in tuning if r["env"] == {"NCCL_AMD_EAGER_REGISTER": "1"}), None)
         if eager is not None:  # the unregistered buffers of the headline, registered on first use
-            out["eager_zero_copy"] = {"env": "NCCL_AMD_EAGER_REGISTER=1 (the multi-process default)", "ms": eager["ms"],
+            out["eager_zero_copy"] = {"env": "NCCL_AMD_EAGER_REGISTER=1", "ms": eager["ms"],
                                       "ms_min": eager["ms_min"], "ms_max": eager["ms_max"],
                                       "busbw_GBps": eager["busbw_GBps"],
                                       "staged_default_ms": dflt["ms"] if dflt else None, "check": eager["check"]}
@@ -849,7 +849,7 @@ def main(argv=None):
     # the dominant (only) kernel of a step: the first one this process launched (warm-up of the same call)
     kernels = launched_kernels(klog)
     kname = kernels[0] if kernels else None
-    zero_copy = bool(kname and "symKernel" in kname)  # eager zero-copy (the multi-process default) or staged
+    zero_copy = bool(kname and "symKernel" in kname)  # eager zero-copy (NCCL_AMD_EAGER_REGISTER) or staged
     if n > 1 and zero_copy:
         workload = (f"ncclAllReduce sum fp32, {size_mib} MiB per rank, {n}xMI355X zero-copy (the ranks' buffers "
                     "registered on first use, DESIGN.md §10.3)")

@@ -236,13 +236,12 @@ void loadTuning(CommTuning* t) {
   t->graphRegister = (int)paramInt("NCCL_GRAPH_REGISTER", 1);
   t->noAggregation = (int)paramInt("NCCL_AMD_NO_AGGREGATION", 0);
   // Eager registration (register.cc regLookup): collectives of at least eagerBytes whose staged plan would be direct
-  // register their unregistered allocations on first use and run the zero-copy kernel. Default
-  // (-1): on for communicators spanning processes whose peers all serve registrations (eagerOn) — one-GPU rehearsal
-  // 0.209 / 1.014 / 1.143 ms vs 0.302 / 1.579 / 1.514 ms staged at n = 2 / 4 / 8 (2.50 S vs 4.0 S of HBM per rank at n = 2
-  // by PMC). Since round 6 its costs are bounded without a blocking call: freed allocations are found and released on
-  // the collective path, and an allocation this rank cannot register runs through the bounce allocation. 0: staged;
-  // 1: on for every communicator (one process too).
-  t->eagerRegister = (int)paramInt("NCCL_AMD_EAGER_REGISTER", -1);
+  // register their unregistered allocations on first use and run the zero-copy kernel. 1: on; -1:
+  // on for communicators spanning processes whose peers all serve registrations (eagerOn; one-GPU rehearsal 2.50 S vs
+  // 4.0 S of HBM per rank at n = 2 by PMC); 0 (default): off. Round 6 made its costs bounded without a blocking call
+  // and added the bounce allocation and the init probe, and measured on the one-GPU n = 8 rehearsal that the runtime
+  // can hand one process's export another process's fresh dma-buf (§10.3): so it stays opt-in.
+  t->eagerRegister = (int)paramInt("NCCL_AMD_EAGER_REGISTER", 0);
   t->eagerBytes = paramInt("NCCL_AMD_EAGER_REGISTER_BYTES", 1 << 20);
   t->eagerMax = (int)paramInt("NCCL_AMD_EAGER_REGISTER_MAX", 64);
   if (t->eagerMax < 1) t->eagerMax = 1;
@@ -677,8 +676,8 @@ bool llPlan(const CollInfo& info, LLOp* op) {
 
 // Plan one op: the kernel launch (PLAN_KERNEL, in p), the symmetric-window launch (PLAN_SYM, in sp) or
 // nothing (PLAN_NONE). Every rank derives the same plan from what all ranks share.
-// Eager zero-copy for this communicator (NCCL_AMD_EAGER_REGISTER: 1 always, 0 never, default when it spans processes
-// whose every peer serves registrations). Every rank computes the same answer from the shared peer table.
+// Eager zero-copy for this communicator (NCCL_AMD_EAGER_REGISTER: 1 always, 0 never (default), -1 when it spans
+// processes whose every peer serves registrations). Every rank computes the same answer from the shared peer table.
 static bool eagerOn(const ncclComm* comm) {
   return comm->tune.eagerRegister > 0 || (comm->tune.eagerRegister < 0 && comm->multiProcess && comm->regIpcAll);
 }

@@ -22,6 +22,7 @@
 #include <fcntl.h>
 #include <poll.h>
 #include <string.h>
+#include <sys/file.h>
 #include <sys/socket.h>
 #include <sys/stat.h>
 #include <sys/un.h>
@@ -503,14 +504,65 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested) {
 // exports, whose only alternative is failing the communicator; no retry was ever seen to succeed in the churn, where
 // the eager path has the bounce allocation instead and asks for one attempt.
 //
-// Every dma-buf this process exported is remembered by its inode (the dma-buf file's identity; the kernel numbers them
-// in increasing order, one per dma-buf created). Measured in round 6 (the eager churn inside the full GPU suite,
-// gpurun_out TRACE logs): a rank exported its send and then its receive allocation, and the peer received the SAME
-// dma-buf for both (one inode, two registrations) — the receive allocation's export had handed back an existing
-// dma-buf, and the peer's zero-copy kernel read the send buffer as the receive one: silently wrong results. An export
-// whose dma-buf was exported before is therefore refused here (the caller falls back as for any refused export).
-// (A dma-buf handed back again for the same allocation — same base, same buffer id — is fine.)
-static std::map<std::pair<uint64_t, uint64_t>, std::pair<uint64_t, uint64_t>> gExported;  // (dev, ino) -> (base, id)
+// An export can hand back a dma-buf that already exists — another allocation's, exported earlier by this process
+// or by another process on the same device — instead of a new one for this allocation. Measured in round 6 (TRACE
+// logs): (1) the eager churn inside the full GPU suite, a rank exported its send and then its receive allocation and
+// the peer received ONE dma-buf (one inode) for both: the peer's zero-copy kernel read the send buffer as the
+// receive one; (2) the n = 8 one-GPU rehearsal, rank 3's export of its 256 MiB output handed back the 512 MiB bounce
+// dma-buf rank 2 had created 66 us earlier: the peers mapped it as rank 3's output and pulled rank 2's input from it —
+// a silently wrong block on every rank but rank 3, in 1 of 4 runs. Serializing every export and import of the node
+// (below) did not remove it (2 such exports in 5 runs, both caught), so it is not a race between concurrent calls
+// but stale state in the export path. Two checks, both under the node lock:
+//  * the dma-buf's size (its llseek end) must be the allocation's (catches (2));
+//  * a node-wide registry of every dma-buf the library's processes exported (/tmp/.ncclamd_dmabuf.reg: inode, the
+//    exporting process's random id, base, buffer id): a dma-buf exported before for any other allocation is refused
+//    (catches (1), and (2) at equal sizes). The same allocation may get its dma-buf back.
+// A refused export's descriptor is closed (the API hands it to the caller) and the caller falls back as for any
+// refused export (hipIpc handle for explicit registrations, the bounce allocation for eager ones).
+struct NodeLock {  // every dma-buf export and import of the library's processes on a node, one at a time
+  int fd = -1;
+  NodeLock() {
+    static const int lockFd = paramInt("NCCL_AMD_DMABUF_NODE_LOCK", 1)
+                                  ? open("/tmp/.ncclamd_dmabuf.lock", O_RDWR | O_CREAT | O_CLOEXEC, 0666)
+                                  : -1;
+    if (lockFd >= 0 && flock(lockFd, LOCK_EX) == 0) fd = lockFd;
+  }
+  ~NodeLock() {
+    if (fd >= 0) (void)flock(fd, LOCK_UN);
+  }
+  bool held() const { return fd >= 0; }
+};
+struct ExportRec {
+  uint64_t dev, ino, proc, base, id;
+};
+static uint64_t processId() {
+  static const uint64_t id = ((uint64_t)randomNonce() << 32) ^ (uint64_t)randomNonce() ^ (uint64_t)getpid();
+  return id;
+}
+// Looks `rec`'s dma-buf up in the node registry (caller holds the node lock): returns false — refuse — if another
+// allocation exported it before; appends it otherwise. Without a readable registry only this process's record counts.
+static bool registryAdmit(const ExportRec& rec, ExportRec* prior) {
+  static std::vector<ExportRec> local;  // this process's exports (the fallback when the file is unusable)
+  static const int regFd = open("/tmp/.ncclamd_dmabuf.reg", O_RDWR | O_CREAT | O_APPEND | O_CLOEXEC, 0666);
+  auto same = [&](const ExportRec& x) { return x.dev == rec.dev && x.ino == rec.ino; };
+  auto mine = [&](const ExportRec& x) { return x.proc == rec.proc && x.base == rec.base && x.id == rec.id; };
+  for (const ExportRec& x : local)
+    if (same(x) && !mine(x)) return *prior = x, false;
+  if (regFd >= 0) {
+    ExportRec buf[256];
+    off_t off = 0;
+    for (;;) {
+      const ssize_t got = pread(regFd, buf, sizeof(buf), off);
+      if (got <= 0) break;
+      for (size_t k = 0; k < (size_t)got / sizeof(ExportRec); k++)
+        if (same(buf[k]) && !mine(buf[k])) return *prior = buf[k], false;
+      off += got;
+    }
+    (void)!write(regFd, &rec, sizeof(rec));
+  }
+  local.push_back(rec);
+  return true;
+}
 
 static uint64_t allocationId(void* p) {
   unsigned long long id = 0;
@@ -526,32 +578,42 @@ hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd, int attempts) {
   for (int attempt = 0; attempt < attempts; attempt++) {
     if (attempt) std::this_thread::sleep_for(std::chrono::milliseconds(1 << (attempt - 1)));
     std::lock_guard<std::mutex> g(gMapMu);
+    NodeLock nl;
     e = hipMemGetHandleForAddressRange(fd, (hipDeviceptr_t)base, size, hipMemRangeHandleTypeDmaBufFd, 0);
-    if (e == hipSuccess) {
-      struct stat st;
-      if (fstat(*fd, &st) != 0) {
-        WARN("ipc: dma-buf export of %p (+%zu MiB) returned fd %d, which fstat refuses: %s", base, size >> 20, *fd,
-             strerror(errno));
-        *fd = -1;
-        return hipErrorInvalidValue;
-      }
-      const std::pair<uint64_t, uint64_t> key((uint64_t)st.st_dev, (uint64_t)st.st_ino);
-      const std::pair<uint64_t, uint64_t> who((uint64_t)base, allocationId(base));
-      auto it = gExported.find(key);
-      if (it != gExported.end() && it->second != who) {
-        // not ours to close: the number may be the runtime's, or another export's still in flight
-        WARN("ipc: dma-buf export of %p (+%zu MiB) handed back fd %d = dma-buf ino %lu, exported before for %lx: "
-             "refused (it would map the other allocation)", base, size >> 20, *fd, (unsigned long)st.st_ino,
-             (unsigned long)it->second.first);
-        *fd = -1;
-        return hipErrorInvalidValue;
-      }
-      gExported[key] = who;
-      TRACE("ipc: exported %p (+%zu MiB) as fd %d, dma-buf ino %lu", base, size >> 20, *fd, (unsigned long)st.st_ino);
-      if (attempt) INFO("ipc: dma-buf export of %p (+%zu MiB) succeeded at attempt %d", base, size >> 20, attempt + 1);
-      return e;
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      continue;
     }
-    (void)hipGetLastError();
+    struct stat st;
+    if (fstat(*fd, &st) != 0) {
+      WARN("ipc: dma-buf export of %p (+%zu MiB) returned fd %d, which fstat refuses: %s", base, size >> 20, *fd,
+           strerror(errno));
+      *fd = -1;
+      return hipErrorInvalidValue;
+    }
+    const off_t dsize = lseek(*fd, 0, SEEK_END);
+    (void)lseek(*fd, 0, SEEK_SET);
+    if (dsize >= 0 && ((uint64_t)dsize < size || (uint64_t)dsize >= size + ((uint64_t)2 << 20))) {
+      WARN("ipc: dma-buf export of %p (+%zu MiB) handed back a dma-buf of %lld bytes (ino %lu): refused (another "
+           "allocation's)", base, size >> 20, (long long)dsize, (unsigned long)st.st_ino);
+      close(*fd);
+      *fd = -1;
+      return hipErrorInvalidValue;
+    }
+    const ExportRec rec = {(uint64_t)st.st_dev, (uint64_t)st.st_ino, processId(), (uint64_t)base, allocationId(base)};
+    ExportRec prior;
+    if (!registryAdmit(rec, &prior)) {
+      WARN("ipc: dma-buf export of %p (+%zu MiB) handed back dma-buf ino %lu, exported before for %lx%s: refused "
+           "(another allocation's)", base, size >> 20, (unsigned long)st.st_ino, (unsigned long)prior.base,
+           prior.proc == rec.proc ? "" : " by another process");
+      close(*fd);
+      *fd = -1;
+      return hipErrorInvalidValue;
+    }
+    TRACE("ipc: exported %p (+%zu MiB) as fd %d, dma-buf ino %lu%s", base, size >> 20, *fd, (unsigned long)st.st_ino,
+          nl.held() ? "" : " (no node lock)");
+    if (attempt) INFO("ipc: dma-buf export of %p (+%zu MiB) succeeded at attempt %d", base, size >> 20, attempt + 1);
+    return e;
   }
   return e;
 }
@@ -764,13 +826,27 @@ static ncclResult_t importFd(int fd, uint64_t size, IpcImport* out) {
   std::lock_guard<std::mutex> g(gMapMu);
   memset(out, 0, sizeof(*out));
   out->fd = -1;
+  // the exporter checked its dma-buf's size against the allocation (ipcExportDmaBuf); the importer checks it against
+  // the size it was asked to map, so a descriptor that names another allocation is never mapped in its place
+  const off_t dsize = lseek(fd, 0, SEEK_END);
+  (void)lseek(fd, 0, SEEK_SET);
+  if (dsize >= 0 && ((uint64_t)dsize < size || (uint64_t)dsize >= size + ((uint64_t)2 << 20))) {
+    close(fd);
+    WARN("ipc: a dma-buf of %lld bytes was handed over for an allocation of %lu: refused", (long long)dsize,
+         (unsigned long)size);
+    return ncclSystemError;
+  }
   hipExternalMemoryHandleDesc hd;
   memset(&hd, 0, sizeof(hd));
   hd.type = hipExternalMemoryHandleTypeOpaqueFd;
   hd.handle.fd = fd;
   hd.size = size;
   hipExternalMemory_t em = nullptr;
-  hipError_t e = hipImportExternalMemory(&em, &hd);
+  hipError_t e;
+  {
+    NodeLock nl;
+    e = hipImportExternalMemory(&em, &hd);
+  }
   if (e != hipSuccess) {
     close(fd);
     WARN("ipc: hipImportExternalMemory(%zu MiB): %s", (size_t)(size >> 20), hipGetErrorString(e));

@@ -8,9 +8,8 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
-# The GPU tests of the staged kernels spawn multi-process communicators, where eager zero-copy is the default since
-# round 6: they keep testing what they name. The eager tests set it on explicitly, and the default
-# itself is tested with the variable removed (tests/test_gpu_eager.py, tests/test_gpu_bench.py).
+# Eager zero-copy is opt-in (NCCL_AMD_EAGER_REGISTER); a caller's environment that turns it on must
+# not change what the staged-kernel tests test. The eager tests set it explicitly.
 os.environ.setdefault("NCCL_AMD_EAGER_REGISTER", "0")
 
 

@@ -43,10 +43,10 @@ def test_bench_two_ranks_quick(built):
     assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-3
     assert 0.5 < roof["achieved"] / d["busbw_GBps"] < 2.0   # per-launch event time vs the whole step's wall time
     assert "hbm" in roof and roof["hbm"]["peak"] == 8000.0
-    # two processes: eager zero-copy by default (round 6), its HBM model and PMC entry
-    assert roof["kernel"] and "ncclamd::symKernel" in roof["kernel"], roof["kernel"]
-    assert "zero-copy" in d["config"]["workload"], d["config"]
-    assert roof["hbm"]["algorithmic_bytes_per_launch"] == int(2.5 * 256 * 2**20), roof["hbm"]
+    # the library's defaults: the staged direct kernel, its HBM model (3S + 2(n-1)/n S = 4S at n = 2)
+    assert roof["kernel"] and "ncclamd::collKernel<float, 0, 0>" in roof["kernel"], roof["kernel"]
+    assert "direct scatter-reduce-gather" in d["config"]["workload"], d["config"]
+    assert roof["hbm"]["algorithmic_bytes_per_launch"] == 4 * 256 * 2**20, roof["hbm"]
     # every N line carries the host-core baseline (rank 0, same run) and the PMC traffic
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1, d["cpu_baseline"]
     assert roof["traffic"] and roof["traffic"] > 0, roof

@@ -1,9 +1,9 @@
 """End to end on the north star's path: a torch DistributedDataParallel training step whose gradient
 buckets are all-reduced by this engine through a DDP comm hook (nccl_amd.ddp_comm_hook), 2 processes on the
 one GPU. After identical steps from identical weights on different data, both ranks must hold identical
-parameters, equal to a single-process reference step on the averaged gradient. `default`: a wider model with
-buckets of several MiB and the library's defaults, so the buckets run eager zero-copy (the multi-process default
-since round 6); `staged`: small buckets on the staged / LL kernels."""
+parameters, equal to a single-process reference step on the averaged gradient. `eager`: a wider model with
+buckets of several MiB and NCCL_AMD_EAGER_REGISTER=-1, so the buckets run eager zero-copy;
+`staged`: small buckets on the staged / LL kernels (the defaults)."""
 import multiprocessing as mp
 import os
 import socket
@@ -31,7 +31,7 @@ def _worker(rank, world, port, uid, q, wide):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), NCCL_AMD_SPIN_TIMEOUT_MS="30000")
         if wide:
-            os.environ.pop("NCCL_AMD_EAGER_REGISTER", None)  # the library's default
+            os.environ["NCCL_AMD_EAGER_REGISTER"] = "-1"  # eager zero-copy across processes
             os.environ.update(NCCL_DEBUG="TRACE", NCCL_DEBUG_FILE=f"/tmp/nccl_amd_ddp_{os.getpid()}.log")
         import torch
         import torch.distributed as dist
@@ -65,9 +65,9 @@ def _worker(rank, world, port, uid, q, wide):
         q.put((rank, repr(e), -1, 0))
 
 
-@pytest.mark.parametrize("mode", ["staged", "default"])
+@pytest.mark.parametrize("mode", ["staged", "eager"])
 def test_ddp_step_through_engine(built, mode):
-    wide = mode == "default"
+    wide = mode == "eager"
     import numpy as np
     import torch
     import nccl_amd

@@ -137,12 +137,12 @@ def test_eager_zero_copy_multi_process(built, nranks, fail_dmabuf_rank, fail_exp
 
 
 def _default_worker(rank, nranks, uid, q, fail_rank=-1):
-    """The library's default (NCCL_AMD_EAGER_REGISTER unset): a communicator spanning processes runs an eligible
-    collective on the ranks' own buffers (round 6). fail_rank: that rank cannot register anything
-    (NCCL_AMD_REG_FAIL_EXPORT=1), so the init-time probe (register.cc eagerProbe) fails there and every rank runs
-    the staged kernel instead."""
+    """NCCL_AMD_EAGER_REGISTER=-1 (on for communicators spanning processes): such a communicator
+    runs an eligible collective on the ranks' own buffers after its init-time probe passed. fail_rank: that rank cannot
+    register anything (NCCL_AMD_REG_FAIL_EXPORT=1), so the probe (register.cc eagerProbe) fails there and every rank
+    runs the staged kernel instead."""
     try:
-        os.environ.pop("NCCL_AMD_EAGER_REGISTER", None)
+        os.environ["NCCL_AMD_EAGER_REGISTER"] = "-1"
         if rank == fail_rank:
             os.environ["NCCL_AMD_REG_FAIL_EXPORT"] = "1"
         logf = _trace_env(f"eagerdefault{nranks}")
@@ -178,7 +178,7 @@ def _default_worker(rank, nranks, uid, q, fail_rank=-1):
 
 
 @pytest.mark.parametrize("fail_rank", [-1, 1])
-def test_eager_zero_copy_is_the_multi_process_default(built, fail_rank):
+def test_eager_zero_copy_across_processes_with_its_probe(built, fail_rank):
     res = _spawn(_default_worker, 2, args=(fail_rank,))
     bad = [e for r in sorted(res) for e in res[r][0]]
     assert not bad, "\n".join(bad)

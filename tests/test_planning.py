@@ -600,12 +600,14 @@ def test_eager_registration_eligibility(exe):
     shares (bytes, the size table), so every rank takes the same kernel."""
     on = dict(NCCL_AMD_EAGER_REGISTER=1)
     S = (256 << 20) // 4
-    assert plan(exe, 2, "ar", 7, S)["algo"] == "direct"                       # default, one process: staged
-    # default since round 6: on for communicators spanning processes (every peer serving registrations); =0 opts out
-    assert plan(exe, 2, "ar", 7, S, PLAN_MULTIPROCESS=1)["algo"] == "sym"
-    assert plan(exe, 8, "rs", 7, S // 8, PLAN_MULTIPROCESS=1)["algo"] == "sym"
-    assert plan(exe, 2, "ar", 7, S, PLAN_MULTIPROCESS=1, NCCL_AMD_EAGER_REGISTER=0)["algo"] == "direct"
-    assert plan(exe, 2, "ar", 7, (1 << 20) // 4, PLAN_MULTIPROCESS=1)["algo"] == "oneshot"
+    assert plan(exe, 2, "ar", 7, S)["algo"] == "direct"                       # default: off
+    assert plan(exe, 2, "ar", 7, S, PLAN_MULTIPROCESS=1)["algo"] == "direct"  # ... across processes too
+    # -1: on for communicators spanning processes (every peer serving registrations), off within one process
+    auto = dict(NCCL_AMD_EAGER_REGISTER=-1)
+    assert plan(exe, 2, "ar", 7, S, PLAN_MULTIPROCESS=1, **auto)["algo"] == "sym"
+    assert plan(exe, 8, "rs", 7, S // 8, PLAN_MULTIPROCESS=1, **auto)["algo"] == "sym"
+    assert plan(exe, 2, "ar", 7, S, **auto)["algo"] == "direct"
+    assert plan(exe, 2, "ar", 7, (1 << 20) // 4, PLAN_MULTIPROCESS=1, **auto)["algo"] == "oneshot"
     assert plan(exe, 2, "ar", 7, S, **on)["algo"] == "sym"
     assert plan(exe, 8, "ar", 7, S, **on)["algo"] == "sym"
     assert plan(exe, 8, "rs", 7, S // 8, **on)["algo"] == "sym"
