@@ -514,18 +514,38 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested) {
 // (below) did not remove it (2 such exports in 5 runs, both caught), so it is not a race between concurrent calls
 // but stale state in the export path. Two checks, both under the node lock:
 //  * the dma-buf's size (its llseek end) must be the allocation's (catches (2));
-//  * a node-wide registry of every dma-buf the library's processes exported (/tmp/.ncclamd_dmabuf.reg: inode, the
-//    exporting process's random id, base, buffer id): a dma-buf exported before for any other allocation is refused
+//  * a node-wide registry of every dma-buf the library's processes exported (/tmp/.ncclamd_dmabuf.<uid>.reg: inode,
+//    the exporting process's random id, base, buffer id): a dma-buf exported before for any other allocation is refused
 //    (catches (1), and (2) at equal sizes). The same allocation may get its dma-buf back.
 // A refused export's descriptor is closed (the API hands it to the caller) and the caller falls back as for any
 // refused export (hipIpc handle for explicit registrations, the bounce allocation for eager ones).
+// The node lock and the registry are files of this user in /tmp (another user's processes keep their own). The lock is
+// waited for at most NCCL_AMD_DMABUF_LOCK_TIMEOUT_MS (5 s; it is held only across one runtime call): a process stuck
+// while holding it delays the others that long, then they go on without it (said once).
+static std::string nodeFile(const char* what) {
+  return std::string("/tmp/.ncclamd_dmabuf.") + std::to_string((unsigned long)getuid()) + "." + what;
+}
 struct NodeLock {  // every dma-buf export and import of the library's processes on a node, one at a time
   int fd = -1;
   NodeLock() {
     static const int lockFd = paramInt("NCCL_AMD_DMABUF_NODE_LOCK", 1)
-                                  ? open("/tmp/.ncclamd_dmabuf.lock", O_RDWR | O_CREAT | O_CLOEXEC, 0666)
+                                  ? open(nodeFile("lock").c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0600)
                                   : -1;
-    if (lockFd >= 0 && flock(lockFd, LOCK_EX) == 0) fd = lockFd;
+    static const int64_t waitMs = paramInt("NCCL_AMD_DMABUF_LOCK_TIMEOUT_MS", 5000);
+    if (lockFd < 0) return;
+    const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(waitMs);
+    while (flock(lockFd, LOCK_EX | LOCK_NB) != 0) {
+      if (errno != EWOULDBLOCK && errno != EINTR) return;
+      if (std::chrono::steady_clock::now() > deadline) {
+        static std::atomic<bool> said{false};
+        if (!said.exchange(true))
+          WARN("ipc: %s held by another process for %lld ms: going on without it", nodeFile("lock").c_str(),
+               (long long)waitMs);
+        return;
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    fd = lockFd;
   }
   ~NodeLock() {
     if (fd >= 0) (void)flock(fd, LOCK_UN);
@@ -543,7 +563,7 @@ static uint64_t processId() {
 // allocation exported it before; appends it otherwise. Without a readable registry only this process's record counts.
 static bool registryAdmit(const ExportRec& rec, ExportRec* prior) {
   static std::vector<ExportRec> local;  // this process's exports (the fallback when the file is unusable)
-  static const int regFd = open("/tmp/.ncclamd_dmabuf.reg", O_RDWR | O_CREAT | O_APPEND | O_CLOEXEC, 0666);
+  static const int regFd = open(nodeFile("reg").c_str(), O_RDWR | O_CREAT | O_APPEND | O_CLOEXEC, 0600);
   auto same = [&](const ExportRec& x) { return x.dev == rec.dev && x.ino == rec.ino; };
   auto mine = [&](const ExportRec& x) { return x.proc == rec.proc && x.base == rec.base && x.id == rec.id; };
   for (const ExportRec& x : local)
