@@ -2,6 +2,7 @@
 # A/B: foldRange with (this build) and without (abvar/nopf, -DNCCL_AMD_FOLD_PREFETCH=0) the next batch's first
 # source loaded during the last source's fold; n-process 256 MiB fp32 AllReduce on the one GPU (scripts/mp_rank.py,
 # rank 0's event time per AllReduce), eager zero-copy and staged at n = 2 and 8, builds interleaved over 3 rounds.
+# Build the variant first: make lib EXTRA=-DNCCL_AMD_FOLD_PREFETCH=0 BUILD=build_ab_nopf LIBDIR=abvar/nopf
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp NCCL_AMD_SPIN_TIMEOUT_MS=20000
