@@ -23,7 +23,10 @@ DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
 all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test mapcheck-test xgmi-probe atomicity-probe \
-     fp8-probe release-probe reuse-probe
+     fp8-probe release-probe reuse-probe export-check-test
+
+.PHONY: export-check-test
+export-check-test: tests/native/export_check_test
 
 lib: $(LIBDIR)/libnccl.so
 
@@ -135,6 +138,11 @@ build/asan/ipc_server_test build/tsan/ipc_server_test: tests/native/ipc_server_t
 	@mkdir -p $(dir $@)
 	$(SANCXX) $(if $(findstring asan,$@),$(ASAN),$(TSAN)) -o $@ tests/native/ipc_server_test.cc $(SRCDIR)/ipc.cc \
 	  $(SRCDIR)/debug.cc -lpthread $(HIPRT)
+
+# CPU test of the stale dma-buf export checks (ipc.cc ipcAdmitExport) with memfd files in place of dma-bufs
+tests/native/export_check_test: tests/native/export_check_test.cc $(SRCDIR)/ipc.cc $(SRCDIR)/debug.cc $(HDRS)
+	$(CXX) -O1 -g -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Iinclude -o $@ tests/native/export_check_test.cc \
+	  $(SRCDIR)/ipc.cc $(SRCDIR)/debug.cc -lpthread $(HIPRT)
 
 build/asan/plan_test: tests/native/plan_test.cc $(SRCDIR)/enqueue.cc $(SRCDIR)/debug.cc $(HDRS)
 	@mkdir -p $(dir $@)

@@ -148,6 +148,7 @@ ncclResult_t ipcServerStart(ncclComm* comm);
 void ipcServerStop(ncclComm* comm);
 ncclResult_t ipcExport(ncclComm* comm, void* base, size_t size, IpcDesc* d);
 hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd, int attempts = 5);  // under gMapMu (ipc.cc)
+bool ipcAdmitExport(int fd, void* base, size_t size);  // its stale-export checks (ipc.cc; CPU-tested)
 void ipcUnexport(ncclComm* comm, const IpcDesc& d);
 ncclResult_t ipcPublish(ncclComm* comm, int fd, size_t size, IpcDesc* d);  // serve an fd (owned) under a new key
 ncclResult_t ipcFetchFd(const IpcDesc& d, int* fd);  // an exporter's fd for d, over its fd server (bounded)

@@ -523,7 +523,8 @@ bool ipcLegacyAllowed(int runtimeVersion, size_t size, bool requested) {
 // waited for at most NCCL_AMD_DMABUF_LOCK_TIMEOUT_MS (5 s; it is held only across one runtime call): a process stuck
 // while holding it delays the others that long, then they go on without it (said once).
 static std::string nodeFile(const char* what) {
-  return std::string("/tmp/.ncclamd_dmabuf.") + std::to_string((unsigned long)getuid()) + "." + what;
+  const char* dir = paramStr("NCCL_AMD_DMABUF_NODE_DIR");  // tests: a directory of their own
+  return std::string(dir ? dir : "/tmp") + "/.ncclamd_dmabuf." + std::to_string((unsigned long)getuid()) + "." + what;
 }
 struct NodeLock {  // every dma-buf export and import of the library's processes on a node, one at a time
   int fd = -1;
@@ -555,8 +556,13 @@ struct NodeLock {  // every dma-buf export and import of the library's processes
 struct ExportRec {
   uint64_t dev, ino, proc, base, id;
 };
-static uint64_t processId() {
-  static const uint64_t id = ((uint64_t)randomNonce() << 32) ^ (uint64_t)randomNonce() ^ (uint64_t)getpid();
+static uint64_t processId() {  // random per process (a forked child draws its own)
+  static uint64_t id = 0;
+  static pid_t owner = 0;
+  if (owner != getpid()) {
+    owner = getpid();
+    id = ((uint64_t)randomNonce() << 32) ^ (uint64_t)randomNonce() ^ (uint64_t)owner;
+  }
   return id;
 }
 // Looks `rec`'s dma-buf up in the node registry (caller holds the node lock): returns false — refuse — if another
@@ -593,6 +599,37 @@ static uint64_t allocationId(void* p) {
   return (uint64_t)id;
 }
 
+// The checks above on a descriptor an export handed back for [base, +size) (the caller holds the node lock): true =
+// admitted (and recorded); false = refused, `fd` closed. Separate from the export so a CPU test can drive it with
+// descriptors of its own (tests/native/export_check_test.cc).
+bool ipcAdmitExport(int fd, void* base, size_t size) {
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    WARN("ipc: dma-buf export of %p (+%zu MiB) returned fd %d, which fstat refuses: %s", base, size >> 20, fd,
+         strerror(errno));
+    return false;
+  }
+  const off_t dsize = lseek(fd, 0, SEEK_END);
+  (void)lseek(fd, 0, SEEK_SET);
+  if (dsize >= 0 && ((uint64_t)dsize < size || (uint64_t)dsize >= size + ((uint64_t)2 << 20))) {
+    WARN("ipc: dma-buf export of %p (+%zu MiB) handed back a dma-buf of %lld bytes (ino %lu): refused (another "
+         "allocation's)", base, size >> 20, (long long)dsize, (unsigned long)st.st_ino);
+    close(fd);
+    return false;
+  }
+  const ExportRec rec = {(uint64_t)st.st_dev, (uint64_t)st.st_ino, processId(), (uint64_t)base, allocationId(base)};
+  ExportRec prior;
+  if (!registryAdmit(rec, &prior)) {
+    WARN("ipc: dma-buf export of %p (+%zu MiB) handed back dma-buf ino %lu, exported before for %lx%s: refused "
+         "(another allocation's)", base, size >> 20, (unsigned long)st.st_ino, (unsigned long)prior.base,
+         prior.proc == rec.proc ? "" : " by another process");
+    close(fd);
+    return false;
+  }
+  TRACE("ipc: exported %p (+%zu MiB) as fd %d, dma-buf ino %lu", base, size >> 20, fd, (unsigned long)st.st_ino);
+  return true;
+}
+
 hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd, int attempts) {
   hipError_t e = hipErrorInvalidValue;
   for (int attempt = 0; attempt < attempts; attempt++) {
@@ -604,34 +641,10 @@ hipError_t ipcExportDmaBuf(void* base, size_t size, int* fd, int attempts) {
       (void)hipGetLastError();
       continue;
     }
-    struct stat st;
-    if (fstat(*fd, &st) != 0) {
-      WARN("ipc: dma-buf export of %p (+%zu MiB) returned fd %d, which fstat refuses: %s", base, size >> 20, *fd,
-           strerror(errno));
+    if (!ipcAdmitExport(*fd, base, size)) {
       *fd = -1;
       return hipErrorInvalidValue;
     }
-    const off_t dsize = lseek(*fd, 0, SEEK_END);
-    (void)lseek(*fd, 0, SEEK_SET);
-    if (dsize >= 0 && ((uint64_t)dsize < size || (uint64_t)dsize >= size + ((uint64_t)2 << 20))) {
-      WARN("ipc: dma-buf export of %p (+%zu MiB) handed back a dma-buf of %lld bytes (ino %lu): refused (another "
-           "allocation's)", base, size >> 20, (long long)dsize, (unsigned long)st.st_ino);
-      close(*fd);
-      *fd = -1;
-      return hipErrorInvalidValue;
-    }
-    const ExportRec rec = {(uint64_t)st.st_dev, (uint64_t)st.st_ino, processId(), (uint64_t)base, allocationId(base)};
-    ExportRec prior;
-    if (!registryAdmit(rec, &prior)) {
-      WARN("ipc: dma-buf export of %p (+%zu MiB) handed back dma-buf ino %lu, exported before for %lx%s: refused "
-           "(another allocation's)", base, size >> 20, (unsigned long)st.st_ino, (unsigned long)prior.base,
-           prior.proc == rec.proc ? "" : " by another process");
-      close(*fd);
-      *fd = -1;
-      return hipErrorInvalidValue;
-    }
-    TRACE("ipc: exported %p (+%zu MiB) as fd %d, dma-buf ino %lu%s", base, size >> 20, *fd, (unsigned long)st.st_ino,
-          nl.held() ? "" : " (no node lock)");
     if (attempt) INFO("ipc: dma-buf export of %p (+%zu MiB) succeeded at attempt %d", base, size >> 20, attempt + 1);
     return e;
   }
