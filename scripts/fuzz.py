@@ -69,11 +69,11 @@ def settings(rng):
         env["NCCL_LL_BUFFSIZE"] = str(rng.choice([4096, 65536, 524288]))
     if rng.random() < 0.15:
         env["NCCL_LL128_BUFFSIZE"] = str(rng.choice([32768, 262144]))
-    # eager zero-copy on the cases' plain torch buffers (register.cc), small thresholds too; unset = the library's
-    # default (on across processes since round 6, so scripts/fuzz_mp.py runs it), "0" = the staged kernels
+    # eager zero-copy on the cases' plain torch buffers (register.cc), small thresholds too: "1" on, "-1" on across
+    # processes only (scripts/fuzz_mp.py; off in this one-process fuzz), "0" or unset off (the default)
     r = rng.random()
     if r < 0.25:
-        env["NCCL_AMD_EAGER_REGISTER"] = "0"
+        env["NCCL_AMD_EAGER_REGISTER"] = "-1"
     elif r < 0.5:
         env["NCCL_AMD_EAGER_REGISTER"] = "1"
     if r < 0.5 or rng.random() < 0.5:
