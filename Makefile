@@ -23,7 +23,7 @@ DEVOBJ   := $(DEVSRC:%.hip=$(BUILD)/%.o)
 HDRS     := $(wildcard $(SRCDIR)/*.h) include/nccl.h
 
 all: lib oracle numerics-host bootstrap-test tuner-test nccl-perf comm-examples plan-test mapcheck-test xgmi-probe atomicity-probe \
-     fp8-probe release-probe reuse-probe export-check-test
+     fp8-probe release-probe reuse-probe export-check-test barrier-probe
 
 .PHONY: export-check-test
 export-check-test: tests/native/export_check_test
@@ -178,6 +178,14 @@ tests/native/mapcheck_test: tests/native/mapcheck_test.cc $(SRCDIR)/mapcheck.cc 
 	  $(SRCDIR)/mapcheck.cc $(SRCDIR)/debug.cc -lpthread
 
 .PHONY: mapcheck-test
+
+# does a kernel queued behind another on the same stream start while the first is resident?
+barrier-probe: tests/native/barrier_probe
+
+tests/native/barrier_probe: tests/native/barrier_probe.hip
+	$(HIPCC) -O2 --offload-arch=$(ARCH) -o $@ $<
+
+.PHONY: barrier-probe
 
 # does unmapping an imported dma-buf mapping wait for the device? (decides where peers' mappings are released,
 # DESIGN.md §3.2)

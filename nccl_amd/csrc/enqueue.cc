@@ -397,15 +397,10 @@ int linkChannelBudget(int n) {
 // Channels per launch that stay co-resident when several ranks share a GPU (NCCL_MULTI_RANK_GPU_ENABLE, the one-GPU
 // rehearsals). A channel spins on the same channel of every peer, so a collective progresses only while, for some
 // channel, every rank's workgroup is resident. A GPU holds 2 of these workgroups per CU (512 threads, 4 waves per
-// SIMD, kernels.h kCoResident). One rank per GPU runs one collective at a time there (stream order), so every channel
-// fits: 2 x CUs. Ranks SHARING a GPU are not in step: a fast rank launches its next collective (or the next on another
-// communicator from the same stream) while slow ranks still finish this one, so two generations of collectives are in
-// flight on the GPU — never three: a rank starting generation k+2 had its k+1 complete, which needed every rank's k+1
-// started, so every rank's k had completed (one stream per rank). The round-5 cap, 2 x CUs / ranks per GPU, fitted ONE
-// generation exactly (8 ranks x 64 = 512 slots): the fast ranks' next-generation workgroups, spinning on the slow
-// ranks' next generation, held slots the slow ranks' current-generation workgroups still waited for, and every rank
-// stalled until the spin timeout (the n = 8 rehearsal stall of round 5). Both generations fit with
-// CUs / ranks per GPU.
+// SIMD, kernels.h kCoResident). One rank per GPU: 2 x CUs. Ranks sharing a GPU: CUs / ranks per GPU, half the slots
+// kept free. Slot arithmetic says 2 x CUs / ranks per GPU would fit (a stream never has two launches resident,
+// tests/native/barrier_probe), yet round 5's n = 8 rehearsal stalled once at exactly that; the cause is not
+// established, so the margin stays.
 int coResidentChannelCap(int minCUs, int ranksPerGpu) {
   if (minCUs < 1) minCUs = 256;
   if (ranksPerGpu < 1) ranksPerGpu = 1;

@@ -139,7 +139,7 @@ static ncclResult_t fillPeerInfo(ncclComm* comm, PeerInfo* p) {
 
 // Channels of one launch must all be resident at once on every GPU (a channel spins on the same
 // channel of its peers). With several ranks on one GPU (NCCL_MULTI_RANK_GPU_ENABLE / test boxes) the
-// launches share the CUs, and two generations of them can be in flight (enqueue.cc coResidentChannelCap).
+// launches share the CUs, with half the slots kept free as a margin (enqueue.cc coResidentChannelCap).
 // Every rank computes this from the same peer table, so all agree.
 static void computeChannelCap(ncclComm* c) {
   int minCU = 1 << 30, maxPer = 1;
