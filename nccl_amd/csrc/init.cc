@@ -150,7 +150,11 @@ static void computeChannelCap(ncclComm* c) {
     if (c->peers[i].numCUs > 0 && c->peers[i].numCUs < minCU) minCU = c->peers[i].numCUs;
   }
   if (minCU == (1 << 30)) minCU = 256;
-  const int cap = coResidentChannelCap(minCU, maxPer);
+  int cap = coResidentChannelCap(minCU, maxPer);
+  // diagnostics (set alike on every rank): the shared-GPU cap itself, up to every slot (2 x CUs / ranks per GPU) —
+  // the round-5 setting is NCCL_AMD_SHARED_GPU_CHANNELS=64 at 8 ranks per GPU
+  const int64_t forced = maxPer > 1 ? paramInt("NCCL_AMD_SHARED_GPU_CHANNELS", 0) : 0;
+  if (forced > 0) cap = (int)std::min<int64_t>(forced, 2 * minCU / maxPer);
   c->chanCap = cap < c->maxChannels ? cap : c->maxChannels;
   bool oneDevice = true;
   for (size_t i = 1; i < c->peers.size(); i++) oneDevice = oneDevice && !strcmp(c->peers[i].busId, c->peers[0].busId);
