@@ -644,8 +644,18 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
     torch.cuda.synchronize()
     same = bool(torch.equal(ref, h_out))  # ... equals the one-stream result bit for bit
     nchunk, ms_p = min(sweep, key=lambda t: t[1])
+    # direct: the collective on the pinned host buffers themselves (the reference accepts any pointer the device can
+    # reach, argcheck.cc:12-28) — its kernel reads and writes across PCIe, both directions at once, with no copies,
+    # chunks or pipeline fill; the one-rank copy caps its grid for host buffers (NCCL_AMD_HOST_COPY_GRID)
+    h_out.zero_()
+    ms_d = _time_ms(lambda: comm.all_reduce_raw(h_in.data_ptr(), h_out.data_ptr(), count, 7, 0, stream.cuda_stream),
+                    stream, 5, warmup=2)
+    ms_d = max_over_ranks(dist, [ms_d])[0]
+    torch.cuda.synchronize()
+    same_d = bool(torch.equal(ref, h_out))
     # PCIe Gen5 x16 bound: 57 GB/s one direction, 96.5 GB/s both at once on the SDMA engines
-    # (profiles/r03_host_staged_pipeline.json): S each way at 96.5 / 2 GB/s per direction
+    # (profiles/r03_host_staged_pipeline.json): S each way at 96.5 / 2 GB/s per direction. The direct kernel's
+    # loads and stores exceed it (about 100 GB/s both ways at N = 1): the bound is the copy engines', not the link's
     bound_ms = S / (96.5e9 / 2) * 1e3
     return {"bytes_per_rank": S, "ms_per_step": round(ms, 4), "algbw_GBps_incl_pcie": round(S / (ms * 1e-3) / 1e9, 2),
             "device_resident_ms": round(ms_dev, 4),
@@ -656,7 +666,11 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
                           "sweep_ms": {str(k): round(v, 4) for k, v in sweep},
                           "check": "pass" if same else "FAIL",
                           "method": "chunks timed at 4 / 8 / 16, the fastest reported: H2D stream, AllReduce on the "
-                                    "launch stream, D2H stream, event-chained"}}
+                                    "launch stream, D2H stream, event-chained"},
+            "direct": {"ms_per_step": round(ms_d, 4), "algbw_GBps_incl_pcie": round(S / (ms_d * 1e-3) / 1e9, 2),
+                       "frac_of_pcie_bound": round(bound_ms / ms_d, 3), "speedup_vs_pipelined": round(ms_p / ms_d, 3),
+                       "check": "pass" if same_d else "FAIL",
+                       "method": "ncclAllReduce with the pinned host buffers as send and receive buffers, no copies"}}
 
 
 def cpu_baseline(count: int, budget_s: float, nbuf: int = 8):

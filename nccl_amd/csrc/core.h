@@ -274,6 +274,7 @@ struct CommTuning {
   int64_t oneShotChannelBytes;  // NCCL_AMD_ONESHOT_CHANNEL_BYTES
   int copyVariant;          // NCCL_AMD_COPY_VARIANT (nRanks == 1 copy kernel, diagnostics)
   int64_t copyGrid;         // NCCL_AMD_COPY_GRID (cap on its workgroups; default: one per 16 KiB tile)
+  int64_t hostCopyGrid;     // NCCL_AMD_HOST_COPY_GRID (the cap when a buffer is pinned host memory; 0 = none)
   int copyXcdShift;         // NCCL_AMD_COPY_XCD_SHIFT (6): each XCD copies runs of 2^shift consecutive tiles
   int64_t ringChunkBytes;   // NCCL_ALGO=RING AllReduce chunk: NCCL_BUFFSIZE / NCCL_STEPS * ALLREDUCE_CHUNKSTEPS
   int refOrder;             // NCCL_AMD_REF_ORDER: AllReduce on the direct kernel in the reference's ring partition

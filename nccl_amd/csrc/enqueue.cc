@@ -263,6 +263,10 @@ void loadTuning(CommTuning* t) {
   t->oneShotChannelBytes = paramInt("NCCL_AMD_ONESHOT_CHANNEL_BYTES", 16 << 10);
   t->copyVariant = (int)paramInt("NCCL_AMD_COPY_VARIANT", 0);
   t->copyGrid = paramInt("NCCL_AMD_COPY_GRID", 1 << 30);
+  // a copy that crosses PCIe (a pinned host send or receive buffer) is bound by the link's outstanding requests, not
+  // by CUs: one workgroup per CU moves a 256 MiB host-to-host bucket in 5.37 ms against 6.28 ms for the HBM default
+  // of one per tile (grid caps 64-320 within 1 %, scripts/host_direct_sweep.sh)
+  t->hostCopyGrid = paramInt("NCCL_AMD_HOST_COPY_GRID", 256);
   t->copyXcdShift = (int)paramInt("NCCL_AMD_COPY_XCD_SHIFT", 6);
   // the reference's RING/SIMPLE chunk: stepSize (NCCL_BUFFSIZE / NCCL_STEPS) x ALLREDUCE_CHUNKSTEPS (NCCL_STEPS / 2),
   // in 512-byte grains (enqueue.cc:2222-2225, 2321; collectives.h:19-20; default NCCL_BUFFSIZE 4 MiB, init.cc:813)
@@ -416,6 +420,16 @@ void resolveLinkChannels(CommTuning* t, int nranks, bool userMaxCTAs) {
 // The fence default once the ranks' devices are known (all ranks see the same peer table and rank 0's knobs).
 void resolveFence(CommTuning* t, bool oneDevice) {
   if (t->p2pFence < 0 && oneDevice) t->protoFlags |= 8;
+}
+
+// pinned (or registered) host memory mapped for the device: a kernel's accesses to it cross PCIe
+static bool isHostMemory(const void* p) {
+  hipPointerAttribute_t attr;
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost;
 }
 
 // Pointer check (reference argcheck.cc:12-28), active with NCCL_CHECK_POINTERS=1.
@@ -715,6 +729,10 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     p.copyVariant = comm->tune.copyVariant;
     p.copyGrid = comm->tune.copyGrid;
     p.copyXcdShift = comm->tune.copyXcdShift;
+    // one pointer query per copy of >= 1 MiB (about a microsecond, overlapped with the GPU's work)
+    if (comm->tune.hostCopyGrid > 0 && bytes >= (1u << 20) &&
+        (isHostMemory(info.sendbuff) || isHostMemory(info.recvbuff)))
+      p.copyGrid = std::min<int64_t>(p.copyGrid, comm->tune.hostCopyGrid);
     return ncclSuccess;
   }
 

@@ -1,6 +1,9 @@
 """Host-staged bucket pipelines (bench.py host_staged): 256 MiB fp32 from pinned host memory, one-rank
 ncclAllReduce, back to pinned host memory. Variants: serial on one stream; 3 streams with the AllReduce on its own
-stream (a); the AllReduce behind its chunk's H2D on the H2D stream (d); chunk counts 4 / 16. One JSON line."""
+stream (a); the AllReduce behind its chunk's H2D on the H2D stream (d); copies only, no AllReduce (c: isolates how
+the runtime moves the chunks); chunk counts from HOST_PIPE_CHUNKS (default 4,16), modes from HOST_PIPE_MODES
+(default a,d); the AllReduce on the pinned host buffers themselves (direct: the kernel crosses PCIe). One JSON
+line."""
 import json
 import os
 import sys
@@ -47,6 +50,8 @@ def make(nch, mode):
                     ev_ar[k].record(s_in)
                 else:
                     ev_in[k].record(s_in)
+            if mode == "c":  # D2H of the chunk just copied in, no AllReduce
+                ev_ar[k] = ev_in[k]
             if mode == "a":
                 s_ar.wait_event(ev_in[k])
                 ar(lo, hi, s_ar)
@@ -72,13 +77,23 @@ def timed(fn, it=5):
     return e0.elapsed_time(e1) / it
 
 
+def kernel_direct():  # the collective's kernel reads and writes the pinned host buffers over PCIe, no copies
+    comm.all_reduce_raw(h_in.data_ptr(), h_out.data_ptr(), count, 7, 0, main.cuda_stream)
+
+
 r = {"serial_ms": round(timed(serial), 3)}
 want = h_in.clone()
-for nch in (4, 16):
-    for mode in ("a", "d"):
+if os.environ.get("HOST_PIPE_DIRECT", "1") == "1":
+    h_out.zero_()
+    r["direct_ms"] = round(timed(kernel_direct), 3)
+    r["direct_ok"] = bool(torch.equal(h_out, want))
+chunks = [int(c) for c in os.environ.get("HOST_PIPE_CHUNKS", "4,16").split(",") if c]
+modes = os.environ.get("HOST_PIPE_MODES", "a,d").split(",")
+for nch in chunks:
+    for mode in modes:
         h_out.zero_()
         ms = timed(make(nch, mode))
-        ok = bool(torch.equal(h_out, want))
+        ok = bool(torch.equal(h_out, want)) if mode != "c" else None
         r[f"{mode}{nch}_ms"] = round(ms, 3)
         r[f"{mode}{nch}_ok"] = ok
 r["GBps_note"] = "bucket bytes / ms (256 MiB)"

@@ -700,3 +700,36 @@ def test_reference_buffer_and_channel_knobs(built):
     assert not errs, errs
     slab = 16 * 2 * 2 * 2 * (128 << 10)  # channels x kinds x slots x ranks x (BUFFSIZE / 2 slots)
     assert slab <= total < slab + (64 << 20), (total, slab)
+
+
+@pytest.mark.parametrize("count", [1_000, 300_001, 4_000_037])
+def test_collectives_on_pinned_host_buffers(two_comms, count):
+    """Pinned host buffers as send and receive buffers (the reference's pointer check accepts any pointer with a
+    device mapping, argcheck.cc:12-28): the kernels read and write them across PCIe, on the LL and staged paths."""
+    import torch
+    import nccl_amd
+    import oracle
+    comms, streams = two_comms
+    ins = _inputs(2, count, seed=31)
+    sends = [torch.from_numpy(x).pin_memory() for x in ins]
+    recvs = [torch.zeros(count, dtype=torch.float32).pin_memory() for _ in range(2)]
+    gathered = [torch.zeros(2 * count, dtype=torch.float32).pin_memory() for _ in range(2)]
+    torch.cuda.synchronize()
+    nccl_amd.group_start()
+    for c, s, x, y in zip(comms, streams, sends, recvs):
+        c.all_reduce_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+    nccl_amd.group_end()
+    torch.cuda.synchronize()
+    want = oracle.all_reduce(ins, 7, 0)
+    for r, y in enumerate(recvs):
+        got = y.numpy()
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, f"AllReduce rank {r}: {bad.size} mismatches, first {bad[:6].tolist()}"
+    nccl_amd.group_start()
+    for c, s, x, y in zip(comms, streams, sends, gathered):
+        c.all_gather_raw(x.data_ptr(), y.data_ptr(), count, 7, s.cuda_stream)
+    nccl_amd.group_end()
+    torch.cuda.synchronize()
+    for r, y in enumerate(gathered):
+        assert np.array_equal(y.numpy(), np.concatenate(ins)), f"AllGather rank {r}"
+    assert all(c.async_error() == 0 for c in comms)

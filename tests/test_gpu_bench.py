@@ -85,6 +85,11 @@ def test_bench_one_gpu_line(built):
     assert "copyKernel" in roof["kernel"], roof
     assert 0 < roof["frac_cold"] <= 1.0 and roof["achieved_cold"] > 0
     assert d["cpu_baseline"]["value"] > 0 and d["cpu_baseline"]["cores"] >= 1
+    # the host-staged bucket: the pipelined copies and the collective on the pinned host buffers, both bitwise equal
+    # to the one-stream result
+    hs = d["host_staged"]
+    assert hs["pipelined"]["check"] == "pass" and hs["direct"]["check"] == "pass", hs
+    assert hs["direct"]["ms_per_step"] > 0
 
 
 def test_bench_reports_a_failed_init(built):
