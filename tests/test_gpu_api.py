@@ -732,4 +732,43 @@ def test_collectives_on_pinned_host_buffers(two_comms, count):
     torch.cuda.synchronize()
     for r, y in enumerate(gathered):
         assert np.array_equal(y.numpy(), np.concatenate(ins)), f"AllGather rank {r}"
+    # ReduceScatter of the gathered (2 * count) buffers, and Reduce to root 1, host buffers on both sides
+    scat = [torch.zeros(count, dtype=torch.float32).pin_memory() for _ in range(2)]
+    nccl_amd.group_start()
+    for c, s, x, y in zip(comms, streams, gathered, scat):
+        c.reduce_scatter_raw(x.data_ptr(), y.data_ptr(), count, 7, 0, s.cuda_stream)
+    nccl_amd.group_end()
+    torch.cuda.synchronize()
+    want_rs = oracle.reduce_scatter([y.numpy().copy() for y in gathered], 7, 0)
+    for r, y in enumerate(scat):
+        assert np.array_equal(y.numpy(), want_rs[r]), f"ReduceScatter rank {r}"
+    red = torch.zeros(count, dtype=torch.float32).pin_memory()
+    nccl_amd.group_start()
+    for r, (c, s, x) in enumerate(zip(comms, streams, sends)):
+        c.reduce_raw(x.data_ptr(), red.data_ptr() if r == 1 else None, count, 7, 0, 1, s.cuda_stream)
+    nccl_amd.group_end()
+    torch.cuda.synchronize()
+    assert np.array_equal(red.numpy(), oracle.reduce(ins, 7, 0, 1)), "Reduce"
     assert all(c.async_error() == 0 for c in comms)
+
+
+@pytest.mark.parametrize("count", [(1 << 18) + 3, 3 << 20])
+def test_one_rank_copy_on_pinned_host_buffers(built, count):
+    """The one-rank path with a pinned host buffer on either side (the copy's grid is capped for PCIe at >= 1 MiB,
+    NCCL_AMD_HOST_COPY_GRID): host -> host, host -> device, device -> host, bit-exact."""
+    import torch
+    import nccl_amd
+    torch.cuda.set_device(0)
+    comm = nccl_amd.Communicator.init_all([0])[0]
+    try:
+        x = torch.randn(count).pin_memory()
+        st = torch.cuda.current_stream().cuda_stream
+        for src_dev, dst_dev in ((False, False), (False, True), (True, False)):
+            src = x.cuda() if src_dev else x
+            dst = torch.zeros(count, device="cuda") if dst_dev else torch.zeros(count).pin_memory()
+            torch.cuda.synchronize()
+            comm.all_reduce_raw(src.data_ptr(), dst.data_ptr(), count, 7, 0, st)
+            torch.cuda.synchronize()
+            assert torch.equal(dst.cpu(), x), (src_dev, dst_dev)
+    finally:
+        comm.destroy()
