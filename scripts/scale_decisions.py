@@ -7,7 +7,9 @@ one line per setting and N, with the medians and spreads they rest on:
 * CU budget: the default channel plan vs `NCCL_MAX_CTAS` 256 / 128 / 64 / 32;
 * eager zero-copy vs the staged default;
 * size table: `suite.size_table_row.file_line` (ready for an NCCL_AMD_SIZE_TABLE file);
-* LL128 class: torn 64-byte lines over a link (`suite.xgmi_probe.store_atomicity`).
+* LL128 class: torn 64-byte lines over a link (`suite.xgmi_probe.store_atomicity`);
+* host buffers: the collective on pinned host buffers (`host_staged.direct`) vs the best copy pipeline — whether
+  the staged kernel's channel count needs a PCIe-sized plan for host buffers (§11 item 3).
 
 A difference is called only when the two medians differ by more than both columns' spreads (max − min over the
 interleaved rounds); otherwise "within spread". usage: python scripts/scale_decisions.py FILE [FILE ...]"""
@@ -78,6 +80,11 @@ def decisions(line):
         out.append(f"  LL128 class: store atomicity over a link {json.dumps(atom)[:160]}")
     else:
         out.append("  LL128 class: no link measurement (ranks on one GPU, or the probe did not run)")
+    hs = line.get("host_staged", {})
+    if "direct" in hs and "pipelined" in hs:
+        d, p = hs["direct"], hs["pipelined"]
+        out.append(f"  host buffers: direct {d['ms_per_step']} ms ({d['check']}) vs pipelined {p['ms_per_step']} ms at "
+                   f"{p['chunks']} chunks ({p['check']}): {d.get('speedup_vs_pipelined')}x")
     return out
 
 
