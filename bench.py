@@ -600,13 +600,13 @@ def host_staged(comm, n: int, count: int, stream, dist) -> dict:
     ms_dev = max_over_ranks(dist, [ms_dev])[0]
     # pipelined: the bucket in chunks over three streams — H2D of chunk k+1, the AllReduce of chunk k and the D2H
     # of chunk k-1 overlap, so both PCIe directions stay busy at once (the reference's proxy pipelines its
-    # network-staged transfers the same way, src/proxy.cc:954-1012). 4 chunks: 6.6 ms vs 7.6 ms at 16 (per-copy
-    # cost) and 9.5 ms serial on the MI355X box (scripts/host_pipe_probe.py, profiles/r03_host_staged_pipeline.json)
+    # network-staged transfers the same way, src/proxy.cc:954-1012). 4 chunks 6.6 ms, 8 chunks 6.1-8.1 ms, 16 chunks
+    # 9.4-17 ms (the runtime blocks inside some chunk copies' enqueue), 9.5 ms serial on the MI355X box
     if os.environ.get("BENCH_HOST_STAGED_PIPE") == "0":  # diagnostics: the one-stream measurement only
         return {"bytes_per_rank": S, "ms_per_step": round(ms, 4), "algbw_GBps_incl_pcie": round(S / (ms * 1e-3) / 1e9, 2),
                 "device_resident_ms": round(ms_dev, 4)}
     # chunk counts timed in the same run: more chunks shorten the pipeline's fill and drain (one
-    # chunk's H2D before the first AllReduce, one chunk's D2H after the last) but pay each copy's fixed cost more often
+    # chunk's H2D before the first AllReduce, one chunk's D2H after the last) but enqueue more copies
     s_in, s_out = torch.cuda.Stream(), torch.cuda.Stream()
     ev_start, ev_end = torch.cuda.Event(), torch.cuda.Event()
 
