@@ -226,12 +226,15 @@ def main():
             if special:  # NaN / +-Inf / +-0 / subnormals / max-finite at every 37th element (oracle: NaN positions)
                 from tests.test_gpu_collectives import _with_specials
                 ins = _with_specials(G.make_inputs(n, dt, count, seed), dt)
-            errs = G.run_case(cs, coll, dt, op, count, mis, seed=seed, inplace=inplace, root=root, inputs=ins)
+            # pinned host buffers on some ranks (the kernels cross PCIe; eager registration falls back to the bounce)
+            host = [rng.random() < 0.5 for _ in range(n)] if rng.random() < 0.15 else False
+            errs = G.run_case(cs, coll, dt, op, count, mis, seed=seed, inplace=inplace, root=root, inputs=ins,
+                              host=host)
             total += 1
             done += 1
             if errs:
                 failures.append(f"n={n} env={env} {coll} dt={dt} op={op} count={count} mis={mis} inplace={inplace} "
-                                f"root={root} specials={special}: {errs[:3]}")
+                                f"root={root} specials={special} host={host}: {errs[:3]}")
                 break
         for c in comms:
             c.destroy()

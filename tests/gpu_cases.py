@@ -15,12 +15,16 @@ FLOAT_TYPES = {6, 7, 8, 9, 10, 11}
 
 
 def to_device(arr: np.ndarray, device, offset_elems: int = 0):
-    """Copy a numpy storage array to a fresh device buffer; `offset_elems` > 0 returns a view that is
-    deliberately NOT 16-byte aligned (exercises the reference's unaligned fallback)."""
+    """Copy a numpy storage array to a fresh device buffer (device "pinned": pinned host memory, which the kernels
+    reach across PCIe); `offset_elems` > 0 returns a view that is deliberately NOT 16-byte aligned (exercises the
+    reference's unaligned fallback)."""
     import torch
     raw = np.ascontiguousarray(arr).view(np.uint8)
     es = arr.dtype.itemsize
-    buf = torch.empty(raw.size + offset_elems * es + 64, dtype=torch.uint8, device=device)
+    if device == "pinned":
+        buf = torch.empty(raw.size + offset_elems * es + 64, dtype=torch.uint8, pin_memory=True)
+    else:
+        buf = torch.empty(raw.size + offset_elems * es + 64, dtype=torch.uint8, device=device)
     view = buf[offset_elems * es: offset_elems * es + raw.size]
     view.copy_(torch.from_numpy(raw.copy()))
     return buf, view
@@ -178,10 +182,11 @@ def case_list(n: int, quick: bool = False):
 
 
 def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=False, root=0, sync=True,
-             inputs=None, algo=""):
+             inputs=None, algo="", host=False):
     """Run one collective on every (comm, stream) of this process; returns list of error strings.
     `comms_and_streams` holds the ranks owned by this process: [(comm, torch stream), ...]; the
-    inputs of ALL ranks are regenerated deterministically so each process can check its own ranks."""
+    inputs of ALL ranks are regenerated deterministically so each process can check its own ranks.
+    `host` (a bool, or one per rank): that rank's buffers are pinned host memory."""
     import torch
     n = comms_and_streams[0][0].nranks
     if inputs is None:
@@ -197,7 +202,10 @@ def run_case(comms_and_streams, coll, dtype, op, count, misalign, seed, inplace=
         if per_rank is not None:  # each rank's buffers misaligned differently (protocol choice must not care)
             misalign = per_rank[r % len(per_rank)]
         dev = torch.device("cuda", comm.device)
+        on_host = host[r % len(host)] if isinstance(host, (list, tuple)) else host
         with torch.cuda.device(dev):
+            if on_host:
+                dev = "pinned"
             if inplace:
                 # one buffer: AR send==recv; RS recv = send + r*recvcount; AG send = recv + r*sendcount
                 if coll in ("allreduce", "reduce"):
