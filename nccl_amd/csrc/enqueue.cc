@@ -729,8 +729,8 @@ ncclResult_t planColl(const CollInfo& info, LaunchPlan& p, SymPlan& sp, int* kin
     p.copyVariant = comm->tune.copyVariant;
     p.copyGrid = comm->tune.copyGrid;
     p.copyXcdShift = comm->tune.copyXcdShift;
-    // one pointer query per copy of >= 1 MiB (about a microsecond, overlapped with the GPU's work)
-    if (comm->tune.hostCopyGrid > 0 && bytes >= (1u << 20) &&
+    // one pointer query per out-of-place copy of >= 1 MiB (about a microsecond, overlapped with the GPU's work)
+    if (comm->tune.hostCopyGrid > 0 && bytes >= (1u << 20) && info.sendbuff != info.recvbuff &&
         (isHostMemory(info.sendbuff) || isHostMemory(info.recvbuff)))
       p.copyGrid = std::min<int64_t>(p.copyGrid, comm->tune.hostCopyGrid);
     return ncclSuccess;
